@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s into the G-buffer at 1920x1080 depth 8 (BASELINE.json metric), MI355X.
+
+A "step" is one full deterministic frame of the hot path (ray generation + sphereflake traversal +
+G-buffer write, reference Sphereflake.h:86-226 / Sphereflake.cpp:149-201) over a 1920x1080 frame at
+the depth-8 camera (BASELINE configs[2]: main.cpp:92-96 camera position scaled by K = 0.25). The
+G-buffer stays resident in HBM (the D2H copy into the host GBuffer is timed separately and reported
+as `d2h_ms`, never as `value`).
+
+Multi-GPU (`--gpus N`, launched by torch.distributed.run): one process per GPU. The frames of a
+camera path are independent units, so each rank renders its own 1920x1080 depth-8 frame per step
+(frame index = step * N + rank); no data-path collective, `scaling: weak`. The row-banded single-frame
+mode with an RCCL gather to rank 0 is `--mode rows` (strong scaling, reported
+with and without the gather).
+
+rank 0 prints ONE JSON line. `roofline` prices the dominant kernel against HBM (32 B/ray of G-buffer
+stores); `cpu_baseline` times the reference's own AVX packet path (oracle/_ref,
+compiled from the reference sources) on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "sphereflake-raytracer_amd"))
+sys.path.insert(0, REPO)
+
+import sphereflake_amd as sf  # noqa: E402
+
+W, H, K = 1920, 1080, 0.25          # BASELINE configs[2]
+BYTES_PER_RAY = 32                  # two float4 G-buffer stores
+HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz (non-FMA fp32)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--mode", choices=["frames", "rows"], default="frames")
+    ap.add_argument("--kernel", choices=["wave", "ray"], default="wave")
+    ap.add_argument("--width", type=int, default=W)
+    ap.add_argument("--height", type=int, default=H)
+    ap.add_argument("--K", type=float, default=K)
+    ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--check", action="store_true", help="verify the frame against the oracle rows")
+    return ap.parse_args()
+
+
+def frame_camera(width, height, k, frame):
+    """Frame `frame` of the camera path: the config camera with yaw advanced 1 mrad per frame."""
+    cam = sf.config_camera(width, height, k)
+    cam.SetYaw(np.float32(sf.DEFAULT_YAW + 1e-3 * frame))
+    return cam
+
+
+def cpu_baseline(width, height, k, threads):
+    """The reference AVX packet path (oracle/_ref/ref_bench, built from /root/reference) on host cores.
+    Falls back to the oracle C restatement (per ray, 1 thread) if the reference build is absent."""
+    from oracle import pyoracle
+    ref = os.path.join(pyoracle.REF_DIR, "ref_bench")
+    if os.path.exists(ref):
+        r = pyoracle.ref_bench(width, height, k, threads, 5)
+        return {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
+                "sample": f"5 full {width}x{height} K={k} frames (reference 8-ray packet footprint, 8/9 pixel "
+                          f"coverage), median; reference AVX path -O3 -mavx, {threads} threads",
+                "frame_ms": round(r["median_s"] * 1e3, 2)}
+    setup = {"W": width, "H": height}
+    cam = sf.config_camera(width, height, k)
+    o, tl, tr, bl = cam.corners()
+    setup.update(origin=o, tl=tl, tr=tr, bl=bl, root=sf.root_transform(o), children=sf.child_transforms())
+    rows = np.arange(0, height, 8)
+    t0 = time.perf_counter()
+    pyoracle.render(setup, rows=rows, threads=1)
+    dt = time.perf_counter() - t0
+    return {"value": round(len(rows) * width / dt / 1e6, 3), "unit": "Mrays/s", "cores": 1, "kind": "port",
+            "sample": f"every 8th row of a {width}x{height} K={k} frame, oracle C restatement, 1 thread"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    dist_on = world > 1
+    if dist_on:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if dist_on else 0)
+    if not os.path.exists(sf.LIB_PATH):
+        if rank == 0:
+            sf.build()
+        if dist_on:
+            dist.barrier()
+    width, height = args.width, args.height
+    n = world
+    stream = torch.cuda.Stream(device=dev)
+    kernel = sf.SF_KERNEL_WAVE if args.kernel == "wave" else sf.SF_KERNEL_PER_RAY
+
+    ctx = sf.Sphereflake(width, height, device=dev.index)
+    sh = stream.cuda_stream
+
+    if args.mode == "frames":
+        views = [frame_camera(width, height, args.K, rank).corners()]   # frame index = rank
+        rays_per_step_rank = width * height
+        slab_rows = height
+    else:
+        cam = sf.config_camera(width, height, args.K)
+        ctx.SetCamera(cam)
+        slab_rows = sf.lib().sf_slab_rows(height, args.band_rows, n, rank)
+        rays_per_step_rank = slab_rows * width
+        slab_p = torch.empty((slab_rows, width, 4), dtype=torch.float32, device=dev)
+        slab_n = torch.empty_like(slab_p)
+        max_rows = max(sf.lib().sf_slab_rows(height, args.band_rows, n, r) for r in range(n))
+        gat_p = [torch.empty((max_rows, width, 4), dtype=torch.float32, device=dev) for _ in range(n)] if rank == 0 else None
+        send_p = torch.zeros((max_rows, width, 4), dtype=torch.float32, device=dev)
+
+    if args.mode == "frames":
+        o, tl, tr, bl = views[0]
+        ctx.SetView(o, tl, tr, bl)
+
+    ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+
+    def run_step(i, timed):
+        with torch.cuda.stream(stream):
+            if timed:
+                ev_s[i].record(stream)
+            if args.mode == "frames":
+                ctx.Render(kernel=kernel, stream=sh)
+            else:
+                ctx.render_to(slab_p.data_ptr(), slab_n.data_ptr(), band_rows=args.band_rows, band_count=n,
+                              band_index=rank, compact=True, kernel=kernel, stream=sh)
+            if timed:
+                ev_e[i].record(stream)
+            if args.mode == "rows" and dist_on:
+                send_p[:slab_rows].copy_(slab_p)
+                dist.gather(send_p, gat_p, dst=0)
+
+    for i in range(args.warmup):
+        run_step(i, False)
+    torch.cuda.synchronize(dev)
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        run_step(i, True)
+    torch.cuda.synchronize(dev)
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    st = ctx.stats()
+    if st.overflow_tiles:
+        raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
+    kern_ms = float(np.mean([ev_s[i].elapsed_time(ev_e[i]) for i in range(args.steps)]))
+
+    t_step = dt / args.steps
+    if dist_on:
+        tt = torch.tensor([t_step, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_step, kern_ms_max = float(tt[0]), float(tt[1])
+    else:
+        kern_ms_max = kern_ms
+    total_rays = rays_per_step_rank * n if args.mode == "frames" else width * height
+    value = total_rays / t_step / 1e6
+
+    # D2H into the host GBuffer (PCIe-inclusive frame rate, reported separately)
+    d2h_ms = None
+    if rank == 0 and args.mode == "frames":
+        t1 = time.perf_counter()
+        ctx.download()
+        d2h_ms = (time.perf_counter() - t1) * 1e3
+
+    check = None
+    if args.check and rank == 0 and args.mode == "frames":
+        from oracle import pyoracle
+        pos, nrm, _, _ = ctx.download()
+        o, tl, tr, bl = views[0]
+        setup = {"W": width, "H": height, "origin": o, "tl": tl, "tr": tr, "bl": bl,
+                 "root": sf.root_transform(o), "children": sf.child_transforms()}
+        rows = np.linspace(0, height - 1, 12).astype(int)
+        r = pyoracle.render(setup, rows=rows)
+        check = bool(np.array_equal(r["pos4"].view(np.uint32), pos[rows].view(np.uint32)) and
+                     np.array_equal(r["nrm4"].view(np.uint32), nrm[rows].view(np.uint32)))
+
+    if rank == 0:
+        per_launch_bytes = BYTES_PER_RAY * rays_per_step_rank
+        achieved = per_launch_bytes / (kern_ms_max * 1e-3) / 1e9
+        out = {
+            "metric": "Mrays/sec into G-buffer at 1920x1080 depth-8; frame time ms",
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_step * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if args.mode == "frames" else "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic fixed-camera frames; no dataset)",
+            "config": {"workload": f"{width}x{height} primary-ray G-buffer, depth-8 camera K={args.K} "
+                                   f"(BASELINE configs[2]), {args.kernel} kernel",
+                       "width": width, "height": height, "K": args.K, "max_depth": st.max_depth,
+                       "parallelism": f"frames x{n}" if args.mode == "frames" else f"row-bands x{n} + RCCL gather"},
+            "frame_ms": round(t_step * 1e3, 4),
+            "kernel_ms": round(kern_ms_max, 4),
+            "d2h_ms": round(d2h_ms, 3) if d2h_ms is not None else None,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "note": "path is VALU-bound (SURVEY.md §8(d)); achieved = 32 B/ray x rays per launch / "
+                                 "mean render time (trace + fixup kernels, HIP events on the launch stream)"},
+        }
+        if check is not None:
+            out["check_rows_bit_exact"] = check
+        if not args.no_cpu_baseline and n == 1:
+            thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+            try:
+                out["cpu_baseline"] = cpu_baseline(width, height, args.K, thr)
+            except Exception as e:  # never lose the GPU number over the baseline leg
+                out["cpu_baseline"] = {"error": str(e)}
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist_on:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

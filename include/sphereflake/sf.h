@@ -1,0 +1,187 @@
+/*
+ * sf.h -- C ABI of the MI355X (gfx950) Sphereflake primary-ray G-buffer renderer.
+ *
+ * This is the drop-in boundary for the reference hot path. The reference has no
+ * FFI: its boundary is the C++ class SphereflakeRaytracer::Sphereflake
+ * (/root/reference/sphereflake/Sphereflake.h:13-58). Each entry point below names
+ * the member of that class (or the reference code) it replaces; the C++ class of
+ * the same name and surface, layered on this ABI, is
+ * sphereflake-raytracer_amd/csrc/Sphereflake.hpp.
+ *
+ * Conventions
+ *   - Every call returns 0 on success and a negative SF_E* code on failure
+ *     (sf_strerror() names it). HIP runtime errors map to SF_EHIP; the HIP code
+ *     is kept in the context (sf_last_hip_error()).
+ *   - The caller owns host buffers; the context owns its device buffers.
+ *   - One context per device per host thread. Calls are stream-ordered on the
+ *     context stream (or params->stream); sf_download() synchronises.
+ *   - G-buffer layout is the reference's: float4 (x, y, z, 1) per pixel,
+ *     row-major x + y*W, y = 0 is the TOP edge (Sphereflake.cpp:186-196). Misses
+ *     are (0, 0, 0, 1), so the GL SSAO post-process consumes it unchanged
+ *     (Shaders/post_final.glsl:20, post_ssao.glsl:33).
+ *   - Arithmetic is IEEE binary32 reproducing the reference AVX path bit for bit
+ *     (per-ray semantics).
+ */
+#ifndef SPHEREFLAKE_SF_H
+#define SPHEREFLAKE_SF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SF_ABI_VERSION 1
+
+enum sf_status {
+    SF_OK = 0,
+    SF_EINVAL = -1,      /* bad argument (null pointer, zero size, out-of-range band) */
+    SF_ENOMEM = -2,      /* device or host allocation failed */
+    SF_EHIP = -3,        /* HIP runtime error (see sf_last_hip_error) */
+    SF_ENODEV = -4,      /* no such device / not a gfx950 device */
+    SF_ENOVIEW = -5,     /* sf_render before sf_set_view */
+    SF_EDEPTH = -6,      /* traversal exceeded SF_MAX_DEPTH_LIMIT levels */
+    SF_ESTATE = -7       /* call not valid in the current state (e.g. progressive mode running) */
+};
+
+/* Traversal kernels. */
+enum sf_kernel {
+    SF_KERNEL_WAVE = 0,      /* default: wave-coherent traversal, one 8x8 pixel tile per wave64,
+                                child transforms built cooperatively into LDS */
+    SF_KERNEL_PER_RAY = 1    /* one thread per ray, private traversal stack */
+};
+
+#define SF_MAX_DEPTH_LIMIT 31   /* traversal levels (expanding depths 0..30) the kernels support */
+
+typedef struct sf_ctx sf_ctx;
+
+/* Per-render options. Zero-initialise and set what you need. */
+typedef struct sf_render_params {
+    /* Row sharding for multi-GPU. The frame is cut into bands of
+       band_rows rows (must be a multiple of 8; 0 = one band = whole frame); this call
+       renders the bands b with b % band_count == band_index (band_count 0 or 1 = all). */
+    uint32_t band_rows;
+    uint32_t band_count;
+    uint32_t band_index;
+    /* 1: write only the owned bands, packed contiguously (a "slab": band k of this
+       rank at rows [k*band_rows, (k+1)*band_rows)); 0: write at frame positions. */
+    uint32_t compact;
+    uint32_t kernel;          /* enum sf_kernel */
+    uint32_t emit_aux;        /* 1: also write minT (float) and hit index (uint32) channels */
+    uint32_t max_depth;       /* traversal stack levels to provision (0 = auto: 12, retried at
+                                 SF_MAX_DEPTH_LIMIT if a tile needs more) */
+    uint32_t reserved;
+    void* stream;             /* hipStream_t to launch on; NULL = the context stream */
+} sf_render_params;
+
+/* Frame statistics; mirrors Sphereflake::GetMaxDepthReached / GetRaysPerSecond /
+   GetClosestSphereDistance (Sphereflake.h:30-58). Accumulated over renders until reset. */
+typedef struct sf_stats {
+    int32_t max_depth;        /* deepest node that passed bounding + LOD (Sphereflake.h:157-160) */
+    float closest;            /* min minT over rays (FLT_MAX if none; may be negative) */
+    int64_t rays;             /* rays traced */
+    int64_t overflow_tiles;   /* tiles re-rendered because they needed a deeper stack */
+} sf_stats;
+
+/* --- lifetime ------------------------------------------------------------ */
+
+/* Replaces Sphereflake::Sphereflake(width, height) (Sphereflake.cpp:43-55): allocates the
+   device G-buffer (2 x W*H float4, zeroed like glm's vec4() default) and the aux channels,
+   computes the 9 child transforms (ComputeChildTransformations, Sphereflake.cpp:216-249). */
+int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out);
+
+/* Replaces Sphereflake::~Sphereflake (Sphereflake.cpp:57-65). */
+void sf_destroy(sf_ctx* ctx);
+
+/* --- view and setup ------------------------------------------------------ */
+
+/* Replaces Sphereflake::SetView (Sphereflake.cpp:76-84): stores the ray origin and image-plane
+   corners; root transform = translate(-origin) * CreateRotationMatrix((90,0,0)). */
+int sf_set_view(sf_ctx* ctx, const float origin[3], const float top_left[3],
+                const float top_right[3], const float bottom_left[3]);
+
+/* Override the host-computed setup constants (root transform and 9 unit child frames,
+   glm column-major 4x4). For parity tests against fixture dumps. */
+int sf_set_setup(sf_ctx* ctx, const float child[9][16], const float root[16]);
+
+/* Read back the setup constants currently in use. */
+int sf_get_setup(const sf_ctx* ctx, float child[9][16], float root[16]);
+
+/* --- rendering ----------------------------------------------------------- */
+
+/* One full-frame (or banded) render into the context's device G-buffer. Replaces the
+   std::thread sampling loop Sphereflake::DoImagePart (Sphereflake.cpp:86-214) with a
+   deterministic frame. params may be NULL (defaults). Asynchronous on the stream. */
+int sf_render(sf_ctx* ctx, const sf_render_params* params);
+
+/* Same, into caller-owned DEVICE buffers (e.g. torch tensors): pos4/nrm4 are float4 arrays
+   of rows*W elements, where rows = H (compact = 0) or the slab height (compact = 1);
+   min_t / hit_index may be NULL. */
+int sf_render_to(sf_ctx* ctx, const sf_render_params* params, float* pos4, float* nrm4,
+                 float* min_t, uint32_t* hit_index);
+
+/* Rows of the slab a (band_rows, band_count, band_index) shard owns (compact layout). */
+uint32_t sf_slab_rows(uint32_t height, uint32_t band_rows, uint32_t band_count, uint32_t band_index);
+
+/* Replaces GetGBuffer() + the GL PBO upload source (Sphereflake.h:25-28,
+   GLPixelBufferObject.h:24-29): synchronous D2H copy of the context G-buffer into host
+   float4 arrays of W*H elements. Any pointer may be NULL to skip that channel. */
+int sf_download(sf_ctx* ctx, float* pos4, float* nrm4, float* min_t, uint32_t* hit_index);
+
+/* Device pointers of the context buffers (any out-pointer may be NULL). */
+int sf_device_buffers(sf_ctx* ctx, float** pos4, float** nrm4, float** min_t, uint32_t** hit_index);
+
+/* Block until all work on the context stream is done. */
+int sf_synchronize(sf_ctx* ctx);
+
+/* --- stats (Sphereflake.h:30-58) ---------------------------------------- */
+
+int sf_get_stats(sf_ctx* ctx, sf_stats* out);          /* synchronises */
+int sf_reset_max_depth(sf_ctx* ctx);                   /* ResetMaxDepthReached */
+int sf_reset_rays(sf_ctx* ctx);                        /* ResetRaysPerSecond */
+int sf_reset_closest(sf_ctx* ctx);                     /* ResetClosestSphereDistance */
+
+/* --- frame-less progressive mode (Initialize + DoImagePart, Sphereflake.cpp:67-74,86-214) --- */
+
+/* Trace `packets` random 8-ray packets into the context G-buffer, exactly as one reference
+   worker thread would: pixel pairs from Sobol dims 0/1 (Sobol.cpp:41-55) scrambled by an
+   mt19937 stream seeded with `seed` (std::uniform_int_distribution<unsigned>(0) draws),
+   packet footprint of Sphereflake.cpp:143-147, scatter of :186-201, sobol counter starting at
+   `counter0`. Packets are traced in parallel; later packets overwrite earlier ones at shared
+   pixels, as in the reference's sequential order. */
+int sf_progressive(sf_ctx* ctx, uint32_t seed, uint64_t counter0, uint32_t packets, void* stream);
+
+/* --- host setup helpers (reference host math, fixture-pinned) ------------ */
+
+/* Camera corners of reference camera.h:37-53 (FOV, quaternion from (yaw, pitch, roll),
+   aspect W/H, scaling tan(fov/2)/3). Angles in radians, fov in degrees. */
+int sf_camera_corners(uint32_t width, uint32_t height, const float position[3], float pitch,
+                      float yaw, float roll, float fov_deg, float origin[3], float top_left[3],
+                      float top_right[3], float bottom_left[3]);
+
+/* The 9 unit child frames of ComputeChildTransformations (Sphereflake.cpp:216-249). */
+int sf_child_transforms(float child[9][16]);
+
+/* Root transform of SetView (Sphereflake.cpp:83) for a ray origin. */
+int sf_root_transform(const float origin[3], float root[16]);
+
+/* Per-depth constants the kernels use: radius r_d (Sphereflake.h:97), and the exact float
+   threshold T_d with  sqrtf(t / r_d) < 70 || t < 0   <=>   t < T_d  (Sphereflake.h:146). */
+int sf_depth_constants(uint32_t depth, float* radius, float* lod_threshold);
+
+/* Reproduction of x86 rsqrtps (the table the kernels use). */
+float sf_rsqrtps(float x);
+
+/* --- misc ---------------------------------------------------------------- */
+
+const char* sf_strerror(int status);
+int sf_last_hip_error(const sf_ctx* ctx);
+int sf_abi_version(void);
+int sf_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SPHEREFLAKE_SF_H */

@@ -1,0 +1,108 @@
+// Sphereflake.cpp -- the reference-compatible C++ class over the C ABI (see Sphereflake.hpp).
+// Reference surface: /root/reference/sphereflake/Sphereflake.h:13-58, Sphereflake.cpp:43-84.
+#include "Sphereflake.hpp"
+
+#include <chrono>
+#include <ctime>
+
+namespace SphereflakeRaytracer {
+
+void Sphereflake::Check(int rc)
+{
+    if (rc != SF_OK) throw std::runtime_error(std::string("sphereflake: ") + sf_strerror(rc));
+}
+
+Sphereflake::Sphereflake(size_t width, size_t height, int device) : m_Width(width), m_Height(height)
+{
+    Check(sf_create(device, (uint32_t)width, (uint32_t)height, &m_Ctx));
+    // reference: m_GBuffer.positions/normals.resize(W*H) of zero vec4 (Sphereflake.cpp:48-49)
+    m_GBuffer.positions.resize(width * height);
+    m_GBuffer.normals.resize(width * height);
+}
+
+Sphereflake::~Sphereflake()
+{
+    m_Deinitialize = true;
+    if (m_Worker.joinable()) m_Worker.join();
+    sf_destroy(m_Ctx);
+}
+
+void Sphereflake::SetView(const sf_vec3& origin, const sf_vec3& topLeft, const sf_vec3& topRight, const sf_vec3& bottomLeft)
+{
+    std::lock_guard<std::mutex> lk(m_Mutex);
+    const float o[3] = { origin.x, origin.y, origin.z };
+    const float tl[3] = { topLeft.x, topLeft.y, topLeft.z };
+    const float tr[3] = { topRight.x, topRight.y, topRight.z };
+    const float bl[3] = { bottomLeft.x, bottomLeft.y, bottomLeft.z };
+    Check(sf_set_view(m_Ctx, o, tl, tr, bl));
+}
+
+void Sphereflake::Render(const sf_render_params* params)
+{
+    std::lock_guard<std::mutex> lk(m_Mutex);
+    Check(sf_render(m_Ctx, params));
+    m_Stale = true;
+}
+
+// Frame-less mode: like the reference's worker threads (seeded from time(NULL), Sphereflake.cpp:88-89),
+// a host thread keeps tracing batches of random packets into the persistent G-buffer.
+void Sphereflake::Initialize()
+{
+    if (m_Worker.joinable()) return;
+    m_Seed = (uint32_t)time(NULL);
+    m_Worker = std::thread([this] { ProgressiveLoop(); });
+}
+
+void Sphereflake::ProgressiveLoop()
+{
+    const uint32_t batch = 1u << 16;
+    while (!m_Deinitialize) {
+        {
+            std::lock_guard<std::mutex> lk(m_Mutex);
+            int rc = sf_progressive(m_Ctx, m_Seed, m_SobolCounter, batch, nullptr);
+            if (rc != SF_OK) return;
+            m_SobolCounter += batch;
+            m_Stale = true;
+        }
+        sf_synchronize(m_Ctx);
+    }
+}
+
+const GBuffer& Sphereflake::GetGBuffer() const
+{
+    std::lock_guard<std::mutex> lk(m_Mutex);
+    if (m_Stale) {
+        Check(sf_download(m_Ctx, &m_GBuffer.positions[0].x, &m_GBuffer.normals[0].x, nullptr, nullptr));
+        m_Stale = false;
+    }
+    return m_GBuffer;
+}
+
+int Sphereflake::GetMaxDepthReached() const
+{
+    sf_stats s;
+    Check(sf_get_stats(m_Ctx, &s));
+    return s.max_depth;
+}
+
+void Sphereflake::ResetMaxDepthReached() { Check(sf_reset_max_depth(m_Ctx)); }
+
+long long Sphereflake::GetRaysPerSecond() const
+{
+    sf_stats s;
+    Check(sf_get_stats(m_Ctx, &s));
+    return (long long)s.rays;
+}
+
+void Sphereflake::ResetRaysPerSecond() { Check(sf_reset_rays(m_Ctx)); }
+
+float Sphereflake::GetClosestSphereDistance() const
+{
+    sf_stats s;
+    Check(sf_get_stats(m_Ctx, &s));
+    return s.closest;
+}
+
+void Sphereflake::ResetClosestSphereDistance() { Check(sf_reset_closest(m_Ctx)); }
+
+}  // namespace SphereflakeRaytracer

@@ -1,0 +1,94 @@
+// Sphereflake.hpp -- drop-in replacement for the reference class
+// SphereflakeRaytracer::Sphereflake (/root/reference/sphereflake/Sphereflake.h:13-58), layered on
+// the C ABI (include/sphereflake/sf.h). Same names, argument meaning and stats semantics, plus a
+// synchronous Render(). The G-buffer keeps the reference layout (std::vector of vec4, row-major,
+// y = 0 top, misses (0,0,0,1)), so the reference's GL path (main.cpp:306-310 PBO upload, SSAO)
+// consumes it unchanged.
+//
+// vec3/vec4: when glm is included first (the reference app does, with GLM_FORCE_RADIANS), define
+// SF_USE_GLM and the class uses glm::vec3 / glm::vec4 exactly like the reference. Otherwise a
+// layout-identical POD is used.
+//
+// Differences, all deliberate:
+//   - Rendering is an explicit full frame: Render() traces every pixel once, deterministically.
+//     Initialize() keeps the reference's frame-less progressive mode (Sphereflake.cpp:67-74) on the
+//     device: a host thread keeps launching batches of random 8-ray packets until destruction.
+//   - GetGBuffer() downloads the device G-buffer (hipMemcpy D2H) when it is stale.
+//   - Errors throw std::runtime_error carrying sf_strerror() (the reference had no error path).
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <limits>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "sphereflake/sf.h"
+
+namespace SphereflakeRaytracer {
+
+#ifdef SF_USE_GLM
+using sf_vec3 = glm::vec3;
+using sf_vec4 = glm::vec4;
+#else
+struct sf_vec3 {
+    float x, y, z;
+    sf_vec3(float a = 0.f, float b = 0.f, float c = 0.f) : x(a), y(b), z(c) {}
+};
+struct sf_vec4 {
+    float x, y, z, w;
+    sf_vec4(float a = 0.f, float b = 0.f, float c = 0.f, float d = 0.f) : x(a), y(b), z(c), w(d) {}
+};
+#endif
+static_assert(sizeof(sf_vec4) == 16, "vec4 must be 4 packed floats");
+
+struct GBuffer {
+    std::vector<sf_vec4> positions;
+    std::vector<sf_vec4> normals;
+};
+
+class Sphereflake {
+public:
+    Sphereflake(size_t width, size_t height, int device = 0);
+    ~Sphereflake();
+    Sphereflake(const Sphereflake&) = delete;
+    Sphereflake& operator=(const Sphereflake&) = delete;
+
+    // Frame-less progressive mode (reference Initialize(), Sphereflake.cpp:67-74).
+    void Initialize();
+
+    void SetView(const sf_vec3& origin, const sf_vec3& topLeft, const sf_vec3& topRight, const sf_vec3& bottomLeft);
+
+    // One deterministic full frame into the device G-buffer (new; the reference renders implicitly).
+    void Render(const sf_render_params* params = nullptr);
+
+    const GBuffer& GetGBuffer() const;
+
+    int GetMaxDepthReached() const;
+    void ResetMaxDepthReached();
+    long long GetRaysPerSecond() const;   // rays traced since the last reset (reference semantics)
+    void ResetRaysPerSecond();
+    float GetClosestSphereDistance() const;
+    void ResetClosestSphereDistance();
+
+    sf_ctx* Context() const { return m_Ctx; }
+
+private:
+    static void Check(int rc);
+    void ProgressiveLoop();
+
+    size_t m_Width, m_Height;
+    sf_ctx* m_Ctx = nullptr;
+    mutable GBuffer m_GBuffer;
+    mutable bool m_Stale = true;
+    mutable std::mutex m_Mutex;
+    std::thread m_Worker;
+    std::atomic<bool> m_Deinitialize{ false };
+    uint64_t m_SobolCounter = 0;
+    uint32_t m_Seed = 0;
+};
+
+}  // namespace SphereflakeRaytracer

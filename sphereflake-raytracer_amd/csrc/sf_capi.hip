@@ -1,0 +1,543 @@
+// sf_capi.hip -- host side of the C ABI declared in include/sphereflake/sf.h.
+//
+// Owns the per-device context: device G-buffer (positions, normals as float4, reference layout
+// Sphereflake.h:7-11), optional aux channels (minT, hit index), the read-only constants block
+// (child frames, per-depth tables, rsqrtps table), stats words and the overflow tile list.
+// Launches are stream-ordered; nothing here synchronises except sf_download / sf_get_stats /
+// sf_synchronize.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+
+#include "sf_internal.h"
+#include "sphereflake/sf.h"
+
+extern "C" __global__ void sf_trace_wave(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
+extern "C" __global__ void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list, uint32_t* counters,
+                                         uint32_t parity);
+extern "C" __global__ void sf_trace_ray(FrameArgs a);
+extern "C" __global__ void sf_mt_draws(uint32_t* state, uint32_t* out, uint32_t n);
+extern "C" __global__ void sf_progressive_trace(FrameArgs a, const uint32_t* draws, uint64_t counter0, uint32_t packets,
+                                                uint64_t ticket0, PacketLane* lanes, unsigned long long* owner);
+extern "C" __global__ void sf_progressive_scatter(FrameArgs a, uint32_t packets, uint64_t ticket0,
+                                                  const PacketLane* lanes, const unsigned long long* owner);
+
+static const uint32_t kLut[2048] = {
+#include "rsqrtps_lut.inc"
+};
+
+namespace {
+
+constexpr uint32_t kDefaultLevels = 12;   // depths 0..11 expand; every BASELINE camera stays <= 10
+
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DevGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+struct sf_ctx {
+    int device = 0;
+    uint32_t W = 0, H = 0;
+    hipStream_t stream = nullptr;
+    float* pos = nullptr;
+    float* nrm = nullptr;
+    float* min_t = nullptr;
+    uint32_t* hit_index = nullptr;
+    int32_t* stats = nullptr;          // [0] max depth, [1] closest key, [2] unrecoverable overflow
+    uint32_t* ovf_counters = nullptr;  // [2], alternating per render
+    uint32_t* ovf_list = nullptr;      // tiles_x * tiles_y entries
+    DeviceConsts* consts = nullptr;
+    DeviceConsts host_consts;
+    float child[9][16];
+    float root[16];
+    float o[3], tl[3], tr[3], bl[3];
+    bool has_view = false;
+    uint32_t parity = 0;
+    int64_t rays = 0;
+    int last_hip = 0;
+    int fixup_blocks = 256;
+    // frame-less progressive mode
+    uint32_t* mt_state = nullptr;      // 624 words + next index (std::mt19937 layout)
+    uint32_t* draws = nullptr;         // 2 per packet
+    PacketLane* lanes = nullptr;       // 8 per packet
+    uint32_t prog_cap = 0;             // packets the scratch buffers hold
+    unsigned long long* owner = nullptr;   // per pixel: highest ticket written
+    bool prog_seeded = false;
+    uint32_t prog_seed = 0;
+    uint64_t prog_next = 0;            // Sobol counter the device MT stream is positioned at
+    uint64_t ticket = 1;
+};
+
+#define SF_HIP(ctx, expr)                                        \
+    do {                                                         \
+        hipError_t e_ = (expr);                                  \
+        if (e_ != hipSuccess) {                                  \
+            if (ctx) (ctx)->last_hip = (int)e_;                  \
+            return SF_EHIP;                                      \
+        }                                                        \
+    } while (0)
+
+static void free_ctx(sf_ctx* c)
+{
+    if (!c) return;
+    DevGuard g(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(c->pos);
+    (void)hipFree(c->nrm);
+    (void)hipFree(c->min_t);
+    (void)hipFree(c->hit_index);
+    (void)hipFree(c->stats);
+    (void)hipFree(c->ovf_counters);
+    (void)hipFree(c->ovf_list);
+    (void)hipFree(c->consts);
+    (void)hipFree(c->mt_state);
+    (void)hipFree(c->draws);
+    (void)hipFree(c->lanes);
+    (void)hipFree(c->owner);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+static int upload_consts(sf_ctx* c)
+{
+    std::memcpy(c->host_consts.child, c->child, sizeof c->child);
+    sfhost::depth_tables(&c->host_consts.dt);
+    std::memcpy(c->host_consts.lut, kLut, sizeof kLut);
+    sfhost::sobol_matrices(c->host_consts.sobol);
+    SF_HIP(c, hipMemcpyAsync(c->consts, &c->host_consts, sizeof(DeviceConsts), hipMemcpyHostToDevice, c->stream));
+    SF_HIP(c, hipStreamSynchronize(c->stream));
+    return SF_OK;
+}
+
+static int reset_stats_dev(sf_ctx* c, int which)
+{
+    // which: bit0 max depth, bit1 closest
+    int32_t init[2] = { -1, sf_float_key(FLT_MAX) };
+    if (which & 1) SF_HIP(c, hipMemcpyAsync(c->stats + 0, &init[0], 4, hipMemcpyHostToDevice, c->stream));
+    if (which & 2) SF_HIP(c, hipMemcpyAsync(c->stats + 1, &init[1], 4, hipMemcpyHostToDevice, c->stream));
+    SF_HIP(c, hipStreamSynchronize(c->stream));
+    return SF_OK;
+}
+
+extern "C" {
+
+int sf_abi_version(void) { return SF_ABI_VERSION; }
+
+int sf_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* sf_strerror(int s)
+{
+    switch (s) {
+    case SF_OK: return "ok";
+    case SF_EINVAL: return "invalid argument";
+    case SF_ENOMEM: return "out of memory";
+    case SF_EHIP: return "HIP runtime error";
+    case SF_ENODEV: return "no such device or not a gfx950 (MI355X) device";
+    case SF_ENOVIEW: return "render before SetView";
+    case SF_EDEPTH: return "traversal deeper than SF_MAX_DEPTH_LIMIT";
+    case SF_ESTATE: return "invalid state";
+    default: return "unknown error";
+    }
+}
+
+int sf_last_hip_error(const sf_ctx* ctx) { return ctx ? ctx->last_hip : 0; }
+
+int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
+{
+    if (!out || width == 0 || height == 0) return SF_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return SF_ENODEV;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SF_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SF_ENODEV;
+
+    sf_ctx* c = new (std::nothrow) sf_ctx();
+    if (!c) return SF_ENOMEM;
+    c->device = device;
+    c->W = width;
+    c->H = height;
+    c->fixup_blocks = prop.multiProcessorCount;
+    DevGuard g(device);
+    const size_t npx = (size_t)width * height;
+    const size_t ntiles = (size_t)((width + 7) / 8) * ((height + 7) / 8);
+    auto fail = [&](hipError_t e) {
+        c->last_hip = (int)e;
+        free_ctx(c);
+        return e == hipErrorOutOfMemory ? SF_ENOMEM : SF_EHIP;
+    };
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->pos, npx * 16)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->nrm, npx * 16)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->min_t, npx * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->hit_index, npx * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->stats, 16)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->ovf_counters, 8)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->ovf_list, ntiles * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->consts, sizeof(DeviceConsts))) != hipSuccess) return fail(e);
+    // G-buffer starts as glm vec4() = (0,0,0,0) (Sphereflake.cpp:48-49, type_vec4.inl:59-64)
+    if ((e = hipMemsetAsync(c->pos, 0, npx * 16, c->stream)) != hipSuccess) return fail(e);
+    if ((e = hipMemsetAsync(c->nrm, 0, npx * 16, c->stream)) != hipSuccess) return fail(e);
+    if ((e = hipMemsetAsync(c->min_t, 0, npx * 4, c->stream)) != hipSuccess) return fail(e);
+    if ((e = hipMemsetAsync(c->hit_index, 0xff, npx * 4, c->stream)) != hipSuccess) return fail(e);
+    if ((e = hipMemsetAsync(c->stats, 0, 16, c->stream)) != hipSuccess) return fail(e);
+    if ((e = hipMemsetAsync(c->ovf_counters, 0, 8, c->stream)) != hipSuccess) return fail(e);
+    sfhost::child_transforms(c->child);
+    int rc = upload_consts(c);
+    if (rc == SF_OK) rc = reset_stats_dev(c, 3);
+    if (rc != SF_OK) {
+        free_ctx(c);
+        return rc;
+    }
+    *out = c;
+    return SF_OK;
+}
+
+void sf_destroy(sf_ctx* ctx) { free_ctx(ctx); }
+
+int sf_set_view(sf_ctx* c, const float origin[3], const float tl[3], const float tr[3], const float bl[3])
+{
+    if (!c || !origin || !tl || !tr || !bl) return SF_EINVAL;
+    std::memcpy(c->o, origin, 12);
+    std::memcpy(c->tl, tl, 12);
+    std::memcpy(c->tr, tr, 12);
+    std::memcpy(c->bl, bl, 12);
+    sfhost::root_transform(origin, c->root);
+    c->has_view = true;
+    return SF_OK;
+}
+
+int sf_set_setup(sf_ctx* c, const float child[9][16], const float root[16])
+{
+    if (!c || !child || !root) return SF_EINVAL;
+    DevGuard g(c->device);
+    std::memcpy(c->child, child, sizeof c->child);
+    std::memcpy(c->root, root, sizeof c->root);
+    return upload_consts(c);
+}
+
+int sf_get_setup(const sf_ctx* c, float child[9][16], float root[16])
+{
+    if (!c) return SF_EINVAL;
+    if (child) std::memcpy(child, c->child, sizeof c->child);
+    if (root) std::memcpy(root, c->root, sizeof c->root);
+    return SF_OK;
+}
+
+uint32_t sf_slab_rows(uint32_t height, uint32_t band_rows, uint32_t band_count, uint32_t band_index)
+{
+    if (band_rows == 0) band_rows = ((height + 7) / 8) * 8;
+    if (band_count == 0) band_count = 1;
+    uint32_t bands = (height + band_rows - 1) / band_rows, rows = 0;
+    for (uint32_t b = band_index; b < bands; b += band_count) {
+        uint32_t y0 = b * band_rows, y1 = y0 + band_rows < height ? y0 + band_rows : height;
+        rows += y1 - y0;
+    }
+    return rows;
+}
+
+static FrameArgs frame_args(const sf_ctx* c)
+{
+    FrameArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.W = c->W;
+    a.H = c->H;
+    a.fw = (float)c->W;                  // (float)m_Width (Sphereflake.cpp:104-110)
+    a.fh = (float)c->H;
+    for (int k = 0; k < 3; ++k) {
+        a.o[k] = c->o[k];
+        a.tl[k] = c->tl[k];
+        a.dh[k] = c->tr[k] - c->tl[k];   // m_TopRight - m_TopLeft (Sphereflake.cpp:162)
+        a.dv[k] = c->bl[k] - c->tl[k];   // m_BottomLeft - m_TopLeft (Sphereflake.cpp:163)
+    }
+    for (int col = 0; col < 4; ++col)
+        for (int r = 0; r < 3; ++r) a.root[3 * col + r] = c->root[4 * col + r];
+    a.tiles_x = (c->W + 7) / 8;
+    a.band_count = 1;
+    a.consts = c->consts;
+    a.stats = c->stats;
+    return a;
+}
+
+static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm, float* min_t, uint32_t* hidx)
+{
+    if (!c) return SF_EINVAL;
+    if (!c->has_view) return SF_ENOVIEW;
+    if (!pos || !nrm) return SF_EINVAL;
+    sf_render_params p;
+    std::memset(&p, 0, sizeof p);
+    if (pp) p = *pp;
+    const uint32_t tiles_y = (c->H + 7) / 8;
+    uint32_t band_rows = p.band_rows ? p.band_rows : tiles_y * 8;
+    uint32_t band_count = p.band_count ? p.band_count : 1;
+    if (band_rows % 8 != 0 || p.band_index >= band_count) return SF_EINVAL;
+    if (p.kernel > SF_KERNEL_PER_RAY || p.max_depth > SF_MAX_DEPTH_LIMIT) return SF_EINVAL;
+    const uint32_t tpb = band_rows / 8;
+    const uint32_t bands = (tiles_y + tpb - 1) / tpb;
+    // owned tile rows: full bands for all but possibly the frame's last band
+    uint32_t tile_rows = 0;
+    for (uint32_t b = p.band_index; b < bands; b += band_count) {
+        uint32_t t0 = b * tpb, t1 = t0 + tpb < tiles_y ? t0 + tpb : tiles_y;
+        tile_rows += t1 - t0;
+    }
+    hipStream_t s = p.stream ? (hipStream_t)p.stream : c->stream;
+    DevGuard g(c->device);
+    if (tile_rows == 0) return SF_OK;
+
+    FrameArgs a = frame_args(c);
+    a.tile_rows = tile_rows;
+    a.tiles_per_band = tpb;
+    a.band_count = band_count;
+    a.band_index = p.band_index;
+    a.compact = p.compact ? 1u : 0u;
+    a.emit_aux = p.emit_aux ? 1u : 0u;
+    a.pos = pos;
+    a.nrm = nrm;
+    a.min_t = min_t;
+    a.hit_index = hidx;
+
+    const uint32_t ntiles = a.tiles_x * tile_rows;
+    const uint32_t blocks = (ntiles + SF_WAVES_PER_BLOCK - 1) / SF_WAVES_PER_BLOCK;
+    if (p.kernel == SF_KERNEL_PER_RAY) {
+        a.max_depth = 31;
+        hipLaunchKernelGGL(sf_trace_ray, dim3(blocks), dim3(256), 0, s, a);
+        SF_HIP(c, hipGetLastError());
+    } else {
+        const bool autod = p.max_depth == 0;
+        a.max_depth = autod ? kDefaultLevels : p.max_depth;
+        const size_t lds = (size_t)SF_WAVES_PER_BLOCK * (SF_LDS_ROOT + a.max_depth * SF_LDS_LEVEL) * 4;
+        uint32_t* cnt = c->ovf_counters + c->parity;
+        hipLaunchKernelGGL(sf_trace_wave, dim3(blocks), dim3(256), lds, s, a, c->ovf_list, cnt);
+        SF_HIP(c, hipGetLastError());
+        const size_t lds_fix = (size_t)SF_WAVES_PER_BLOCK * (SF_LDS_ROOT + 31 * SF_LDS_LEVEL) * 4;
+        hipLaunchKernelGGL(sf_fixup_wave, dim3(c->fixup_blocks), dim3(256), lds_fix, s, a,
+                           (const uint32_t*)c->ovf_list, c->ovf_counters, c->parity);
+        SF_HIP(c, hipGetLastError());
+        c->parity ^= 1u;
+    }
+    uint32_t rows = 0;
+    for (uint32_t b = p.band_index; b < bands; b += band_count) {
+        uint32_t y0 = b * band_rows, y1 = y0 + band_rows < c->H ? y0 + band_rows : c->H;
+        rows += y1 - y0;
+    }
+    c->rays += (int64_t)rows * c->W;
+    return SF_OK;
+}
+
+int sf_render(sf_ctx* c, const sf_render_params* p)
+{
+    if (!c) return SF_EINVAL;
+    return launch(c, p, c->pos, c->nrm, c->min_t, c->hit_index);
+}
+
+int sf_render_to(sf_ctx* c, const sf_render_params* p, float* pos4, float* nrm4, float* min_t, uint32_t* hidx)
+{
+    return launch(c, p, pos4, nrm4, min_t, hidx);
+}
+
+// Frame-less progressive mode (Sphereflake.cpp:67-74, 86-214). The device MT stream is kept in the
+// context; a call that does not continue where the previous one stopped (other seed or counter)
+// reseeds and skips ahead by generating and discarding 2 * counter0 draws.
+int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets, void* stream)
+{
+    if (!c) return SF_EINVAL;
+    if (!c->has_view) return SF_ENOVIEW;
+    if (c->W < 3 || c->H < 3) return SF_EINVAL;   // the reference samples x0 in [1, W-2]
+    if (packets == 0) return SF_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    DevGuard g(c->device);
+    if (!c->mt_state) {
+        SF_HIP(c, hipMalloc(&c->mt_state, 625 * 4));
+        SF_HIP(c, hipMalloc(&c->owner, (size_t)c->W * c->H * 8));
+        SF_HIP(c, hipMemsetAsync(c->owner, 0, (size_t)c->W * c->H * 8, s));
+    }
+    if (packets > c->prog_cap) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(c->draws);
+        (void)hipFree(c->lanes);
+        c->draws = nullptr;
+        c->lanes = nullptr;
+        c->prog_cap = 0;
+        SF_HIP(c, hipMalloc(&c->draws, (size_t)packets * 2 * 4));
+        SF_HIP(c, hipMalloc(&c->lanes, (size_t)packets * 8 * sizeof(PacketLane)));
+        c->prog_cap = packets;
+    }
+    if (!c->prog_seeded || seed != c->prog_seed || counter0 != c->prog_next) {
+        uint32_t st[625];
+        sfhost::mt19937_seed(seed, st);
+        SF_HIP(c, hipMemcpyAsync(c->mt_state, st, sizeof st, hipMemcpyHostToDevice, s));
+        SF_HIP(c, hipStreamSynchronize(s));
+        uint64_t skip = 2 * counter0;
+        while (skip > 0) {
+            uint32_t n = (uint32_t)(skip < 2ull * c->prog_cap ? skip : 2ull * c->prog_cap);
+            hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(1024), 0, s, c->mt_state, c->draws, n);
+            SF_HIP(c, hipGetLastError());
+            skip -= n;
+        }
+        c->prog_seeded = true;
+        c->prog_seed = seed;
+    }
+    FrameArgs a = frame_args(c);
+    a.pos = c->pos;
+    a.nrm = c->nrm;
+    a.min_t = c->min_t;
+    a.emit_aux = 1;
+    hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(1024), 0, s, c->mt_state, c->draws, 2 * packets);
+    SF_HIP(c, hipGetLastError());
+    const uint32_t waves = (packets + 7) / 8;
+    const uint32_t blocks = (waves + SF_WAVES_PER_BLOCK - 1) / SF_WAVES_PER_BLOCK;
+    const size_t lds = (size_t)SF_WAVES_PER_BLOCK * (SF_LDS_ROOT + 16 * SF_LDS_LEVEL) * 4;
+    hipLaunchKernelGGL(sf_progressive_trace, dim3(blocks), dim3(256), lds, s, a, (const uint32_t*)c->draws, counter0,
+                       packets, c->ticket, c->lanes, c->owner);
+    SF_HIP(c, hipGetLastError());
+    hipLaunchKernelGGL(sf_progressive_scatter, dim3((packets * 8 + 255) / 256), dim3(256), 0, s, a, packets, c->ticket,
+                       (const PacketLane*)c->lanes, (const unsigned long long*)c->owner);
+    SF_HIP(c, hipGetLastError());
+    c->ticket += packets;
+    c->prog_next = counter0 + packets;
+    c->rays += 8 * (int64_t)packets;                 // m_RaysPerSecond += 8 (Sphereflake.cpp:184)
+    return SF_OK;
+}
+
+int sf_synchronize(sf_ctx* c)
+{
+    if (!c) return SF_EINVAL;
+    DevGuard g(c->device);
+    SF_HIP(c, hipStreamSynchronize(c->stream));
+    int32_t st[3];
+    SF_HIP(c, hipMemcpy(st, c->stats, 12, hipMemcpyDeviceToHost));
+    if (st[2] != 0) return SF_EDEPTH;
+    return SF_OK;
+}
+
+int sf_download(sf_ctx* c, float* pos4, float* nrm4, float* min_t, uint32_t* hidx)
+{
+    if (!c) return SF_EINVAL;
+    int rc = sf_synchronize(c);
+    if (rc != SF_OK) return rc;
+    DevGuard g(c->device);
+    const size_t npx = (size_t)c->W * c->H;
+    if (pos4) SF_HIP(c, hipMemcpy(pos4, c->pos, npx * 16, hipMemcpyDeviceToHost));
+    if (nrm4) SF_HIP(c, hipMemcpy(nrm4, c->nrm, npx * 16, hipMemcpyDeviceToHost));
+    if (min_t) SF_HIP(c, hipMemcpy(min_t, c->min_t, npx * 4, hipMemcpyDeviceToHost));
+    if (hidx) SF_HIP(c, hipMemcpy(hidx, c->hit_index, npx * 4, hipMemcpyDeviceToHost));
+    return SF_OK;
+}
+
+int sf_device_buffers(sf_ctx* c, float** pos4, float** nrm4, float** min_t, uint32_t** hidx)
+{
+    if (!c) return SF_EINVAL;
+    if (pos4) *pos4 = c->pos;
+    if (nrm4) *nrm4 = c->nrm;
+    if (min_t) *min_t = c->min_t;
+    if (hidx) *hidx = c->hit_index;
+    return SF_OK;
+}
+
+int sf_get_stats(sf_ctx* c, sf_stats* out)
+{
+    if (!c || !out) return SF_EINVAL;
+    DevGuard g(c->device);
+    SF_HIP(c, hipStreamSynchronize(c->stream));
+    int32_t st[3];
+    SF_HIP(c, hipMemcpy(st, c->stats, 12, hipMemcpyDeviceToHost));
+    out->max_depth = st[0] < 0 ? 0 : st[0];
+    out->closest = sf_key_float(st[1]);
+    out->rays = c->rays;
+    out->overflow_tiles = st[2];
+    return SF_OK;
+}
+
+int sf_reset_max_depth(sf_ctx* c)
+{
+    if (!c) return SF_EINVAL;
+    DevGuard g(c->device);
+    return reset_stats_dev(c, 1);
+}
+
+int sf_reset_rays(sf_ctx* c)
+{
+    if (!c) return SF_EINVAL;
+    c->rays = 0;
+    return SF_OK;
+}
+
+int sf_reset_closest(sf_ctx* c)
+{
+    if (!c) return SF_EINVAL;
+    DevGuard g(c->device);
+    return reset_stats_dev(c, 2);
+}
+
+int sf_camera_corners(uint32_t W, uint32_t H, const float pos[3], float pitch, float yaw, float roll, float fov,
+                      float o[3], float tl[3], float tr[3], float bl[3])
+{
+    if (!W || !H || !pos || !o || !tl || !tr || !bl) return SF_EINVAL;
+    sfhost::camera_corners(W, H, pos, pitch, yaw, roll, fov, o, tl, tr, bl);
+    return SF_OK;
+}
+
+int sf_child_transforms(float child[9][16])
+{
+    if (!child) return SF_EINVAL;
+    sfhost::child_transforms(child);
+    return SF_OK;
+}
+
+int sf_root_transform(const float origin[3], float root[16])
+{
+    if (!origin || !root) return SF_EINVAL;
+    sfhost::root_transform(origin, root);
+    return SF_OK;
+}
+
+int sf_depth_constants(uint32_t depth, float* radius, float* lod)
+{
+    if (depth >= SF_DEPTH_TABLE) return SF_EINVAL;
+    float r = sfhost::radius(depth);
+    if (radius) *radius = r;
+    if (lod) *lod = sfhost::lod_threshold(r);
+    return SF_OK;
+}
+
+float sf_rsqrtps(float x)
+{
+    uint32_t b;
+    std::memcpy(&b, &x, 4);
+    uint32_t E = (b >> 23) & 0xffu;
+    uint32_t r;
+    if ((b & 0x7fffffffu) > 0x7f800000u) r = b | 0x00400000u;
+    else if (E == 0u) r = (b & 0x80000000u) | 0x7f800000u;
+    else if (b & 0x80000000u) r = 0xffc00000u;
+    else if (E == 0xffu) r = 0u;
+    else {
+        uint32_t key = ((E & 1u) << 10) | ((b & 0x7fffffu) >> 13);
+        int32_t E0 = (E & 1u) ? 127 : 128;
+        int32_t k = ((int32_t)E - E0) / 2;
+        r = (uint32_t)((int32_t)kLut[key] - k * (1 << 23));
+    }
+    float f;
+    std::memcpy(&f, &r, 4);
+    return f;
+}
+
+}  // extern "C"

@@ -1,0 +1,85 @@
+// sf_internal.h -- structures shared by the C ABI layer (sf_capi.hip), the host setup math
+// (sf_setup.cpp, g++) and the gfx950 kernels (sf_kernels.hip). Not installed.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define SF_HD __host__ __device__
+#else
+#define SF_HD
+#endif
+
+#define SF_DEPTH_TABLE 33      // depths 0..32 (SF_MAX_DEPTH_LIMIT)
+#define SF_TILE 8              // a wave64 traces one 8x8 pixel tile
+#define SF_WAVES_PER_BLOCK 4   // 256-thread workgroups
+#define SF_LDS_ROOT 16         // floats reserved per wave for the root transform
+#define SF_LDS_LEVEL 108       // floats per traversal level: 9 children x 12 (3x4 column-major)
+
+struct DepthTables {
+    float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)
+    float r2_self[SF_DEPTH_TABLE];    // r_d^2      node's own sphere (Sphereflake.h:180)
+    float scale[SF_DEPTH_TABLE];      // (4/3) r_d  child translation scale (Sphereflake.h:162)
+    float lod[SF_DEPTH_TABLE];        // T_d: sqrtf(t/r_d) < 70 || t < 0  <=>  t < T_d (Sphereflake.h:146)
+};
+
+// Per-context read-only device block (global memory; lane-indexed reads hit L1/L2).
+struct DeviceConsts {
+    float child[9][16];               // unit child frames, glm column-major (Sphereflake.cpp:216-249)
+    DepthTables dt;
+    uint32_t lut[2048];               // x86 rsqrtps table (rsqrtps_lut.inc)
+    uint32_t sobol[2][52];            // Sobol direction numbers, dims 0 and 1 (Sobol.cpp:34-39, 57-162)
+};
+
+// Frame-less progressive mode: one traced packet lane (staged between trace and scatter).
+struct PacketLane {
+    float px, py, pz, nx, ny, nz, min_t;
+    uint32_t pixel;                   // x + y*W (Sphereflake.cpp:188), 0xffffffff = skipped
+};
+
+// Everything a launch needs, passed by value as the kernel argument.
+struct FrameArgs {
+    uint32_t W, H;
+    float fw, fh;                     // (float)W, (float)H  (Sphereflake.cpp:104-110)
+    float o[3], tl[3], dh[3], dv[3];  // origin, top-left, TR-TL, BL-TL (Sphereflake.cpp:162-166)
+    float root[12];                   // root transform columns 0..3, xyz (Sphereflake.cpp:83)
+    uint32_t tiles_x;                 // ceil(W / 8)
+    uint32_t tile_rows;               // tile rows this launch renders
+    uint32_t tiles_per_band;          // band_rows / 8
+    uint32_t band_count, band_index;
+    uint32_t compact;                 // write rows packed into the shard's slab
+    uint32_t max_depth;               // traversal levels provisioned (<= SF_MAX_DEPTH_LIMIT)
+    uint32_t emit_aux;
+    const DeviceConsts* consts;
+    float* pos;                       // G-buffer positions (float4 x,y,z,1 per pixel)
+    float* nrm;                       // G-buffer normals
+    float* min_t;                     // optional aux channel
+    uint32_t* hit_index;              // optional aux channel (heap index 9n+1+i, 0xffffffff = miss)
+    int32_t* stats;                   // [0] max depth (atomicMax), [1] closest key (atomicMin), [2] overflow count
+};
+
+namespace sfhost {
+void child_transforms(float child[9][16]);
+void root_transform(const float origin[3], float root[16]);
+void camera_corners(uint32_t W, uint32_t H, const float pos[3], float pitch, float yaw, float roll,
+                    float fov, float o[3], float tl[3], float tr[3], float bl[3]);
+float radius(uint32_t depth);
+float lod_threshold(float r);
+void depth_tables(DepthTables* t);
+void sobol_matrices(uint32_t out[2][52]);
+void mt19937_seed(uint32_t seed, uint32_t state[625]);
+}  // namespace sfhost
+
+// Order-preserving map float <-> int32 for atomicMin on floats (negative values included).
+SF_HD static inline int32_t sf_float_key(float f)
+{
+    union { float f; int32_t i; } u;
+    u.f = f;
+    return u.i >= 0 ? u.i : (int32_t)(u.i ^ 0x7fffffff);
+}
+SF_HD static inline float sf_key_float(int32_t k)
+{
+    union { float f; int32_t i; } u;
+    u.i = k >= 0 ? k : (int32_t)(k ^ 0x7fffffff);
+    return u.f;
+}

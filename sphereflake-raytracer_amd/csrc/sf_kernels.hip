@@ -1,0 +1,637 @@
+// sf_kernels.hip -- gfx950 (CDNA4) kernels of the Sphereflake primary-ray G-buffer renderer.
+//
+// Hot path replaced (reference paths relative to /root/reference):
+//   ray generation           sphereflake/Sphereflake.cpp:149-150,162-167
+//   recursive traversal      sphereflake/Sphereflake.h:86-226 (IntersectSphereflake)
+//   packet math              sphereflake/SIMD_AVX.h:59-81 (4x4 product), 163-180 (Dot/Normalize),
+//                            236-270 (RaySphereIntersection)
+//   G-buffer scatter         sphereflake/Sphereflake.cpp:186-201
+//   frame-less sampler       sphereflake/Sphereflake.cpp:86-214, Sobol.cpp:41-55
+//
+// Numerics: IEEE binary32, the reference's exact operation order, contraction OFF (this file
+// and the compile line), correctly rounded division and sqrt (HIP default), denormals kept,
+// x86 rsqrtps reproduced from a table. Full frames equal the reference AVX path bit for bit
+// under per-ray semantics; the progressive mode reproduces the reference's
+// 8-ray packet semantics (packet-wide early-outs, Sphereflake.h:140-153, 207-211,
+// SIMD_AVX.h:247-258) bit for bit.
+//
+// Kernels
+//   sf_trace_wave   -- default full-frame kernel. One wave64 traces one 8x8 pixel tile. The DFS
+//                      over the sphereflake is wave-uniform: a node is visited iff at least one
+//                      lane of the tile visits it; each lane carries its own "active" bit per
+//                      level, so every lane sees exactly its per-ray visit sequence. When a node
+//                      expands, the 64 lanes build its 9 child transforms cooperatively (108
+//                      matrix entries, 2 per lane) into the wave's LDS level, instead of every
+//                      ray doing 9 4x4 products per node as the reference packets do.
+//   sf_fixup_wave   -- re-traces the tiles sf_trace_wave flagged as needing more LDS levels than
+//                      provisioned, with SF_MAX_LEVELS levels.
+//   sf_trace_ray    -- one thread per ray with a private traversal stack (the straightforward
+//                      formulation; cross-check and comparison point).
+//   sf_mt_draws / sf_progressive_trace / sf_progressive_scatter -- frame-less progressive mode.
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdint.h>
+
+#include "sf_internal.h"
+
+#pragma clang fp contract(off)
+
+#define SF_MAX_LEVELS 31         // SF_MAX_DEPTH_LIMIT (ebits is 32 bits)
+#define SF_PROGRESSIVE_LEVELS 16
+
+namespace {
+
+// x86 rsqrtps (SIMD_AVX.h:173), reproduced exactly from the measured table.
+__device__ __forceinline__ float rsqrtps_x86(float x, const uint32_t* __restrict__ lut)
+{
+    const uint32_t b = __float_as_uint(x);
+    const uint32_t E = (b >> 23) & 0xffu;
+    const uint32_t key = ((E & 1u) << 10) | ((b & 0x7fffffu) >> 13);
+    const int32_t E0 = (E & 1u) ? 127 : 128;
+    const int32_t k = ((int32_t)E - E0) / 2;
+    uint32_t r = (uint32_t)((int32_t)lut[key] - k * (1 << 23));
+    if ((b & 0x7fffffffu) > 0x7f800000u) r = b | 0x00400000u;     // NaN -> quiet NaN
+    else if (E == 0u) r = (b & 0x80000000u) | 0x7f800000u;        // +-0 / denormal -> +-inf
+    else if (b & 0x80000000u) r = 0xffc00000u;                    // negative -> default NaN
+    else if (E == 0xffu) r = 0u;                                  // +inf -> +0
+    return __uint_as_float(r);
+}
+
+// SIMD::Normalize (SIMD_AVX.h:170-180): rsqrt + one Newton-Raphson step.
+__device__ __forceinline__ void normalize3(float& x, float& y, float& z, const uint32_t* __restrict__ lut)
+{
+    const float len = (x * x + y * y) + z * z;
+    const float nr = rsqrtps_x86(len, lut);
+    const float muls = (len * nr) * nr;
+    const float s = (0.5f * nr) * (3.0f - muls);
+    x = x * s;
+    y = y * s;
+    z = z * s;
+}
+
+// Ray direction (Sphereflake.cpp:149-150, 162-167): u = x/W, v = y/H at the pixel corner.
+__device__ __forceinline__ void ray_dir(const FrameArgs& a, float x, float y, float& dx, float& dy, float& dz,
+                                        const uint32_t* __restrict__ lut)
+{
+    const float u = x / a.fw;
+    const float v = y / a.fh;
+    dx = ((a.tl[0] + a.dh[0] * u) + a.dv[0] * v) - a.o[0];
+    dy = ((a.tl[1] + a.dh[1] * u) + a.dv[1] * v) - a.o[1];
+    dz = ((a.tl[2] + a.dh[2] * u) + a.dv[2] * v) - a.o[2];
+    normalize3(dx, dy, dz, lut);
+}
+
+// Near root of RaySphereIntersection (SIMD_AVX.h:260-267); NaN when R2 < d2 (lanes that missed).
+__device__ __forceinline__ float near_root(float tca, float d2, float R2)
+{
+    const float thc = __builtin_sqrtf(R2 - d2);
+    const float t0 = tca + thc;
+    const float t1 = tca - thc;
+    return (t0 <= t1) ? t0 : t1;
+}
+
+struct HitState {
+    float minT;
+    float cx, cy, cz;     // centre of the nearest accepted sphere
+    uint32_t index;       // its heap index (low 32 bits)
+    bool hit;
+};
+
+// Position and normal of the nearest hit (Sphereflake.h:218-224). Computed once from the winning
+// t and centre: the same operations on the same operands as the reference's per-acceptance update.
+__device__ __forceinline__ void shade(float dx, float dy, float dz, const HitState& h, const uint32_t* __restrict__ lut,
+                                      float& px, float& py, float& pz, float& nx, float& ny, float& nz)
+{
+    px = py = pz = nx = ny = nz = 0.f;
+    if (h.hit) {
+        px = dx * h.minT;
+        py = dy * h.minT;
+        pz = dz * h.minT;
+        nx = px - h.cx;
+        ny = py - h.cy;
+        nz = pz - h.cz;
+        normalize3(nx, ny, nz, lut);
+    }
+}
+
+__device__ __forceinline__ float wave_min(float v)
+{
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = fminf(v, __shfl_xor(v, m, 64));
+    return v;
+}
+
+// "Any lane of my group": a group is the lane itself (per-ray semantics) or the 8 lanes of a
+// reference AVX packet (packet semantics: movemask early-outs, SIMD_AVX.h:247,255, Sphereflake.h:140,149,207).
+template <bool PACKET>
+__device__ __forceinline__ bool group_any(bool p)
+{
+    if constexpr (PACKET) {
+        const uint64_t b = __ballot(p);
+        return ((b >> (threadIdx.x & 56u)) & 0xffull) != 0ull;
+    } else {
+        return p;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Wave-coherent traversal of IntersectSphereflake (Sphereflake.h:86-226).
+//
+// LDS per wave: [root transform: 16 floats][level 0 .. levels-1: 9 children x 12 floats].
+// Level L holds the world transforms of the 9 children of the node currently open at depth L,
+// as 3x4 column-major (col0.xyz, col1.xyz, col2.xyz, col3.xyz = centre).
+// Uniform traversal state: depth d of the node under evaluation, packed child cursors (4 bits
+// per level), heap index of the current node, LDS offset of its transform. Per-lane state:
+// ebits bit L = this lane (or its packet) expanded the open node at depth L.
+//
+// Per node (group = lane for per-ray semantics, 8-lane packet for packet semantics):
+//   bounding   hb = active && any_g(tca >= 0) && any_g(d2 <= (2r)^2)
+//   LOD        ex = hb && any_g(t < T_d)          [T_d exact threshold of sqrtf(t/r) < 70 || t < 0]
+//   children   if any lane ex: build 9 child transforms, descend
+//   self       hs = ex && any_g(tca >= 0) && any_g(d2 <= r^2); accept lanes with d2 <= r^2 && t < minT
+// For per-ray groups these are exactly the per-lane tests of the reference.
+// ------------------------------------------------------------------------------------------
+template <bool PACKET>
+__device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ L,
+                                         uint32_t levels, float dx, float dy, float dz, bool valid, HitState& h,
+                                         int32_t& maxd, bool& overflowed)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+
+    // root transform -> LDS (lanes 0..11)
+    if (lane < 12u) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) v = (lane == (uint32_t)k) ? root[k] : v;
+        L[lane] = v;
+    }
+
+    // This lane's two entries of the cooperative child build: e = lane and e = lane + 64 (< 108).
+    // Entry e of a level = child i = e / 12, column c = (e % 12) / 3, row r = e % 3.
+    float bA[4], bB[4];
+    uint32_t rA, rB;
+    bool tA, tB;
+    {
+        const uint32_t e = lane, i = e / 12u, c = (e % 12u) / 3u;
+        rA = e % 3u;
+        tA = (c == 3u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bA[j] = K->child[i][4u * c + j];
+    }
+    const bool hasB = lane < (SF_LDS_LEVEL - 64u);
+    {
+        const uint32_t e = hasB ? lane + 64u : 0u, i = e / 12u, c = (e % 12u) / 3u;
+        rB = e % 3u;
+        tB = (c == 3u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bB[j] = K->child[i][4u * c + j];
+    }
+
+    h.minT = FLT_MAX;
+    h.cx = h.cy = h.cz = 0.f;
+    h.index = 0xffffffffu;
+    h.hit = false;
+
+    uint32_t ebits = 0;       // per lane
+    uint32_t d = 0;           // uniform: depth of the node being evaluated
+    uint64_t cis = 0;         // uniform: child cursor of level L at bits 4L..4L+3 (levels < 16)
+    uint64_t cis_hi = 0;      //          levels 16..30
+    uint64_t idx = 0;         // uniform: heap index of the node (root 0, child i of n: 9n+1+i)
+    uint32_t nbase = 0;       // uniform: LDS offset of the current node's transform
+
+    __builtin_amdgcn_wave_barrier();
+    __asm__ volatile("" ::: "memory");
+
+    auto cursor = [&](uint32_t lvl) -> uint32_t {
+        return lvl < 16u ? (uint32_t)(cis >> (4u * lvl)) & 15u : (uint32_t)(cis_hi >> (4u * (lvl - 16u))) & 15u;
+    };
+    auto set_cursor = [&](uint32_t lvl, uint32_t v) {
+        if (lvl < 16u) cis = (cis & ~(15ull << (4u * lvl))) | ((uint64_t)v << (4u * lvl));
+        else cis_hi = (cis_hi & ~(15ull << (4u * (lvl - 16u)))) | ((uint64_t)v << (4u * (lvl - 16u)));
+    };
+
+    for (;;) {
+        // ---- evaluate node at depth d: bounding sphere (2r) + LOD (Sphereflake.h:97-153)
+        {
+            const bool active = (d == 0u) ? valid : (((ebits >> (d - 1u)) & 1u) != 0u);
+            const float cx = L[nbase + 9], cy = L[nbase + 10], cz = L[nbase + 11];
+            const float tca = (cx * dx + cy * dy) + cz * dz;                 // Dot(centre, dir)
+            const float cc = (cx * cx + cy * cy) + cz * cz;                  // Dot(centre, centre)
+            const float d2 = cc - tca * tca;
+            const float R2b = K->dt.r2_bound[d];
+            const bool hb = active && group_any<PACKET>(tca >= 0.0f) && group_any<PACKET>(d2 <= R2b);
+            bool ex = false;
+            if (__ballot(hb)) {
+                const float tb = near_root(tca, d2, R2b);
+                ex = hb && group_any<PACKET>(tb < K->dt.lod[d]);            // exact LOD threshold
+            }
+            const uint64_t me = __ballot(ex);
+            ebits = ex ? (ebits | (1u << d)) : (ebits & ~(1u << d));
+            if (me) {
+                maxd = (int32_t)d > maxd ? (int32_t)d : maxd;                // Sphereflake.h:157-160
+                if (d < levels) {
+                    // ---- build the 9 child world transforms into level d (Sphereflake.h:162-172):
+                    // child translation scaled by (4/3) r, world = parent * child (SIMD_AVX.h:59-81)
+                    const float s = K->dt.scale[d];
+                    const uint32_t lb = SF_LDS_ROOT + d * SF_LDS_LEVEL;
+                    {
+                        const float a0 = L[nbase + rA], a1 = L[nbase + 3 + rA], a2 = L[nbase + 6 + rA],
+                                    a3 = L[nbase + 9 + rA];
+                        const float b0 = tA ? bA[0] * s : bA[0];
+                        const float b1 = tA ? bA[1] * s : bA[1];
+                        const float b2 = tA ? bA[2] * s : bA[2];
+                        L[lb + lane] = ((a0 * b0 + a1 * b1) + a2 * b2) + a3 * bA[3];
+                    }
+                    if (hasB) {
+                        const float a0 = L[nbase + rB], a1 = L[nbase + 3 + rB], a2 = L[nbase + 6 + rB],
+                                    a3 = L[nbase + 9 + rB];
+                        const float b0 = tB ? bB[0] * s : bB[0];
+                        const float b1 = tB ? bB[1] * s : bB[1];
+                        const float b2 = tB ? bB[2] * s : bB[2];
+                        L[lb + 64u + lane] = ((a0 * b0 + a1 * b1) + a2 * b2) + a3 * bB[3];
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    __asm__ volatile("" ::: "memory");
+                    set_cursor(d, 0u);
+                    d += 1u;
+                    idx = 9u * idx + 1u;
+                    nbase = lb;
+                    continue;   // evaluate child 0
+                }
+                // needs a deeper stack than provisioned: drop the subtree, flag the tile
+                overflowed = true;
+                ebits &= ~(1u << d);
+            }
+        }
+        // ---- advance: next sibling, or close finished nodes with their own sphere test
+        bool finished = false;
+        for (;;) {
+            if (d == 0u) { finished = true; break; }
+            const uint32_t p = d - 1u;
+            const uint32_t ci = cursor(p);
+            if (ci < 8u) {
+                set_cursor(p, ci + 1u);
+                idx += 1u;
+                nbase += 12u;
+                break;
+            }
+            // all 9 children of the node at depth p done: self test (Sphereflake.h:174-224)
+            idx = (idx - 9u) / 9u;
+            d = p;
+            nbase = p == 0u ? 0u : SF_LDS_ROOT + (p - 1u) * SF_LDS_LEVEL + cursor(p - 1u) * 12u;
+            const bool act = ((ebits >> p) & 1u) != 0u;
+            const float cx = L[nbase + 9], cy = L[nbase + 10], cz = L[nbase + 11];
+            const float tca = (cx * dx + cy * dy) + cz * dz;
+            const float cc = (cx * cx + cy * cy) + cz * cz;
+            const float d2 = cc - tca * tca;
+            const float R2s = K->dt.r2_self[p];
+            const bool in = d2 <= R2s;
+            const bool hs = act && group_any<PACKET>(tca >= 0.0f) && group_any<PACKET>(in);
+            if (__ballot(hs)) {
+                const float ts = near_root(tca, d2, R2s);
+                const bool acc = hs && in && (ts < h.minT);                  // strict: first wins ties
+                if (acc) {
+                    h.minT = ts;
+                    h.cx = cx;
+                    h.cy = cy;
+                    h.cz = cz;
+                    h.index = (uint32_t)idx;
+                    h.hit = true;
+                }
+            }
+        }
+        if (finished) break;
+    }
+}
+
+struct Tile {
+    uint32_t x, y, orow;
+    bool valid;
+};
+
+// Tile of a wave: owned tile row k (band sharding) -> frame tile row.
+__device__ __forceinline__ Tile tile_of(const FrameArgs& a, uint32_t tile, uint32_t lane)
+{
+    const uint32_t tx = tile % a.tiles_x, k = tile / a.tiles_x;
+    const uint32_t band = a.band_index + (k / a.tiles_per_band) * a.band_count;
+    const uint32_t ty = band * a.tiles_per_band + k % a.tiles_per_band;
+    Tile t;
+    t.x = tx * SF_TILE + (lane & 7u);
+    t.y = ty * SF_TILE + (lane >> 3);
+    t.valid = t.x < a.W && t.y < a.H;
+    t.orow = a.compact ? (k * SF_TILE + (lane >> 3)) : t.y;
+    return t;
+}
+
+// G-buffer write (Sphereflake.cpp:186-196): (pos, 1), (nrm, 1); a miss writes (0,0,0,1).
+__device__ __forceinline__ void write_pixel(const FrameArgs& a, const Tile& t, float dx, float dy, float dz,
+                                            const HitState& h, const uint32_t* __restrict__ lut)
+{
+    float px, py, pz, nx, ny, nz;
+    shade(dx, dy, dz, h, lut, px, py, pz, nx, ny, nz);
+    const size_t o = (size_t)t.orow * a.W + t.x;
+    reinterpret_cast<float4*>(a.pos)[o] = make_float4(px, py, pz, 1.0f);
+    reinterpret_cast<float4*>(a.nrm)[o] = make_float4(nx, ny, nz, 1.0f);
+    if (a.emit_aux) {
+        if (a.min_t) a.min_t[o] = h.minT;
+        if (a.hit_index) a.hit_index[o] = h.hit ? h.index : 0xffffffffu;
+    }
+}
+
+template <bool FIXUP>
+__device__ __forceinline__ void trace_tile(const FrameArgs& a, float* __restrict__ L, uint32_t tile, uint32_t levels,
+                                           uint32_t* overflow_list, uint32_t* overflow_count)
+{
+    const DeviceConsts* __restrict__ K = a.consts;
+    const uint32_t lane = threadIdx.x & 63u;
+    const Tile t = tile_of(a, tile, lane);
+    float dx, dy, dz;
+    ray_dir(a, (float)t.x, (float)t.y, dx, dy, dz, K->lut);
+
+    HitState h;
+    int32_t maxd = -1;
+    bool overflowed = false;
+    traverse<false>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed);
+
+    if (!FIXUP && overflowed && lane == 0u) {
+        // a deeper re-trace (sf_fixup_wave) rewrites this whole tile
+        const uint32_t slot = atomicAdd(overflow_count, 1u);
+        overflow_list[slot] = tile;
+    }
+    if (t.valid) write_pixel(a, t, dx, dy, dz, h, K->lut);
+
+    // stats: max depth reached, closest sphere distance (Sphereflake.h:157-160, Sphereflake.cpp:197-200)
+    const float closest = wave_min(t.valid ? h.minT : FLT_MAX);
+    if (lane == 0u) {
+        if (maxd >= 0) atomicMax(&a.stats[0], maxd);
+        atomicMin(&a.stats[1], sf_float_key(closest));
+        if (FIXUP && overflowed) atomicAdd(&a.stats[2], 1);
+    }
+}
+
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(256) void sf_trace_wave(FrameArgs a, uint32_t* overflow_list,
+                                                                uint32_t* overflow_count)
+{
+    extern __shared__ float lds[];
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t per_wave = SF_LDS_ROOT + a.max_depth * SF_LDS_LEVEL;
+    const uint32_t tile = blockIdx.x * SF_WAVES_PER_BLOCK + wv;
+    if (tile >= a.tiles_x * a.tile_rows) return;
+    trace_tile<false>(a, lds + wv * per_wave, tile, a.max_depth, overflow_list, overflow_count);
+}
+
+// Re-traces flagged tiles with SF_MAX_LEVELS levels. Grid-stride over the list; reads this
+// render's counter and zeroes the other one (the next render's), so no memset is needed.
+extern "C" __global__ __launch_bounds__(256) void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list,
+                                                                uint32_t* counters, uint32_t parity)
+{
+    extern __shared__ float lds[];
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t per_wave = SF_LDS_ROOT + SF_MAX_LEVELS * SF_LDS_LEVEL;
+    if (blockIdx.x == 0 && threadIdx.x == 0) counters[parity ^ 1u] = 0u;
+    const uint32_t n = counters[parity];
+    for (uint32_t i = blockIdx.x * SF_WAVES_PER_BLOCK + wv; i < n; i += gridDim.x * SF_WAVES_PER_BLOCK)
+        trace_tile<true>(a, lds + wv * per_wave, overflow_list[i], SF_MAX_LEVELS, nullptr, nullptr);
+}
+
+// ------------------------------------------------------------------------------------------
+// One thread per ray, private stack (Sphereflake.h:86-226 restated as an explicit DFS).
+// ------------------------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(256) void sf_trace_ray(FrameArgs a)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t tile = blockIdx.x * SF_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (tile >= a.tiles_x * a.tile_rows) return;
+    const DeviceConsts* __restrict__ K = a.consts;
+    const uint32_t* __restrict__ lut = K->lut;
+    const Tile t = tile_of(a, tile, lane);
+    float dx, dy, dz;
+    ray_dir(a, (float)t.x, (float)t.y, dx, dy, dz, lut);
+
+    float xf[SF_MAX_LEVELS + 1][12];
+    uint8_t cur[SF_MAX_LEVELS + 1];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) xf[0][k] = a.root[k];
+
+    HitState h;
+    h.minT = FLT_MAX;
+    h.cx = h.cy = h.cz = 0.f;
+    h.index = 0xffffffffu;
+    h.hit = false;
+    int32_t maxd = -1;
+    bool overflowed = false;
+
+    auto make_child = [&](uint32_t p, uint32_t i) {
+        const float s = K->dt.scale[p];
+        const float* P = xf[p];
+        float* out = xf[p + 1];
+        for (int c = 0; c < 4; ++c) {
+            const float* B = K->child[i] + 4 * c;
+            const float b0 = c == 3 ? B[0] * s : B[0];
+            const float b1 = c == 3 ? B[1] * s : B[1];
+            const float b2 = c == 3 ? B[2] * s : B[2];
+            const float b3 = B[3];
+            for (int r = 0; r < 3; ++r)
+                out[3 * c + r] = ((P[r] * b0 + P[3 + r] * b1) + P[6 + r] * b2) + P[9 + r] * b3;
+        }
+    };
+
+    if (t.valid) {
+        uint32_t d = 0;
+        uint64_t idx = 0;
+        for (;;) {
+            bool ex = false;
+            {
+                const float cx = xf[d][9], cy = xf[d][10], cz = xf[d][11];
+                const float tca = (cx * dx + cy * dy) + cz * dz;
+                const float d2 = ((cx * cx + cy * cy) + cz * cz) - tca * tca;
+                const float R2b = K->dt.r2_bound[d];
+                if (tca >= 0.0f && d2 <= R2b) ex = near_root(tca, d2, R2b) < K->dt.lod[d];
+            }
+            if (ex) {
+                maxd = (int32_t)d > maxd ? (int32_t)d : maxd;
+                if (d < SF_MAX_LEVELS) {
+                    cur[d] = 0;
+                    make_child(d, 0);
+                    d += 1;
+                    idx = 9u * idx + 1u;
+                    continue;
+                }
+                overflowed = true;
+            }
+            bool finished = false;
+            for (;;) {
+                if (d == 0) { finished = true; break; }
+                const uint32_t p = d - 1;
+                if (cur[p] < 8) {
+                    cur[p] += 1;
+                    make_child(p, cur[p]);
+                    idx += 1u;
+                    break;
+                }
+                idx = (idx - 9u) / 9u;
+                d = p;
+                const float cx = xf[p][9], cy = xf[p][10], cz = xf[p][11];
+                const float tca = (cx * dx + cy * dy) + cz * dz;
+                const float d2 = ((cx * cx + cy * cy) + cz * cz) - tca * tca;
+                const float R2s = K->dt.r2_self[p];
+                if (tca >= 0.0f && d2 <= R2s) {
+                    const float ts = near_root(tca, d2, R2s);
+                    if (ts < h.minT) {
+                        h.minT = ts;
+                        h.cx = cx;
+                        h.cy = cy;
+                        h.cz = cz;
+                        h.index = (uint32_t)idx;
+                        h.hit = true;
+                    }
+                }
+            }
+            if (finished) break;
+        }
+        write_pixel(a, t, dx, dy, dz, h, lut);
+    }
+    // wave-level stats
+    float closest = wave_min(t.valid ? h.minT : FLT_MAX);
+    int32_t md = maxd;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) md = max(md, __shfl_xor(md, m, 64));
+    const bool anyov = __ballot(overflowed) != 0;
+    if (lane == 0u) {
+        if (md >= 0) atomicMax(&a.stats[0], md);
+        atomicMin(&a.stats[1], sf_float_key(closest));
+        if (anyov) atomicAdd(&a.stats[2], 1);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Frame-less progressive mode (Sphereflake.cpp:86-214): random 8-ray packets.
+// ------------------------------------------------------------------------------------------
+
+// std::mt19937 continuation: state[0..623] + next index state[624]; writes n raw 32-bit outputs
+// (std::uniform_int_distribution<unsigned>(0) over the full range returns them unchanged).
+// One workgroup; the twist runs in four dependency phases through LDS.
+extern "C" __global__ __launch_bounds__(1024) void sf_mt_draws(uint32_t* state, uint32_t* out, uint32_t n)
+{
+    __shared__ uint32_t s[624], t[624];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < 624u; i += blockDim.x) s[i] = state[i];
+    uint32_t pos = state[624];
+    __syncthreads();
+    auto f = [](uint32_t a, uint32_t b, uint32_t c) {
+        const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+        return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    };
+    uint32_t done = 0;
+    while (done < n) {
+        if (pos >= 624u) {
+            if (tid < 227u) t[tid] = f(s[tid], s[tid + 1], s[tid + 397]);
+            __syncthreads();
+            if (tid >= 227u && tid < 454u) t[tid] = f(s[tid], s[tid + 1], t[tid - 227]);
+            __syncthreads();
+            if (tid >= 454u && tid < 623u) t[tid] = f(s[tid], s[tid + 1], t[tid - 227]);
+            __syncthreads();
+            if (tid == 623u) t[623] = f(s[623], t[0], t[396]);
+            __syncthreads();
+            if (tid < 624u) s[tid] = t[tid];
+            __syncthreads();
+            pos = 0;
+        }
+        const uint32_t m = min(624u - pos, n - done);
+        if (tid < m) {
+            uint32_t y = s[pos + tid];
+            y ^= y >> 11;
+            y ^= (y << 7) & 0x9d2c5680u;
+            y ^= (y << 15) & 0xefc60000u;
+            y ^= y >> 18;
+            out[done + tid] = y;
+        }
+        pos += m;
+        done += m;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < 624u; i += blockDim.x) state[i] = s[i];
+    if (tid == 0) state[624] = pos;
+}
+
+namespace {
+// Sobol::Sample (Sobol.cpp:41-55) for dims 0/1.
+__device__ __forceinline__ float sobol_sample(uint64_t index, const uint32_t* __restrict__ m, uint32_t scramble)
+{
+    uint32_t r = scramble;
+    for (uint32_t i = 0; index; index >>= 1, ++i)
+        if (index & 1u) r ^= m[i];
+    return (float)r * (1.f / 4294967296.0f);
+}
+}  // namespace
+
+// Trace `packets` packets: one 8-lane group per packet, 8 packets per wave. Lane q of packet j uses
+// the footprint of Sphereflake.cpp:143-147 around (x0, y0) drawn at Sobol index counter0 + j with
+// scrambles draws[2j], draws[2j+1] (Sphereflake.cpp:139-141). Results are staged per lane; the
+// owner word of each pixel keeps the highest ticket, so the scatter reproduces sequential order.
+extern "C" __global__ __launch_bounds__(256) void sf_progressive_trace(FrameArgs a, const uint32_t* draws,
+                                                                       uint64_t counter0, uint32_t packets,
+                                                                       uint64_t ticket0, PacketLane* lanes,
+                                                                       unsigned long long* owner)
+{
+    extern __shared__ float lds[];
+    const DeviceConsts* __restrict__ K = a.consts;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t packet = (blockIdx.x * SF_WAVES_PER_BLOCK + wv) * 8u + (lane >> 3);
+    if ((blockIdx.x * SF_WAVES_PER_BLOCK + wv) * 8u >= packets) return;   // wave-uniform
+    const bool valid = packet < packets;
+    const uint32_t q = lane & 7u;
+    float x0 = 0.f, y0 = 0.f;
+    if (valid) {
+        const uint64_t c = counter0 + packet;
+        x0 = 1.0f + floorf(sobol_sample(c, K->sobol[0], draws[2u * packet]) * (float)(a.W - 2u));
+        y0 = 1.0f + floorf(sobol_sample(c, K->sobol[1], draws[2u * packet + 1u]) * (float)(a.H - 2u));
+    }
+    // footprint: xa = {x0, x0+1, x0+1, x0, x0, x0+1, x0-1, x0-1}, ya = {y0, y0+1, y0, y0+1, y0-1, y0-1, y0, y0-1}
+    const float ox = (q == 1u || q == 2u || q == 5u) ? 1.0f : (q >= 6u ? -1.0f : 0.0f);
+    const float oy = (q == 1u || q == 3u) ? 1.0f : ((q == 4u || q == 5u || q == 7u) ? -1.0f : 0.0f);
+    const float xf = x0 + ox, yf = y0 + oy;
+    float dx, dy, dz;
+    ray_dir(a, xf, yf, dx, dy, dz, K->lut);
+
+    HitState h;
+    int32_t maxd = -1;
+    bool overflowed = false;
+    traverse<true>(K, a.root, lds + wv * (SF_LDS_ROOT + SF_PROGRESSIVE_LEVELS * SF_LDS_LEVEL), SF_PROGRESSIVE_LEVELS,
+                   dx, dy, dz, valid, h, maxd, overflowed);
+
+    PacketLane out;
+    shade(dx, dy, dz, h, K->lut, out.px, out.py, out.pz, out.nx, out.ny, out.nz);
+    out.min_t = h.minT;
+    // idx = (size_t)xa + (size_t)ya * W; the reference skips idx > size (Sphereflake.cpp:188-191)
+    const uint64_t pix = (uint64_t)xf + (uint64_t)yf * a.W;
+    const bool inb = valid && pix < (uint64_t)a.W * a.H;
+    out.pixel = inb ? (uint32_t)pix : 0xffffffffu;
+    if (valid) lanes[(size_t)packet * 8u + q] = out;
+    if (inb) atomicMax(owner + pix, (unsigned long long)(ticket0 + packet));
+
+    const float closest = wave_min(inb ? h.minT : FLT_MAX);
+    const bool anyov = __ballot(overflowed) != 0ull;
+    if (lane == 0u) {
+        if (maxd >= 0) atomicMax(&a.stats[0], maxd);
+        atomicMin(&a.stats[1], sf_float_key(closest));
+        if (anyov) atomicAdd(&a.stats[2], 1);
+    }
+}
+
+// Last writer wins by ticket (= the reference worker's sequential packet order).
+extern "C" __global__ __launch_bounds__(256) void sf_progressive_scatter(FrameArgs a, uint32_t packets, uint64_t ticket0,
+                                                                         const PacketLane* lanes,
+                                                                         const unsigned long long* owner)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= packets * 8u) return;
+    const PacketLane l = lanes[i];
+    if (l.pixel == 0xffffffffu) return;
+    if (owner[l.pixel] != (unsigned long long)(ticket0 + i / 8u)) return;
+    reinterpret_cast<float4*>(a.pos)[l.pixel] = make_float4(l.px, l.py, l.pz, 1.0f);
+    reinterpret_cast<float4*>(a.nrm)[l.pixel] = make_float4(l.nx, l.ny, l.nz, 1.0f);
+    if (a.emit_aux && a.min_t) a.min_t[l.pixel] = l.min_t;
+}

@@ -1,0 +1,381 @@
+"""Python host mirror of the reference ``SphereflakeRaytracer::Sphereflake`` class
+(/root/reference/sphereflake/Sphereflake.h:13-58) over the gfx950 C ABI
+(include/sphereflake/sf.h, built as build/libsphereflake_hip.so).
+
+There is no CPU fallback: if the HIP library is missing or the device is not a gfx950,
+constructing a :class:`Sphereflake` raises. The CPU restatement under ``oracle/`` is test
+infrastructure and is never imported from here.
+
+Names follow the reference: ``SetView``, ``GetGBuffer``, ``GetMaxDepthReached``,
+``ResetMaxDepthReached``, ``GetRaysPerSecond``, ``ResetRaysPerSecond``,
+``GetClosestSphereDistance``, ``ResetClosestSphereDistance``, ``Initialize`` (frame-less
+progressive mode), plus ``Render`` (one deterministic full frame). ``Camera`` mirrors
+reference camera.h.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT_DIR = os.path.dirname(PKG_DIR)                 # sphereflake-raytracer_amd/
+LIB_PATH = os.path.join(ROOT_DIR, "build", "libsphereflake_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(ROOT_DIR), "include", "sphereflake", "sf.h")
+
+SF_OK, SF_EINVAL, SF_ENOMEM, SF_EHIP, SF_ENODEV, SF_ENOVIEW, SF_EDEPTH, SF_ESTATE = 0, -1, -2, -3, -4, -5, -6, -7
+SF_KERNEL_WAVE, SF_KERNEL_PER_RAY = 0, 1
+SF_MAX_DEPTH_LIMIT = 31
+FLT_MAX = float(np.finfo(np.float32).max)
+
+# Camera of reference main.cpp:92-96; BASELINE configs scale the position by K.
+DEFAULT_CAMERA_POSITION = (-5.4098, -7.2139, 1.19006)
+DEFAULT_PITCH = -1.371
+DEFAULT_YAW = 0.921999
+
+
+class SphereflakeError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = _strerror(code)
+        super().__init__(f"{what}: {msg} ({code})" if what else f"{msg} ({code})")
+
+
+class sf_render_params(ctypes.Structure):
+    _fields_ = [("band_rows", ctypes.c_uint32), ("band_count", ctypes.c_uint32),
+                ("band_index", ctypes.c_uint32), ("compact", ctypes.c_uint32),
+                ("kernel", ctypes.c_uint32), ("emit_aux", ctypes.c_uint32),
+                ("max_depth", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("stream", ctypes.c_void_p)]
+
+
+class sf_stats(ctypes.Structure):
+    _fields_ = [("max_depth", ctypes.c_int32), ("closest", ctypes.c_float),
+                ("rays", ctypes.c_int64), ("overflow_tiles", ctypes.c_int64)]
+
+
+# exported symbol -> (restype, argtypes); checked against include/sphereflake/sf.h by the tests
+_F = ctypes.POINTER(ctypes.c_float)
+_U = ctypes.POINTER(ctypes.c_uint32)
+_CTX = ctypes.c_void_p
+SIGNATURES = {
+    "sf_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+    "sf_destroy": (None, [_CTX]),
+    "sf_set_view": (ctypes.c_int, [_CTX, _F, _F, _F, _F]),
+    "sf_set_setup": (ctypes.c_int, [_CTX, _F, _F]),
+    "sf_get_setup": (ctypes.c_int, [_CTX, _F, _F]),
+    "sf_render": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_render_params)]),
+    "sf_render_to": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_render_params), ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p]),
+    "sf_slab_rows": (ctypes.c_uint32, [ctypes.c_uint32] * 4),
+    "sf_download": (ctypes.c_int, [_CTX, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "sf_device_buffers": (ctypes.c_int, [_CTX] + [ctypes.POINTER(ctypes.c_void_p)] * 4),
+    "sf_synchronize": (ctypes.c_int, [_CTX]),
+    "sf_get_stats": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_stats)]),
+    "sf_reset_max_depth": (ctypes.c_int, [_CTX]),
+    "sf_reset_rays": (ctypes.c_int, [_CTX]),
+    "sf_reset_closest": (ctypes.c_int, [_CTX]),
+    "sf_progressive": (ctypes.c_int, [_CTX, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p]),
+    "sf_camera_corners": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, _F, ctypes.c_float, ctypes.c_float,
+                                         ctypes.c_float, ctypes.c_float, _F, _F, _F, _F]),
+    "sf_child_transforms": (ctypes.c_int, [_F]),
+    "sf_root_transform": (ctypes.c_int, [_F, _F]),
+    "sf_depth_constants": (ctypes.c_int, [ctypes.c_uint32, _F, _F]),
+    "sf_rsqrtps": (ctypes.c_float, [ctypes.c_float]),
+    "sf_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "sf_last_hip_error": (ctypes.c_int, [_CTX]),
+    "sf_abi_version": (ctypes.c_int, []),
+    "sf_device_count": (ctypes.c_int, []),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def build(force: bool = False) -> str:
+    """Compile the gfx950 library in-tree (hipcc cross-compiles without a GPU)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-C", ROOT_DIR, "all"])
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    """Load build/libsphereflake_hip.so; raises if it is missing (no fallback path exists)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(f"HIP renderer library not built: {LIB_PATH} (run make -C {ROOT_DIR})")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def _strerror(code: int) -> str:
+    try:
+        return lib().sf_strerror(code).decode()
+    except Exception:  # library not loadable: still give a message
+        return f"sphereflake error {code}"
+
+
+def _check(rc: int, what: str = "", ctx=None) -> None:
+    if rc != SF_OK:
+        err = SphereflakeError(rc, what)
+        if ctx is not None and rc == SF_EHIP:
+            err.hip_error = lib().sf_last_hip_error(ctx)
+        raise err
+
+
+def _f32(a, n=None) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+    if n is not None and a.size != n:
+        raise ValueError(f"expected {n} floats, got {a.size}")
+    return a
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(_F)
+
+
+# ----------------------------------------------------------------------------- host setup helpers
+
+def child_transforms() -> np.ndarray:
+    """9 unit child frames (reference Sphereflake.cpp:216-249), [9, 16] glm column-major."""
+    out = np.zeros((9, 16), np.float32)
+    _check(lib().sf_child_transforms(_fp(out)), "sf_child_transforms")
+    return out
+
+
+def root_transform(origin) -> np.ndarray:
+    """Root transform of SetView (Sphereflake.cpp:83) for a ray origin, [16]."""
+    o = _f32(origin, 3)
+    out = np.zeros(16, np.float32)
+    _check(lib().sf_root_transform(_fp(o), _fp(out)), "sf_root_transform")
+    return out
+
+
+def depth_constants(depth: int):
+    """(radius r_d, exact LOD threshold T_d) used by the kernels at a depth."""
+    r, t = ctypes.c_float(), ctypes.c_float()
+    _check(lib().sf_depth_constants(depth, ctypes.byref(r), ctypes.byref(t)), "sf_depth_constants")
+    return r.value, t.value
+
+
+def rsqrtps(x: float) -> float:
+    """x86 rsqrtps as reproduced by the renderer (host copy of the kernels' table)."""
+    return lib().sf_rsqrtps(float(x))
+
+
+def device_count() -> int:
+    return lib().sf_device_count()
+
+
+class Camera:
+    """Mirror of reference camera.h (SphereflakeRaytracer::Camera): FOV 60, angles in radians."""
+
+    def __init__(self, width: int, height: int):
+        self.width, self.height = int(width), int(height)
+        self.position = np.zeros(3, np.float32)
+        self.fov, self.roll, self.pitch, self.yaw = 60.0, 0.0, 0.0, 0.0
+
+    def SetPosition(self, p):
+        self.position = _f32(p, 3).copy()
+
+    def GetPosition(self):
+        return self.position.copy()
+
+    def SetPitch(self, v): self.pitch = float(v)
+    def SetYaw(self, v): self.yaw = float(v)
+    def SetRoll(self, v): self.roll = float(v)
+    def SetFOV(self, v): self.fov = float(v)
+
+    def corners(self):
+        o, tl, tr, bl = (np.zeros(3, np.float32) for _ in range(4))
+        pos = _f32(self.position, 3)
+        _check(lib().sf_camera_corners(self.width, self.height, _fp(pos), self.pitch, self.yaw, self.roll,
+                                       self.fov, _fp(o), _fp(tl), _fp(tr), _fp(bl)), "sf_camera_corners")
+        return o, tl, tr, bl
+
+    def GetTopLeft(self): return self.corners()[1]
+    def GetTopRight(self): return self.corners()[2]
+    def GetBottomLeft(self): return self.corners()[3]
+
+
+def config_camera(width: int, height: int, K: float) -> Camera:
+    """The fixed camera of the BASELINE configs: main.cpp:92-96 with position scaled by K."""
+    cam = Camera(width, height)
+    cam.SetPosition(np.asarray(DEFAULT_CAMERA_POSITION, np.float32) * np.float32(K))
+    cam.SetPitch(np.float32(DEFAULT_PITCH))
+    cam.SetYaw(np.float32(DEFAULT_YAW))
+    cam.SetRoll(0.0)
+    return cam
+
+
+# ----------------------------------------------------------------------------- the renderer
+
+@dataclass
+class GBuffer:
+    """Reference GBuffer (Sphereflake.h:7-11): positions / normals as [H, W, 4] float32 (x, y, z, 1)."""
+    positions: np.ndarray
+    normals: np.ndarray
+
+
+def render_params(band_rows=0, band_count=1, band_index=0, compact=False, kernel=SF_KERNEL_WAVE,
+                  emit_aux=False, max_depth=0, stream=None) -> sf_render_params:
+    return sf_render_params(band_rows, band_count, band_index, int(bool(compact)), kernel, int(bool(emit_aux)),
+                            max_depth, 0, stream)
+
+
+class Sphereflake:
+    """Drop-in for the reference class. Owns a device context (G-buffer in HBM)."""
+
+    def __init__(self, width: int, height: int, device: int = 0):
+        self.width, self.height, self.device = int(width), int(height), int(device)
+        L = lib()
+        h = ctypes.c_void_p()
+        _check(L.sf_create(self.device, self.width, self.height, ctypes.byref(h)), "sf_create")
+        self._ctx = h
+        self._worker = None
+        self._stop = threading.Event()
+        self._mutex = threading.Lock()
+        self._seed = 0
+        self._counter = 0
+
+    # lifetime --------------------------------------------------------------
+    def close(self):
+        self._stop.set()
+        if self._worker is not None:
+            self._worker.join()
+            self._worker = None
+        if getattr(self, "_ctx", None):
+            lib().sf_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def ctx(self):
+        return self._ctx
+
+    # view ------------------------------------------------------------------
+    def SetView(self, origin, topLeft, topRight, bottomLeft):
+        o, tl, tr, bl = (_f32(v, 3) for v in (origin, topLeft, topRight, bottomLeft))
+        _check(lib().sf_set_view(self._ctx, _fp(o), _fp(tl), _fp(tr), _fp(bl)), "SetView", self._ctx)
+
+    def SetCamera(self, cam: Camera):
+        o, tl, tr, bl = cam.corners()
+        self.SetView(o, tl, tr, bl)
+
+    def SetSetup(self, child, root):
+        c, r = _f32(child, 144), _f32(root, 16)
+        _check(lib().sf_set_setup(self._ctx, _fp(c), _fp(r)), "sf_set_setup", self._ctx)
+
+    def GetSetup(self):
+        c, r = np.zeros((9, 16), np.float32), np.zeros(16, np.float32)
+        _check(lib().sf_get_setup(self._ctx, _fp(c), _fp(r)), "sf_get_setup", self._ctx)
+        return c, r
+
+    # rendering -------------------------------------------------------------
+    def Render(self, **kw):
+        """One deterministic frame into the device G-buffer (asynchronous)."""
+        p = render_params(**kw)
+        with self._mutex:
+            _check(lib().sf_render(self._ctx, ctypes.byref(p)), "Render", self._ctx)
+
+    def render_to(self, pos_ptr: int, nrm_ptr: int, min_t_ptr: int = 0, index_ptr: int = 0, **kw):
+        """Render into caller-owned device buffers (e.g. torch tensor data_ptr())."""
+        p = render_params(**kw)
+        _check(lib().sf_render_to(self._ctx, ctypes.byref(p), ctypes.c_void_p(pos_ptr), ctypes.c_void_p(nrm_ptr),
+                                  ctypes.c_void_p(min_t_ptr or None), ctypes.c_void_p(index_ptr or None)),
+               "sf_render_to", self._ctx)
+
+    def Synchronize(self):
+        _check(lib().sf_synchronize(self._ctx), "sf_synchronize", self._ctx)
+
+    def device_buffers(self):
+        ptrs = [ctypes.c_void_p() for _ in range(4)]
+        _check(lib().sf_device_buffers(self._ctx, *[ctypes.byref(p) for p in ptrs]), "sf_device_buffers")
+        return [p.value for p in ptrs]
+
+    def download(self, aux: bool = False):
+        """Synchronous D2H of the device G-buffer (+ minT and hit index channels if aux)."""
+        H, W = self.height, self.width
+        pos = np.empty((H, W, 4), np.float32)
+        nrm = np.empty((H, W, 4), np.float32)
+        mint = np.empty((H, W), np.float32) if aux else None
+        idx = np.empty((H, W), np.uint32) if aux else None
+        vp = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+        with self._mutex:
+            _check(lib().sf_download(self._ctx, vp(pos), vp(nrm), vp(mint), vp(idx)), "download", self._ctx)
+        return pos, nrm, mint, idx
+
+    def GetGBuffer(self) -> GBuffer:
+        pos, nrm, _, _ = self.download()
+        return GBuffer(pos, nrm)
+
+    # stats (Sphereflake.h:30-58) --------------------------------------------
+    def stats(self) -> sf_stats:
+        s = sf_stats()
+        _check(lib().sf_get_stats(self._ctx, ctypes.byref(s)), "sf_get_stats", self._ctx)
+        return s
+
+    def GetMaxDepthReached(self) -> int:
+        return int(self.stats().max_depth)
+
+    def ResetMaxDepthReached(self):
+        _check(lib().sf_reset_max_depth(self._ctx), "ResetMaxDepthReached")
+
+    def GetRaysPerSecond(self) -> int:
+        """Rays traced since the last reset (the reference counter's meaning, main.cpp:285-291)."""
+        return int(self.stats().rays)
+
+    def ResetRaysPerSecond(self):
+        _check(lib().sf_reset_rays(self._ctx), "ResetRaysPerSecond")
+
+    def GetClosestSphereDistance(self) -> float:
+        return float(self.stats().closest)
+
+    def ResetClosestSphereDistance(self):
+        _check(lib().sf_reset_closest(self._ctx), "ResetClosestSphereDistance")
+
+    # frame-less progressive mode (Sphereflake.cpp:67-74, 86-214) -------------
+    def Progressive(self, seed: int, packets: int, counter0: int | None = None):
+        """Trace `packets` random 8-ray packets of one reference worker stream (seed, Sobol counter)."""
+        c0 = self._counter if counter0 is None else int(counter0)
+        with self._mutex:
+            _check(lib().sf_progressive(self._ctx, seed & 0xffffffff, c0, packets, None), "sf_progressive", self._ctx)
+        self._counter = c0 + packets
+
+    def Initialize(self, seed: int | None = None, batch: int = 1 << 16):
+        """Start the frame-less progressive loop on a host thread (reference Initialize())."""
+        import time
+        if self._worker is not None:
+            return
+        self._seed = int(time.time()) if seed is None else int(seed)
+        self._stop.clear()
+
+        def loop():
+            while not self._stop.is_set():
+                self.Progressive(self._seed, batch)
+                self.Synchronize()
+
+        self._worker = threading.Thread(target=loop, daemon=True)
+        self._worker.start()

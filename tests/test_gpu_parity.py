@@ -1,0 +1,225 @@
+"""GPU parity: the gfx950 kernels, called through the C ABI, against the golden vectors the reference
+AVX path produced (tests/golden/). Bar: bit-exact G-buffer (positions, normals), minT and hit-sphere
+heap index; the north star's tolerance (nearest-hit sphere index exact, position/normal within
+1e-5 fp32) is asserted separately on the sampled pixels."""
+import numpy as np
+import pytest
+
+from conftest import load_frame, load_npz, load_progressive
+from sfcheck import FLT_MAX, aux_digests, bad_rows, frame_digest, row_digests, samples_arrays
+
+pytestmark = pytest.mark.gpu
+
+import sphereflake_amd as sf  # noqa: E402
+
+TOL = 1e-5   # north star: position/normal within 1e-5 fp32
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    sf.build()
+    n = sf.device_count()
+    assert n >= 1, "no HIP device visible: GPU tests must run on an MI355X"
+    return n
+
+
+def render(name, kernel=sf.SF_KERNEL_WAVE, **kw):
+    fx = load_frame(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        s.Render(kernel=kernel, emit_aux=True, **kw)
+        pos, nrm, mint, idx = s.download(aux=True)
+        st = s.stats()
+    return fx, pos, nrm, mint, idx, st
+
+
+def check_stats(fx, st, mint):
+    e = fx["stats"]
+    assert st.max_depth == e["max_depth"]
+    assert np.float32(st.closest) == np.float32(float.fromhex(e["closest"]))
+    if fx["row_step"] == 1:
+        assert int((mint < np.float32(FLT_MAX)).sum()) == e["hits"]
+        assert st.rays == e["rays"]
+    assert st.overflow_tiles == 0
+
+
+@pytest.mark.parametrize("kernel", [sf.SF_KERNEL_WAVE, sf.SF_KERNEL_PER_RAY])
+@pytest.mark.parametrize("name", ["t1", "t2", "t3", "t4", "t5"])
+def test_tiny_frames_bit_exact(name, kernel):
+    exp = load_npz(name)
+    fx, pos, nrm, mint, idx, st = render(name, kernel)
+    for k, got in (("pos4", pos), ("nrm4", nrm), ("minT", mint), ("index", idx)):
+        assert np.array_equal(np.ascontiguousarray(got).view(np.uint8), np.ascontiguousarray(exp[k]).view(np.uint8)), k
+    check_stats(fx, st, mint)
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c4"])
+def test_config_frames_bit_exact(name):
+    fx, pos, nrm, mint, idx, st = render(name)
+    bad = bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm))
+    assert bad == [], f"{len(bad)} G-buffer rows differ, first {bad[:5]}"
+    bad = bad_rows(fx["row_digest_aux"], aux_digests(mint, idx))
+    assert bad == [], f"{len(bad)} minT/index rows differ, first {bad[:5]}"
+    assert frame_digest(pos, nrm) == fx["frame_digest"]
+    check_stats(fx, st, mint)
+
+
+@pytest.mark.parametrize("name", ["c1", "c2"])
+def test_per_ray_kernel_bit_exact(name):
+    fx, pos, nrm, mint, idx, st = render(name, sf.SF_KERNEL_PER_RAY)
+    assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == []
+    assert bad_rows(fx["row_digest_aux"], aux_digests(mint, idx)) == []
+    check_stats(fx, st, mint)
+
+
+@pytest.mark.parametrize("name", ["c1", "c3"])
+def test_north_star_tolerance_on_samples(name):
+    """Hit-sphere index bit-exact, position/normal within 1e-5 (BASELINE.json north_star)."""
+    fx, pos, nrm, mint, idx, st = render(name)
+    s = samples_arrays(fx)
+    y, x = s["y"], s["x"]
+    assert np.array_equal(idx[y, x], s["index"])
+    assert np.abs(pos[y, x, :3] - s["pos"]).max() <= TOL
+    assert np.abs(nrm[y, x, :3] - s["nrm"]).max() <= TOL
+    assert np.all(pos[y, x, 3] == 1.0) and np.all(nrm[y, x, 3] == 1.0)
+
+
+def test_c5_rows_16384():
+    """configs[4]: 16384x16384 depth 10. Rows y % 64 == 0 rendered as band shard 0 of 8 (8-row bands)
+    into a compact slab in caller-owned device memory (torch), checked against the reference rows."""
+    import torch
+    fx = load_frame("c5")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    rows = sf.lib().sf_slab_rows(H, 8, 8, 0)
+    assert rows == H // 8
+    dev = torch.device("cuda:0")
+    pos = torch.empty((rows, W, 4), dtype=torch.float32, device=dev)
+    nrm = torch.empty_like(pos)
+    mint = torch.empty((rows, W), dtype=torch.float32, device=dev)
+    idx = torch.empty((rows, W), dtype=torch.int32, device=dev)
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        torch.cuda.synchronize()
+        s.render_to(pos.data_ptr(), nrm.data_ptr(), mint.data_ptr(), idx.data_ptr(),
+                    band_rows=8, band_count=8, band_index=0, compact=True, emit_aux=True)
+        s.Synchronize()
+        st = s.stats()
+    sel = torch.arange(0, rows, 8, device=dev)
+    p, n = pos[sel].cpu().numpy(), nrm[sel].cpu().numpy()
+    m, i = mint[sel].cpu().numpy(), idx[sel].cpu().numpy().view(np.uint32)
+    assert bad_rows(fx["row_digest_gbuf"], row_digests(p, n)) == []
+    assert bad_rows(fx["row_digest_aux"], aux_digests(m, i)) == []
+    assert st.overflow_tiles == 0
+    assert st.max_depth >= fx["stats"]["max_depth"]   # the shard covers more rows than the fixture
+
+
+def test_banded_shards_reassemble_full_frame():
+    """Row-band sharding: 4 shards of 16-row bands, compact slabs, de-interleaved,
+    equal the full frame bit for bit."""
+    import torch
+    fx = load_frame("c2")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    band, n = 16, 4
+    full = np.zeros((H, W, 4), np.float32)
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for r in range(n):
+            rows = sf.lib().sf_slab_rows(H, band, n, r)
+            pos = torch.empty((rows, W, 4), dtype=torch.float32, device="cuda:0")
+            nrm = torch.empty_like(pos)
+            s.render_to(pos.data_ptr(), nrm.data_ptr(), band_rows=band, band_count=n, band_index=r, compact=True)
+            s.Synchronize()
+            slab = pos.cpu().numpy()
+            k = 0
+            for b in range(r, (H + band - 1) // band, n):
+                y0, y1 = b * band, min(H, (b + 1) * band)
+                full[y0:y1] = slab[k:k + (y1 - y0)]
+                k += y1 - y0
+            assert k == rows
+    fx2, pos, nrm, mint, idx, st = render("c2")
+    assert np.array_equal(full.view(np.uint32), pos.view(np.uint32))
+
+
+def test_overflow_fixup_path():
+    """Provision only 4 LDS levels: tiles needing depth > 4 are re-traced by sf_fixup_wave; the frame
+    must still be exact and no tile may remain unresolved."""
+    fx, pos, nrm, mint, idx, st = render("c3", max_depth=4)
+    assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == []
+    assert bad_rows(fx["row_digest_aux"], aux_digests(mint, idx)) == []
+    check_stats(fx, st, mint)
+
+
+def test_repeat_renders_deterministic_and_stats_reset():
+    fx = load_frame("t2")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        s.Render()
+        a = s.download()[0].copy()
+        s.Render()
+        b = s.download()[0]
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+        assert s.GetRaysPerSecond() == 2 * W * H
+        s.ResetRaysPerSecond()
+        assert s.GetRaysPerSecond() == 0
+        assert s.GetMaxDepthReached() == fx["stats"]["max_depth"]
+        s.ResetMaxDepthReached()
+        assert s.GetMaxDepthReached() == 0
+        s.ResetClosestSphereDistance()
+        assert s.GetClosestSphereDistance() == np.float32(FLT_MAX)
+
+
+def test_gbuffer_initial_state_and_errors():
+    with sf.Sphereflake(16, 8) as s:
+        g = s.GetGBuffer()
+        assert np.all(g.positions == 0) and np.all(g.normals == 0)   # glm vec4() default
+        with pytest.raises(sf.SphereflakeError) as e:
+            s.Render()
+        assert e.value.code == sf.SF_ENOVIEW
+        s.SetCamera(sf.config_camera(16, 8, 1.0))
+        with pytest.raises(sf.SphereflakeError) as e:
+            s.Render(band_rows=12, band_count=2)
+        assert e.value.code == sf.SF_EINVAL
+
+
+@pytest.mark.parametrize("name", ["p1", "p2", "p3"])
+def test_progressive_matches_reference_worker(name):
+    """Frame-less mode (Sphereflake.cpp:86-214): one reference worker's packet stream from mt19937(seed)
+    -- Sobol pixel draws, 8-ray packets with packet-wide early-outs, sequential scatter."""
+    fx = load_progressive(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        half = fx["packets"] // 3
+        s.Progressive(fx["seed"], half, counter0=0)
+        s.Progressive(fx["seed"], fx["packets"] - half)           # continues the stream
+        pos, nrm, _, _ = s.download()
+        st = s.stats()
+    bad = bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm))
+    assert bad == [], f"{len(bad)} rows differ, first {bad[:5]}"
+    assert st.max_depth == fx["stats"]["max_depth"]
+    assert np.float32(st.closest) == np.float32(float.fromhex(fx["stats"]["closest"]))
+    assert st.rays == fx["stats"]["rays"]
+
+
+def test_progressive_reseed_skip_ahead():
+    """A call that does not continue the stream reseeds and skips ahead: the pixels the p1 stream writes
+    come out exactly as from one uninterrupted call on a fresh context."""
+    fx = load_progressive("p1")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        s.Progressive(fx["seed"] + 1, 100, counter0=0)               # unrelated stream first
+        s.Progressive(fx["seed"], 1000, counter0=0)
+        s.Progressive(fx["seed"] + 7, 10, counter0=5)
+        s.Progressive(fx["seed"], fx["packets"] - 1000, counter0=1000)   # reseed + skip 2000 draws
+        pos, nrm, _, _ = s.download()
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        s.Progressive(fx["seed"], fx["packets"], counter0=0)
+        epos, enrm, _, _ = s.download()
+    assert bad_rows(fx["row_digest_gbuf"], row_digests(epos, enrm)) == []
+    w = epos[..., 3] == 1.0
+    assert np.array_equal(pos[w].view(np.uint32), epos[w].view(np.uint32))
+    assert np.array_equal(nrm[w].view(np.uint32), enrm[w].view(np.uint32))
