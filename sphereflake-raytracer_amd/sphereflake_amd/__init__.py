@@ -110,6 +110,13 @@ def lib() -> ctypes.CDLL:
         if _lib is None:
             if not os.path.exists(LIB_PATH):
                 raise ImportError(f"HIP renderer library not built: {LIB_PATH} (run make -C {ROOT_DIR})")
+            # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64 (SONAME
+            # libamdhip64.so.7). Loading it first makes our NEEDED libamdhip64.so.7 resolve to the
+            # same runtime, so torch tensors / streams and our contexts can be mixed freely.
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             L = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(L, name)
