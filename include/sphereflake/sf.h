@@ -173,6 +173,14 @@ int sf_depth_constants(uint32_t depth, float* radius, float* lod_threshold);
 /* Reproduction of x86 rsqrtps (the table the kernels use). */
 float sf_rsqrtps(float x);
 
+/* --- diagnostics --------------------------------------------------------- */
+
+/* Per-tile timing of the wave kernel (s_memrealtime, 100 MHz) for schedule analysis: when enabled,
+   every full-frame render records {start, end, (XCC id << 32) | HW_ID} per 8x8 tile. Off by default;
+   never changes results. */
+int sf_set_tile_trace(sf_ctx* ctx, int enable);
+int sf_get_tile_trace(sf_ctx* ctx, uint64_t* out, size_t n);   /* n >= 3 * tiles; synchronises */
+
 /* --- misc ---------------------------------------------------------------- */
 
 const char* sf_strerror(int status);

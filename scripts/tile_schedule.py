@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Diagnostics: record the per-tile schedule of the wave kernel (sf_set_tile_trace) for a config and
+save it as .npy for offline analysis (start/end ticks at 100 MHz, XCC id, HW_ID)."""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "sphereflake-raytracer_amd"))
+import sphereflake_amd as sf  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--K", type=float, default=0.25)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "tile_trace.npy"))
+    a = ap.parse_args()
+    with sf.Sphereflake(a.width, a.height) as s:
+        s.SetCamera(sf.config_camera(a.width, a.height, a.K))
+        s.tile_trace(True)
+        for _ in range(a.reps):
+            s.Render()
+        tr = s.tile_trace()
+        ph = s.phase_sums.astype(np.float64)
+    if ph.sum() > 0:
+        names = {1: "push", 6: "expand: node read + build", 2: "expand: child tests", 3: "head->self",
+                 4: "self test", 5: "pop"}
+        tot = ph[1:7].sum()
+        print("segment shares (stamp build, all reps):",
+              ", ".join(f"{names[k]} {100 * ph[k] / tot:.1f}%" for k in (1, 6, 2, 3, 4, 5)))
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    np.save(a.out, tr)
+    t0 = tr[:, 0].min()
+    dur = (tr[:, 1] - tr[:, 0]) / 100.0   # us
+    span = (tr[:, 1].max() - t0) / 100.0
+    print(f"tiles {len(tr)} span {span:.1f} us; tile us mean {dur.mean():.2f} p50 {np.median(dur):.2f} "
+          f"p99 {np.percentile(dur, 99):.2f} max {dur.max():.2f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -15,7 +15,9 @@
 #include "sf_internal.h"
 #include "sphereflake/sf.h"
 
-extern "C" __global__ void sf_trace_wave(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
+extern "C" __global__ void sf_trace_wave1(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
+extern "C" __global__ void sf_trace_wave2(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
+extern "C" __global__ void sf_trace_wave4(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
 extern "C" __global__ void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list, uint32_t* counters,
                                          uint32_t parity);
 extern "C" __global__ void sf_trace_ray(FrameArgs a);
@@ -69,6 +71,8 @@ struct sf_ctx {
     int64_t rays = 0;
     int last_hip = 0;
     int fixup_blocks = 256;
+    uint32_t waves_per_block = SF_TRACE_WAVES;   // tuning knob: env SF_TRACE_WAVES = 1 | 2 | 4
+    uint32_t levels_override = 0;                // tuning knob: env SF_LEVELS (LDS levels, 0 = adaptive)
     // frame-less progressive mode
     uint32_t* mt_state = nullptr;      // 624 words + next index (std::mt19937 layout)
     uint32_t* draws = nullptr;         // 2 per packet
@@ -79,6 +83,11 @@ struct sf_ctx {
     uint32_t prog_seed = 0;
     uint64_t prog_next = 0;            // Sobol counter the device MT stream is positioned at
     uint64_t ticket = 1;
+    // LDS provisioning hint: max depth seen by a completed render (pinned copy of the device
+    // stats word, refreshed asynchronously after every render). Only sizes the traversal stack;
+    // a tile that needs more is re-traced by sf_fixup_wave, so a stale hint costs time, never results.
+    int32_t* h_depth = nullptr;
+    uint64_t* tile_trace = nullptr;    // diagnostics: per tile {start, end, hw id}
 };
 
 #define SF_HIP(ctx, expr)                                        \
@@ -107,6 +116,8 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->draws);
     (void)hipFree(c->lanes);
     (void)hipFree(c->owner);
+    if (c->h_depth) (void)hipHostFree(c->h_depth);
+    (void)hipFree(c->tile_trace);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -115,6 +126,12 @@ static int upload_consts(sf_ctx* c)
 {
     std::memcpy(c->host_consts.child, c->child, sizeof c->child);
     sfhost::depth_tables(&c->host_consts.dt);
+    for (int d = 0; d < SF_DEPTH_TABLE; ++d) {
+        c->host_consts.depth4[d][0] = c->host_consts.dt.r2_bound[d];
+        c->host_consts.depth4[d][1] = c->host_consts.dt.r2_self[d];
+        c->host_consts.depth4[d][2] = c->host_consts.dt.scale[d];
+        c->host_consts.depth4[d][3] = c->host_consts.dt.lod[d];
+    }
     std::memcpy(c->host_consts.lut, kLut, sizeof kLut);
     sfhost::sobol_matrices(c->host_consts.sobol);
     SF_HIP(c, hipMemcpyAsync(c->consts, &c->host_consts, sizeof(DeviceConsts), hipMemcpyHostToDevice, c->stream));
@@ -176,6 +193,14 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     c->W = width;
     c->H = height;
     c->fixup_blocks = prop.multiProcessorCount;
+    if (const char* ev = std::getenv("SF_TRACE_WAVES")) {
+        const int w = std::atoi(ev);
+        c->waves_per_block = (w == 1 || w == 2 || w == 4) ? (uint32_t)w : SF_TRACE_WAVES;
+    }
+    if (const char* ev = std::getenv("SF_LEVELS")) {
+        const int l = std::atoi(ev);
+        c->levels_override = (l >= 2 && l <= SF_MAX_DEPTH_LIMIT) ? (uint32_t)l : 0u;
+    }
     DevGuard g(device);
     const size_t npx = (size_t)width * height;
     const size_t ntiles = (size_t)((width + 7) / 8) * ((height + 7) / 8);
@@ -194,6 +219,8 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if ((e = hipMalloc(&c->ovf_counters, 8)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->ovf_list, ntiles * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->consts, sizeof(DeviceConsts))) != hipSuccess) return fail(e);
+    if ((e = hipHostMalloc(&c->h_depth, 4, hipHostMallocDefault)) != hipSuccess) return fail(e);
+    *c->h_depth = -1;
     // G-buffer starts as glm vec4() = (0,0,0,0) (Sphereflake.cpp:48-49, type_vec4.inl:59-64)
     if ((e = hipMemsetAsync(c->pos, 0, npx * 16, c->stream)) != hipSuccess) return fail(e);
     if ((e = hipMemsetAsync(c->nrm, 0, npx * 16, c->stream)) != hipSuccess) return fail(e);
@@ -314,6 +341,11 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
     a.nrm = nrm;
     a.min_t = min_t;
     a.hit_index = hidx;
+    a.tile_trace = c->tile_trace;
+    if (c->tile_trace) {
+        const size_t ntr = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8);
+        a.phase_sums = c->tile_trace + 3 * ntr;
+    }
 
     const uint32_t ntiles = a.tiles_x * tile_rows;
     const uint32_t blocks = (ntiles + SF_WAVES_PER_BLOCK - 1) / SF_WAVES_PER_BLOCK;
@@ -323,16 +355,26 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
         SF_HIP(c, hipGetLastError());
     } else {
         const bool autod = p.max_depth == 0;
-        a.max_depth = autod ? kDefaultLevels : p.max_depth;
-        const size_t lds = (size_t)SF_WAVES_PER_BLOCK * (SF_LDS_ROOT + a.max_depth * SF_LDS_LEVEL) * 4;
+        uint32_t levels = kDefaultLevels;
+        const int32_t seen = *(volatile int32_t*)c->h_depth;
+        if (seen >= 0) levels = (uint32_t)seen + 1u < 4u ? 4u : (uint32_t)seen + 1u;
+        if (levels > SF_MAX_DEPTH_LIMIT) levels = SF_MAX_DEPTH_LIMIT;
+        if (c->levels_override) levels = c->levels_override;
+        a.max_depth = autod ? levels : p.max_depth;
+        const size_t lds = (size_t)SF_LDS_WAVE_FLOATS(a.max_depth) * 4;
         uint32_t* cnt = c->ovf_counters + c->parity;
-        hipLaunchKernelGGL(sf_trace_wave, dim3(blocks), dim3(256), lds, s, a, c->ovf_list, cnt);
+        const uint32_t wpb = c->waves_per_block;
+        const dim3 grid((ntiles + wpb - 1) / wpb), block(64 * wpb);
+        if (wpb == 1) hipLaunchKernelGGL(sf_trace_wave1, grid, block, lds, s, a, c->ovf_list, cnt);
+        else if (wpb == 2) hipLaunchKernelGGL(sf_trace_wave2, grid, block, 2 * lds, s, a, c->ovf_list, cnt);
+        else hipLaunchKernelGGL(sf_trace_wave4, grid, block, 4 * lds, s, a, c->ovf_list, cnt);
         SF_HIP(c, hipGetLastError());
-        const size_t lds_fix = (size_t)SF_WAVES_PER_BLOCK * (SF_LDS_ROOT + 31 * SF_LDS_LEVEL) * 4;
-        hipLaunchKernelGGL(sf_fixup_wave, dim3(c->fixup_blocks), dim3(256), lds_fix, s, a,
+        const size_t lds_fix = (size_t)SF_LDS_WAVE_FLOATS(SF_MAX_DEPTH_LIMIT) * 4;
+        hipLaunchKernelGGL(sf_fixup_wave, dim3(4 * c->fixup_blocks), dim3(64), lds_fix, s, a,
                            (const uint32_t*)c->ovf_list, c->ovf_counters, c->parity);
         SF_HIP(c, hipGetLastError());
         c->parity ^= 1u;
+        SF_HIP(c, hipMemcpyAsync(c->h_depth, c->stats, 4, hipMemcpyDeviceToHost, s));
     }
     uint32_t rows = 0;
     for (uint32_t b = p.band_index; b < bands; b += band_count) {
@@ -404,9 +446,8 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(1024), 0, s, c->mt_state, c->draws, 2 * packets);
     SF_HIP(c, hipGetLastError());
     const uint32_t waves = (packets + 7) / 8;
-    const uint32_t blocks = (waves + SF_WAVES_PER_BLOCK - 1) / SF_WAVES_PER_BLOCK;
-    const size_t lds = (size_t)SF_WAVES_PER_BLOCK * (SF_LDS_ROOT + 16 * SF_LDS_LEVEL) * 4;
-    hipLaunchKernelGGL(sf_progressive_trace, dim3(blocks), dim3(256), lds, s, a, (const uint32_t*)c->draws, counter0,
+    const size_t lds = (size_t)SF_LDS_WAVE_FLOATS(16) * 4;
+    hipLaunchKernelGGL(sf_progressive_trace, dim3(waves), dim3(64), lds, s, a, (const uint32_t*)c->draws, counter0,
                        packets, c->ticket, c->lanes, c->owner);
     SF_HIP(c, hipGetLastError());
     hipLaunchKernelGGL(sf_progressive_scatter, dim3((packets * 8 + 255) / 256), dim3(256), 0, s, a, packets, c->ticket,
@@ -440,6 +481,37 @@ int sf_download(sf_ctx* c, float* pos4, float* nrm4, float* min_t, uint32_t* hid
     if (nrm4) SF_HIP(c, hipMemcpy(nrm4, c->nrm, npx * 16, hipMemcpyDeviceToHost));
     if (min_t) SF_HIP(c, hipMemcpy(min_t, c->min_t, npx * 4, hipMemcpyDeviceToHost));
     if (hidx) SF_HIP(c, hipMemcpy(hidx, c->hit_index, npx * 4, hipMemcpyDeviceToHost));
+    return SF_OK;
+}
+
+int sf_set_tile_trace(sf_ctx* c, int enable)
+{
+    if (!c) return SF_EINVAL;
+    DevGuard g(c->device);
+    SF_HIP(c, hipStreamSynchronize(c->stream));
+    if (!enable) {
+        (void)hipFree(c->tile_trace);
+        c->tile_trace = nullptr;
+        return SF_OK;
+    }
+    if (!c->tile_trace) {
+        const size_t ntiles = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8);
+        SF_HIP(c, hipMalloc(&c->tile_trace, (ntiles * 3 + 8) * 8));
+        SF_HIP(c, hipMemset(c->tile_trace, 0, (ntiles * 3 + 8) * 8));
+    }
+    return SF_OK;
+}
+
+int sf_get_tile_trace(sf_ctx* c, uint64_t* out, size_t n)
+{
+    if (!c || !out || !c->tile_trace) return SF_EINVAL;
+    DevGuard g(c->device);
+    const size_t ntiles = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8);
+    if (n < ntiles * 3) return SF_EINVAL;
+    SF_HIP(c, hipStreamSynchronize(c->stream));
+    // n >= 3 * tiles + 8 also returns the 8 segment sums of stamp builds (zeros otherwise)
+    SF_HIP(c, hipMemcpy(out, c->tile_trace, (n >= ntiles * 3 + 8 ? ntiles * 3 + 8 : ntiles * 3) * 8,
+                        hipMemcpyDeviceToHost));
     return SF_OK;
 }
 

@@ -12,9 +12,21 @@
 
 #define SF_DEPTH_TABLE 33      // depths 0..32 (SF_MAX_DEPTH_LIMIT)
 #define SF_TILE 8              // a wave64 traces one 8x8 pixel tile
-#define SF_WAVES_PER_BLOCK 4   // 256-thread workgroups
-#define SF_LDS_ROOT 16         // floats reserved per wave for the root transform
-#define SF_LDS_LEVEL 108       // floats per traversal level: 9 children x 12 (3x4 column-major)
+#define SF_WAVES_PER_BLOCK 4   // 256-thread workgroups (per-ray kernel)
+#ifndef SF_TRACE_WAVES
+#define SF_TRACE_WAVES 4       // independent waves (tiles) per workgroup of the wave kernel
+#endif
+// Wave-coherent traversal LDS image, per wave (units: floats):
+//   [root: 16][tables: levels x 144][E: levels x 32][stack: levels x 4]
+// A transform is 16 floats: [cx cy cz cc | col0.xyz - | col1.xyz - | col2.xyz -] (cc = Dot(centre, centre)).
+#define SF_LDS_ROOT 16
+#define SF_LDS_CHILD 16
+#define SF_LDS_TABLE (9 * SF_LDS_CHILD)   // the 9 child transforms of the node open at a level
+#define SF_LDS_E 32                       // 64 lanes x u16: per-lane child-expand bits of that node
+#define SF_LDS_STACK 4                    // pending children, child cursor, heap index lo/hi
+#define SF_LDS_LEVEL (SF_LDS_TABLE + SF_LDS_E + SF_LDS_STACK)
+#define SF_LDS_DEPTH (4 * SF_DEPTH_TABLE)   // per-depth constants, staged in front of the image
+#define SF_LDS_WAVE_FLOATS(levels) (SF_LDS_DEPTH + SF_LDS_ROOT + (levels) * SF_LDS_LEVEL)
 
 struct DepthTables {
     float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)
@@ -27,6 +39,7 @@ struct DepthTables {
 struct DeviceConsts {
     float child[9][16];               // unit child frames, glm column-major (Sphereflake.cpp:216-249)
     DepthTables dt;
+    float depth4[SF_DEPTH_TABLE][4];  // the same, interleaved {r2_bound, r2_self, scale, lod} (staged into LDS)
     uint32_t lut[2048];               // x86 rsqrtps table (rsqrtps_lut.inc)
     uint32_t sobol[2][52];            // Sobol direction numbers, dims 0 and 1 (Sobol.cpp:34-39, 57-162)
 };
@@ -56,6 +69,8 @@ struct FrameArgs {
     float* min_t;                     // optional aux channel
     uint32_t* hit_index;              // optional aux channel (heap index 9n+1+i, 0xffffffff = miss)
     int32_t* stats;                   // [0] max depth (atomicMax), [1] closest key (atomicMin), [2] overflow count
+    uint64_t* tile_trace;             // diagnostics (NULL = off): per tile {start, end} s_memrealtime, hw id
+    uint64_t* phase_sums;             // diagnostics, stamp builds only (make PHASES=1): 8 segment sums
 };
 
 namespace sfhost {

@@ -121,13 +121,23 @@ __device__ __forceinline__ float wave_min(float v)
     return v;
 }
 
+// Wave64 ballot straight on the compare mask (no bool -> int -> compare round trip).
+__device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+// Exact near root, kept out of line so the compiler cannot if-convert the rare exact path of the
+// fast LOD bracket into every child test.
+__device__ __attribute__((noinline)) float near_root_exact(float tca, float d2, float R2)
+{
+    return near_root(tca, d2, R2);
+}
+
 // "Any lane of my group": a group is the lane itself (per-ray semantics) or the 8 lanes of a
 // reference AVX packet (packet semantics: movemask early-outs, SIMD_AVX.h:247,255, Sphereflake.h:140,149,207).
 template <bool PACKET>
 __device__ __forceinline__ bool group_any(bool p)
 {
     if constexpr (PACKET) {
-        const uint64_t b = __ballot(p);
+        const uint64_t b = wave_ballot(p);
         return ((b >> (threadIdx.x & 56u)) & 0xffull) != 0ull;
     } else {
         return p;
@@ -137,171 +147,278 @@ __device__ __forceinline__ bool group_any(bool p)
 // ------------------------------------------------------------------------------------------
 // Wave-coherent traversal of IntersectSphereflake (Sphereflake.h:86-226).
 //
-// LDS per wave: [root transform: 16 floats][level 0 .. levels-1: 9 children x 12 floats].
-// Level L holds the world transforms of the 9 children of the node currently open at depth L,
-// as 3x4 column-major (col0.xyz, col1.xyz, col2.xyz, col3.xyz = centre).
-// Uniform traversal state: depth d of the node under evaluation, packed child cursors (4 bits
-// per level), heap index of the current node, LDS offset of its transform. Per-lane state:
-// ebits bit L = this lane (or its packet) expanded the open node at depth L.
+// The DFS runs over EXPANDED nodes only (nodes that passed bounding sphere + LOD for at least one
+// lane of the wave). When a node expands, the wave
+//   1. builds its 9 child world transforms cooperatively into the LDS table of its level
+//      (36 lanes: one column each; child translation scaled by (4/3) r, world = parent * child,
+//      SIMD_AVX.h:59-81, Sphereflake.h:162-172) plus Dot(centre, centre) of each child;
+//   2. evaluates the bounding + LOD tests of all 9 children at once (independent, so they overlap
+//      instead of forming a serial chain), giving each lane a 9-bit "child expands" vector E and
+//      the wave a 9-bit "pending" mask of children some lane expands.
+// Children are then entered in index order; a node's own sphere is tested after all its children
+// (post-order, Sphereflake.h:174-224), exactly the reference's per-ray visiting order. Children that
+// no lane expands cost only their (batched) bounding test, as in the reference.
 //
-// Per node (group = lane for per-ray semantics, 8-lane packet for packet semantics):
+// Per node (group = the lane itself for per-ray semantics, the 8 lanes of a reference AVX packet
+// for packet semantics):
 //   bounding   hb = active && any_g(tca >= 0) && any_g(d2 <= (2r)^2)
 //   LOD        ex = hb && any_g(t < T_d)          [T_d exact threshold of sqrtf(t/r) < 70 || t < 0]
-//   children   if any lane ex: build 9 child transforms, descend
-//   self       hs = ex && any_g(tca >= 0) && any_g(d2 <= r^2); accept lanes with d2 <= r^2 && t < minT
-// For per-ray groups these are exactly the per-lane tests of the reference.
+//   self       hs = active && any_g(tca >= 0) && any_g(d2 <= r^2); accept lanes with d2 <= r^2 && t < minT
+// For per-ray groups these are exactly the reference's per-lane tests.
 // ------------------------------------------------------------------------------------------
+struct TraverseLds {
+    float* base;
+    uint32_t levels;
+    // {(2r)^2, r^2, (4/3) r, T} of a depth: one uniform ds_read_b128
+    __device__ __forceinline__ float4 depth(uint32_t d) const { return reinterpret_cast<const float4*>(base)[d]; }
+    __device__ __forceinline__ float* img() const { return base + SF_LDS_DEPTH; }
+    __device__ __forceinline__ float* root() const { return img(); }
+    __device__ __forceinline__ float* table(uint32_t lvl) const { return img() + SF_LDS_ROOT + lvl * SF_LDS_TABLE; }
+    __device__ __forceinline__ uint16_t* E(uint32_t lvl) const
+    {
+        return reinterpret_cast<uint16_t*>(img() + SF_LDS_ROOT + levels * SF_LDS_TABLE + lvl * SF_LDS_E);
+    }
+    __device__ __forceinline__ uint32_t* stack(uint32_t lvl) const
+    {
+        return reinterpret_cast<uint32_t*>(img() + SF_LDS_ROOT + levels * (SF_LDS_TABLE + SF_LDS_E) + lvl * SF_LDS_STACK);
+    }
+};
+
+__device__ __forceinline__ void lds_fence()
+{
+    __builtin_amdgcn_wave_barrier();
+    __asm__ volatile("" ::: "memory");
+}
+
+// Diagnostic build only (make PHASES=1): s_memtime stamps at the DFS segment boundaries, summed per
+// segment into 64-bit scalars and added to phase_sums once per wave. Segments: 0->1 push bookkeeping,
+// 1->2 expand (node read, build, child tests), 3->4 self test, 4->5 pop; 0 is taken at the loop head.
+// Never compiled into the product library; read its SHARES, not its run time.
+#ifdef SF_PHASE_STAMPS
+#define SF_STAMP_DECL uint64_t ph_last = __builtin_amdgcn_s_memtime(), ph_sum[7] = {0, 0, 0, 0, 0, 0, 0}
+#define SF_STAMP(k)                                                                            \
+    do {                                                                                       \
+        uint64_t t_;                                                                           \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        __asm__ volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        if ((k) != 0) ph_sum[k] += t_ - ph_last;                                               \
+        ph_last = t_;                                                                          \
+    } while (0)
+#define SF_STAMP_FLUSH(p)                                                                      \
+    do {                                                                                       \
+        if ((p) && lane == 0u) {                                                               \
+            atomicAdd((unsigned long long*)(p) + 1, ph_sum[1]);                                \
+            atomicAdd((unsigned long long*)(p) + 2, ph_sum[2]);                                \
+            atomicAdd((unsigned long long*)(p) + 3, ph_sum[3]);                                \
+            atomicAdd((unsigned long long*)(p) + 4, ph_sum[4]);                                \
+            atomicAdd((unsigned long long*)(p) + 5, ph_sum[5]);                                \
+            atomicAdd((unsigned long long*)(p) + 6, ph_sum[6]);                                \
+        }                                                                                      \
+    } while (0)
+#else
+#define SF_STAMP_DECL
+#define SF_STAMP(k)
+#define SF_STAMP_FLUSH(p) (void)(p)
+#endif
+
 template <bool PACKET>
-__device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ L,
+__device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ Lbase,
                                          uint32_t levels, float dx, float dy, float dz, bool valid, HitState& h,
-                                         int32_t& maxd, bool& overflowed)
+                                         int32_t& maxd, bool& overflowed, uint64_t* phase_sums = nullptr)
 {
     const uint32_t lane = threadIdx.x & 63u;
+    const TraverseLds L{ Lbase, levels };
+    SF_STAMP_DECL;
 
-    // root transform -> LDS (lanes 0..11)
-    if (lane < 12u) {
-        float v = 0.f;
-#pragma unroll
-        for (int k = 0; k < 12; ++k) v = (lane == (uint32_t)k) ? root[k] : v;
-        L[lane] = v;
-    }
-
-    // This lane's two entries of the cooperative child build: e = lane and e = lane + 64 (< 108).
-    // Entry e of a level = child i = e / 12, column c = (e % 12) / 3, row r = e % 3.
-    float bA[4], bB[4];
-    uint32_t rA, rB;
-    bool tA, tB;
-    {
-        const uint32_t e = lane, i = e / 12u, c = (e % 12u) / 3u;
-        rA = e % 3u;
-        tA = (c == 3u);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bA[j] = K->child[i][4u * c + j];
-    }
-    const bool hasB = lane < (SF_LDS_LEVEL - 64u);
-    {
-        const uint32_t e = hasB ? lane + 64u : 0u, i = e / 12u, c = (e % 12u) / 3u;
-        rB = e % 3u;
-        tB = (c == 3u);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bB[j] = K->child[i][4u * c + j];
-    }
+    // per-depth constants -> LDS (lanes 0..32): uniform reads later cost one ds_read_b128
+    if (lane < (uint32_t)SF_DEPTH_TABLE)
+        reinterpret_cast<float4*>(Lbase)[lane] = reinterpret_cast<const float4*>(K->depth4)[lane];
 
     h.minT = FLT_MAX;
     h.cx = h.cy = h.cz = 0.f;
     h.index = 0xffffffffu;
     h.hit = false;
 
-    uint32_t ebits = 0;       // per lane
-    uint32_t d = 0;           // uniform: depth of the node being evaluated
-    uint64_t cis = 0;         // uniform: child cursor of level L at bits 4L..4L+3 (levels < 16)
-    uint64_t cis_hi = 0;      //          levels 16..30
-    uint64_t idx = 0;         // uniform: heap index of the node (root 0, child i of n: 9n+1+i)
-    uint32_t nbase = 0;       // uniform: LDS offset of the current node's transform
+    // ---- root node (depth 0): bounding sphere + LOD, centre straight from the kernel arguments
+    const float rcx = root[9], rcy = root[10], rcz = root[11];
+    const float rcc = (rcx * rcx + rcy * rcy) + rcz * rcz;
+    bool ex0;
+    {
+        const float tca = (rcx * dx + rcy * dy) + rcz * dz;
+        const float d2 = rcc - tca * tca;
+        const float R2b = K->dt.r2_bound[0];
+        const bool hb = valid && group_any<PACKET>(tca >= 0.0f) && group_any<PACKET>(d2 <= R2b);
+        ex0 = hb && group_any<PACKET>(near_root(tca, d2, R2b) < K->dt.lod[0]);
+    }
+    if (!wave_ballot(ex0)) return;
+    maxd = 0;
 
-    __builtin_amdgcn_wave_barrier();
-    __asm__ volatile("" ::: "memory");
+    // root transform -> LDS in the transform layout (lanes 0..15)
+    if (lane < 16u) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            float rk = 0.f;
+            if (k < 3) rk = root[9 + k];
+            else if (k == 3) rk = rcc;
+            else if ((k & 3) != 3) rk = root[3 * ((k >> 2) - 1) + (k & 3)];
+            v = (lane == (uint32_t)k) ? rk : v;
+        }
+        L.root()[lane] = v;
+    }
 
-    auto cursor = [&](uint32_t lvl) -> uint32_t {
-        return lvl < 16u ? (uint32_t)(cis >> (4u * lvl)) & 15u : (uint32_t)(cis_hi >> (4u * (lvl - 16u))) & 15u;
-    };
-    auto set_cursor = [&](uint32_t lvl, uint32_t v) {
-        if (lvl < 16u) cis = (cis & ~(15ull << (4u * lvl))) | ((uint64_t)v << (4u * lvl));
-        else cis_hi = (cis_hi & ~(15ull << (4u * (lvl - 16u)))) | ((uint64_t)v << (4u * (lvl - 16u)));
-    };
+    // this lane's column of the cooperative child build: child i = lane / 4, column c = lane % 4
+    const bool builder = lane < 36u;
+    const uint32_t bi = builder ? lane >> 2 : 0u, bc = lane & 3u;
+    float b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = K->child[bi][4u * bc + j];
+    float* const slot_base = L.table(0) + bi * SF_LDS_CHILD + (bc == 3u ? 0u : 4u + 4u * bc);
 
-    for (;;) {
-        // ---- evaluate node at depth d: bounding sphere (2r) + LOD (Sphereflake.h:97-153)
-        {
-            const bool active = (d == 0u) ? valid : (((ebits >> (d - 1u)) & 1u) != 0u);
-            const float cx = L[nbase + 9], cy = L[nbase + 10], cz = L[nbase + 11];
-            const float tca = (cx * dx + cy * dy) + cz * dz;                 // Dot(centre, dir)
-            const float cc = (cx * cx + cy * cy) + cz * cz;                  // Dot(centre, centre)
-            const float d2 = cc - tca * tca;
-            const float R2b = K->dt.r2_bound[d];
-            const bool hb = active && group_any<PACKET>(tca >= 0.0f) && group_any<PACKET>(d2 <= R2b);
-            bool ex = false;
-            if (__ballot(hb)) {
-                const float tb = near_root(tca, d2, R2b);
-                ex = hb && group_any<PACKET>(tb < K->dt.lod[d]);            // exact LOD threshold
-            }
-            const uint64_t me = __ballot(ex);
-            ebits = ex ? (ebits | (1u << d)) : (ebits & ~(1u << d));
-            if (me) {
-                maxd = (int32_t)d > maxd ? (int32_t)d : maxd;                // Sphereflake.h:157-160
-                if (d < levels) {
-                    // ---- build the 9 child world transforms into level d (Sphereflake.h:162-172):
-                    // child translation scaled by (4/3) r, world = parent * child (SIMD_AVX.h:59-81)
-                    const float s = K->dt.scale[d];
-                    const uint32_t lb = SF_LDS_ROOT + d * SF_LDS_LEVEL;
-                    {
-                        const float a0 = L[nbase + rA], a1 = L[nbase + 3 + rA], a2 = L[nbase + 6 + rA],
-                                    a3 = L[nbase + 9 + rA];
-                        const float b0 = tA ? bA[0] * s : bA[0];
-                        const float b1 = tA ? bA[1] * s : bA[1];
-                        const float b2 = tA ? bA[2] * s : bA[2];
-                        L[lb + lane] = ((a0 * b0 + a1 * b1) + a2 * b2) + a3 * bA[3];
-                    }
-                    if (hasB) {
-                        const float a0 = L[nbase + rB], a1 = L[nbase + 3 + rB], a2 = L[nbase + 6 + rB],
-                                    a3 = L[nbase + 9 + rB];
-                        const float b0 = tB ? bB[0] * s : bB[0];
-                        const float b1 = tB ? bB[1] * s : bB[1];
-                        const float b2 = tB ? bB[2] * s : bB[2];
-                        L[lb + 64u + lane] = ((a0 * b0 + a1 * b1) + a2 * b2) + a3 * bB[3];
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    __asm__ volatile("" ::: "memory");
-                    set_cursor(d, 0u);
-                    d += 1u;
-                    idx = 9u * idx + 1u;
-                    nbase = lb;
-                    continue;   // evaluate child 0
-                }
-                // needs a deeper stack than provisioned: drop the subtree, flag the tile
-                overflowed = true;
-                ebits &= ~(1u << d);
+    // ---- expand: build the children of the node at `node` (depth d) into table(d), then batch-
+    // evaluate them (depth d+1) for the lanes in `act`. Returns this lane's 9-bit E; *pend = wave mask.
+    auto expand = [&](const float* node, uint32_t d, bool act, uint32_t& pend) -> uint32_t {
+        d = __builtin_amdgcn_readfirstlane(d);   // wave-uniform: depth tables come by scalar loads
+        lds_fence();
+        const float4 pc = *reinterpret_cast<const float4*>(node);
+        const float4 p0 = *reinterpret_cast<const float4*>(node + 4);
+        const float4 p1 = *reinterpret_cast<const float4*>(node + 8);
+        const float4 p2 = *reinterpret_cast<const float4*>(node + 12);
+        const float4 dtn = L.depth(d);            // this node's depth: (4/3) r
+        const float4 dtc = L.depth(d + 1u);       // its children's: (2r)^2, T
+        if (builder) {
+            const float s = dtn.z;
+            const float b0 = bc == 3u ? b[0] * s : b[0];
+            const float b1 = bc == 3u ? b[1] * s : b[1];
+            const float b2 = bc == 3u ? b[2] * s : b[2];
+            const float x = ((p0.x * b0 + p1.x * b1) + p2.x * b2) + pc.x * b[3];
+            const float y = ((p0.y * b0 + p1.y * b1) + p2.y * b2) + pc.y * b[3];
+            const float z = ((p0.z * b0 + p1.z * b1) + p2.z * b2) + pc.z * b[3];
+            const float w = bc == 3u ? (x * x + y * y) + z * z : 0.0f;
+            *reinterpret_cast<float4*>(slot_base + d * SF_LDS_TABLE) = make_float4(x, y, z, w);
+        }
+        lds_fence();
+        SF_STAMP(6);
+        const float* tab = L.table(d);
+        const float R2b = dtc.x;
+        const float T = dtc.w;
+        // all 9 centres first: straight-line code, so the reads overlap and the tests interleave
+        float4 c[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) c[i] = *reinterpret_cast<const float4*>(tab + i * SF_LDS_CHILD);
+        uint32_t e = 0, pm = 0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const float tca = (c[i].x * dx + c[i].y * dy) + c[i].z * dz;
+            const float d2 = c[i].w - tca * tca;
+            const bool hb = act & group_any<PACKET>(tca >= 0.0f) & group_any<PACKET>(d2 <= R2b);
+            if (wave_ballot(hb)) {   // ~1/3 of the children: only then the LOD test
+                // LOD on t = fl(tca - sqrt_rn(R2b - d2)) (SIMD_AVX.h:260-267; t0 <= t1 picks t1 for
+                // thc >= 0). Fast bracket: the hardware sqrt is within 2 ulp of sqrt_rn and t is
+                // monotone in it, so [fl(tca - (s + 2ulp)), fl(tca - (s - 2ulp))] contains t; the
+                // exact path runs only when T falls inside (or the sqrt argument is tiny).
+                const float x = R2b - d2;
+                const float s = __builtin_amdgcn_sqrtf(x);
+                const float s_lo = __uint_as_float((uint32_t)max((int32_t)__float_as_uint(s) - 2, 0));
+                const float s_hi = __uint_as_float(__float_as_uint(s) + 2u);
+                const float t_hi = tca - s_lo;           // >= t
+                const float t_lo = tca - s_hi;           // <= t
+                // a stand-in for t on the same side of T as t whenever the bracket decides
+                float t_dec = t_hi < T ? t_hi : t_lo;
+                const bool undecided = hb & ((!(t_hi < T) & !(t_lo >= T)) | (x < 0x1p-96f));
+                if (wave_ballot(undecided)) t_dec = undecided ? near_root_exact(tca, d2, R2b) : t_dec;
+                const bool exi = hb & group_any<PACKET>(t_dec < T);
+                const uint64_t mi = wave_ballot(exi);
+                e |= exi ? (1u << i) : 0u;
+                pm |= (mi != 0ull ? 1u : 0u) << i;
             }
         }
-        // ---- advance: next sibling, or close finished nodes with their own sphere test
-        bool finished = false;
-        for (;;) {
-            if (d == 0u) { finished = true; break; }
-            const uint32_t p = d - 1u;
-            const uint32_t ci = cursor(p);
-            if (ci < 8u) {
-                set_cursor(p, ci + 1u);
-                idx += 1u;
-                nbase += 12u;
-                break;
+        pend = pm;
+        return e;
+    };
+
+    uint32_t d = 0;                 // uniform: depth of the open (expanded) node
+    uint32_t cN = 0;                // uniform: its index in the parent's table
+    uint64_t idxN = 0;              // uniform: its heap index (root 0, child i of n: 9n+1+i)
+    const float* node = L.root();   // uniform: its transform
+    uint32_t actbits = ex0 ? 1u : 0u;   // per lane: bit L = active at the open node of depth L
+    uint32_t pend;
+    uint32_t eN = expand(node, 0u, ex0, pend);
+
+    for (;;) {
+        d = __builtin_amdgcn_readfirstlane(d);
+        pend = __builtin_amdgcn_readfirstlane(pend);
+        SF_STAMP(0);
+        if (pend) {
+            const uint32_t c = __builtin_ctz(pend);
+            pend &= pend - 1u;
+            if (d + 1u >= levels) {        // needs a deeper stack than provisioned: flag the tile
+                overflowed = true;
+                continue;
             }
-            // all 9 children of the node at depth p done: self test (Sphereflake.h:174-224)
-            idx = (idx - 9u) / 9u;
-            d = p;
-            nbase = p == 0u ? 0u : SF_LDS_ROOT + (p - 1u) * SF_LDS_LEVEL + cursor(p - 1u) * 12u;
-            const bool act = ((ebits >> p) & 1u) != 0u;
-            const float cx = L[nbase + 9], cy = L[nbase + 10], cz = L[nbase + 11];
-            const float tca = (cx * dx + cy * dy) + cz * dz;
-            const float cc = (cx * cx + cy * cy) + cz * cz;
-            const float d2 = cc - tca * tca;
-            const float R2s = K->dt.r2_self[p];
+            // save the open node's state, enter child c
+            if (lane == 0u) {
+                uint32_t* st = L.stack(d);
+                st[0] = pend;
+                st[1] = cN;
+                st[2] = (uint32_t)idxN;
+                st[3] = (uint32_t)(idxN >> 32);
+            }
+            L.E(d)[lane] = (uint16_t)eN;
+            const bool a = ((eN >> c) & 1u) != 0u;
+            const uint32_t bit = 1u << (d + 1u);
+            actbits = a ? (actbits | bit) : (actbits & ~bit);
+            idxN = 9u * idxN + 1u + c;
+            cN = c;
+            node = L.table(d) + c * SF_LDS_CHILD;
+            d += 1u;
+            maxd = (int32_t)d > maxd ? (int32_t)d : maxd;            // Sphereflake.h:157-160
+            SF_STAMP(1);
+            eN = expand(node, d, a, pend);
+            SF_STAMP(2);
+            continue;
+        }
+        // ---- all children done: the open node's own sphere (Sphereflake.h:174-224)
+        SF_STAMP(3);
+        {
+            const bool act = ((actbits >> d) & 1u) != 0u;
+            const float4 c = *reinterpret_cast<const float4*>(node);
+            const float tca = (c.x * dx + c.y * dy) + c.z * dz;
+            const float d2 = c.w - tca * tca;
+            const float R2s = L.depth(d).y;
             const bool in = d2 <= R2s;
             const bool hs = act && group_any<PACKET>(tca >= 0.0f) && group_any<PACKET>(in);
-            if (__ballot(hs)) {
+            if (wave_ballot(hs)) {
                 const float ts = near_root(tca, d2, R2s);
-                const bool acc = hs && in && (ts < h.minT);                  // strict: first wins ties
+                const bool acc = hs && in && (ts < h.minT);           // strict: the first wins ties
                 if (acc) {
                     h.minT = ts;
-                    h.cx = cx;
-                    h.cy = cy;
-                    h.cz = cz;
-                    h.index = (uint32_t)idx;
+                    h.cx = c.x;
+                    h.cy = c.y;
+                    h.cz = c.z;
+                    h.index = (uint32_t)idxN;
                     h.hit = true;
                 }
             }
         }
-        if (finished) break;
+        SF_STAMP(4);
+        if (d == 0u) break;
+        // ---- back to the parent
+        d -= 1u;
+        lds_fence();
+        {
+            const uint32_t* st = L.stack(d);
+            pend = __builtin_amdgcn_readfirstlane(st[0]);
+            cN = __builtin_amdgcn_readfirstlane(st[1]);
+            idxN = (uint64_t)__builtin_amdgcn_readfirstlane(st[2]) | ((uint64_t)__builtin_amdgcn_readfirstlane(st[3]) << 32);
+        }
+        eN = L.E(d)[lane];
+        node = d == 0u ? L.root() : L.table(d - 1u) + cN * SF_LDS_CHILD;
+        (void)__builtin_amdgcn_readfirstlane(eN);   // (stamp builds: close the pop segment after its reads)
+        SF_STAMP(5);
     }
+    SF_STAMP_FLUSH(phase_sums);
 }
 
 struct Tile {
@@ -345,13 +462,25 @@ __device__ __forceinline__ void trace_tile(const FrameArgs& a, float* __restrict
     const DeviceConsts* __restrict__ K = a.consts;
     const uint32_t lane = threadIdx.x & 63u;
     const Tile t = tile_of(a, tile, lane);
+    const uint64_t t_start = a.tile_trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     float dx, dy, dz;
     ray_dir(a, (float)t.x, (float)t.y, dx, dy, dz, K->lut);
 
     HitState h;
     int32_t maxd = -1;
     bool overflowed = false;
-    traverse<false>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed);
+    traverse<false>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed, FIXUP ? nullptr : a.phase_sums);
+    if (a.tile_trace && lane == 0u && !FIXUP) {
+        // diagnostics only: never read by the kernel, never feeds an output value
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        uint32_t hw;
+        __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        uint32_t xcc;
+        __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        a.tile_trace[3u * tile + 0u] = t_start;
+        a.tile_trace[3u * tile + 1u] = t_end;
+        a.tile_trace[3u * tile + 2u] = ((uint64_t)xcc << 32) | hw;
+    }
 
     if (!FIXUP && overflowed && lane == 0u) {
         // a deeper re-trace (sf_fixup_wave) rewrites this whole tile
@@ -371,29 +500,41 @@ __device__ __forceinline__ void trace_tile(const FrameArgs& a, float* __restrict
 
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(256) void sf_trace_wave(FrameArgs a, uint32_t* overflow_list,
-                                                                uint32_t* overflow_count)
+// One wave (one 8x8 tile) per workgroup: LDS is the occupancy limit, so the finest granularity packs best.
+// WAVES independent waves per workgroup (adjacent tiles, similar cost); the host picks the variant.
+template <int WAVES>
+__device__ __forceinline__ void trace_wave_body(const FrameArgs& a, uint32_t* overflow_list, uint32_t* overflow_count)
 {
     extern __shared__ float lds[];
     const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t per_wave = SF_LDS_ROOT + a.max_depth * SF_LDS_LEVEL;
-    const uint32_t tile = blockIdx.x * SF_WAVES_PER_BLOCK + wv;
+    const uint32_t tile = blockIdx.x * WAVES + wv;
     if (tile >= a.tiles_x * a.tile_rows) return;
-    trace_tile<false>(a, lds + wv * per_wave, tile, a.max_depth, overflow_list, overflow_count);
+    trace_tile<false>(a, lds + wv * SF_LDS_WAVE_FLOATS(a.max_depth), tile, a.max_depth, overflow_list, overflow_count);
+}
+
+extern "C" __global__ __launch_bounds__(64) void sf_trace_wave1(FrameArgs a, uint32_t* ol, uint32_t* oc)
+{
+    trace_wave_body<1>(a, ol, oc);
+}
+extern "C" __global__ __launch_bounds__(128) void sf_trace_wave2(FrameArgs a, uint32_t* ol, uint32_t* oc)
+{
+    trace_wave_body<2>(a, ol, oc);
+}
+extern "C" __global__ __launch_bounds__(256) void sf_trace_wave4(FrameArgs a, uint32_t* ol, uint32_t* oc)
+{
+    trace_wave_body<4>(a, ol, oc);
 }
 
 // Re-traces flagged tiles with SF_MAX_LEVELS levels. Grid-stride over the list; reads this
 // render's counter and zeroes the other one (the next render's), so no memset is needed.
-extern "C" __global__ __launch_bounds__(256) void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list,
-                                                                uint32_t* counters, uint32_t parity)
+extern "C" __global__ __launch_bounds__(64) void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list,
+                                                               uint32_t* counters, uint32_t parity)
 {
     extern __shared__ float lds[];
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t per_wave = SF_LDS_ROOT + SF_MAX_LEVELS * SF_LDS_LEVEL;
     if (blockIdx.x == 0 && threadIdx.x == 0) counters[parity ^ 1u] = 0u;
     const uint32_t n = counters[parity];
-    for (uint32_t i = blockIdx.x * SF_WAVES_PER_BLOCK + wv; i < n; i += gridDim.x * SF_WAVES_PER_BLOCK)
-        trace_tile<true>(a, lds + wv * per_wave, overflow_list[i], SF_MAX_LEVELS, nullptr, nullptr);
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x)
+        trace_tile<true>(a, lds, overflow_list[i], SF_MAX_LEVELS, nullptr, nullptr);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -498,7 +639,7 @@ extern "C" __global__ __launch_bounds__(256) void sf_trace_ray(FrameArgs a)
     int32_t md = maxd;
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) md = max(md, __shfl_xor(md, m, 64));
-    const bool anyov = __ballot(overflowed) != 0;
+    const bool anyov = wave_ballot(overflowed) != 0;
     if (lane == 0u) {
         if (md >= 0) atomicMax(&a.stats[0], md);
         atomicMin(&a.stats[1], sf_float_key(closest));
@@ -571,16 +712,16 @@ __device__ __forceinline__ float sobol_sample(uint64_t index, const uint32_t* __
 // the footprint of Sphereflake.cpp:143-147 around (x0, y0) drawn at Sobol index counter0 + j with
 // scrambles draws[2j], draws[2j+1] (Sphereflake.cpp:139-141). Results are staged per lane; the
 // owner word of each pixel keeps the highest ticket, so the scatter reproduces sequential order.
-extern "C" __global__ __launch_bounds__(256) void sf_progressive_trace(FrameArgs a, const uint32_t* draws,
+extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace(FrameArgs a, const uint32_t* draws,
                                                                        uint64_t counter0, uint32_t packets,
                                                                        uint64_t ticket0, PacketLane* lanes,
                                                                        unsigned long long* owner)
 {
     extern __shared__ float lds[];
     const DeviceConsts* __restrict__ K = a.consts;
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint32_t packet = (blockIdx.x * SF_WAVES_PER_BLOCK + wv) * 8u + (lane >> 3);
-    if ((blockIdx.x * SF_WAVES_PER_BLOCK + wv) * 8u >= packets) return;   // wave-uniform
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t packet = blockIdx.x * 8u + (lane >> 3);
+    if (blockIdx.x * 8u >= packets) return;   // wave-uniform
     const bool valid = packet < packets;
     const uint32_t q = lane & 7u;
     float x0 = 0.f, y0 = 0.f;
@@ -599,8 +740,7 @@ extern "C" __global__ __launch_bounds__(256) void sf_progressive_trace(FrameArgs
     HitState h;
     int32_t maxd = -1;
     bool overflowed = false;
-    traverse<true>(K, a.root, lds + wv * (SF_LDS_ROOT + SF_PROGRESSIVE_LEVELS * SF_LDS_LEVEL), SF_PROGRESSIVE_LEVELS,
-                   dx, dy, dz, valid, h, maxd, overflowed);
+    traverse<true>(K, a.root, lds, SF_PROGRESSIVE_LEVELS, dx, dy, dz, valid, h, maxd, overflowed);
 
     PacketLane out;
     shade(dx, dy, dz, h, K->lut, out.px, out.py, out.pz, out.nx, out.ny, out.nz);
@@ -613,7 +753,7 @@ extern "C" __global__ __launch_bounds__(256) void sf_progressive_trace(FrameArgs
     if (inb) atomicMax(owner + pix, (unsigned long long)(ticket0 + packet));
 
     const float closest = wave_min(inb ? h.minT : FLT_MAX);
-    const bool anyov = __ballot(overflowed) != 0ull;
+    const bool anyov = wave_ballot(overflowed) != 0ull;
     if (lane == 0u) {
         if (maxd >= 0) atomicMax(&a.stats[0], maxd);
         atomicMin(&a.stats[1], sf_float_key(closest));

@@ -24,7 +24,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT_DIR = os.path.dirname(PKG_DIR)                 # sphereflake-raytracer_amd/
-LIB_PATH = os.path.join(ROOT_DIR, "build", "libsphereflake_hip.so")
+# SF_LIB selects another build of the same library (e.g. the stamp diagnostics build_phases/)
+LIB_PATH = os.environ.get("SF_LIB") or os.path.join(ROOT_DIR, "build", "libsphereflake_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(ROOT_DIR), "include", "sphereflake", "sf.h")
 
 SF_OK, SF_EINVAL, SF_ENOMEM, SF_EHIP, SF_ENODEV, SF_ENOVIEW, SF_EDEPTH, SF_ESTATE = 0, -1, -2, -3, -4, -5, -6, -7
@@ -86,6 +87,8 @@ SIGNATURES = {
     "sf_root_transform": (ctypes.c_int, [_F, _F]),
     "sf_depth_constants": (ctypes.c_int, [ctypes.c_uint32, _F, _F]),
     "sf_rsqrtps": (ctypes.c_float, [ctypes.c_float]),
+    "sf_set_tile_trace": (ctypes.c_int, [_CTX, ctypes.c_int]),
+    "sf_get_tile_trace": (ctypes.c_int, [_CTX, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]),
     "sf_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "sf_last_hip_error": (ctypes.c_int, [_CTX]),
     "sf_abi_version": (ctypes.c_int, []),
@@ -337,6 +340,19 @@ class Sphereflake:
     def GetGBuffer(self) -> GBuffer:
         pos, nrm, _, _ = self.download()
         return GBuffer(pos, nrm)
+
+    def tile_trace(self, enable: bool | None = None):
+        """Diagnostics: enable per-tile timing, or (enable=None) fetch [tiles, 3] uint64
+        (start, end in 100 MHz ticks, (xcc << 32) | HW_ID) of the last render."""
+        if enable is not None:
+            _check(lib().sf_set_tile_trace(self._ctx, int(bool(enable))), "sf_set_tile_trace", self._ctx)
+            return None
+        n = ((self.width + 7) // 8) * ((self.height + 7) // 8)
+        out = np.zeros(3 * n + 8, np.uint64)
+        _check(lib().sf_get_tile_trace(self._ctx, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), out.size),
+               "sf_get_tile_trace", self._ctx)
+        self.phase_sums = out[3 * n:]          # segment cycle sums of stamp builds (zeros otherwise)
+        return out[:3 * n].reshape(n, 3)
 
     # stats (Sphereflake.h:30-58) --------------------------------------------
     def stats(self) -> sf_stats:
