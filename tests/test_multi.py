@@ -1,0 +1,100 @@
+"""Multi-rank host logic of the row-band path on CPU: world_size 2 and 3 over
+gloo. Each rank produces the slab of the bands it owns, with the CPU oracle standing in for the
+GPU (the checker only, as on the GPU box the slab comes from sf_render_to). Slabs are gathered and
+reassembled on rank 0, and must equal the golden full frame bit for bit. Stats reduce as the
+reference counters would."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import load_frame, load_npz
+from sphereflake_amd import shard
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, name, band_rows, errq):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from oracle import pyoracle
+        fx = load_frame(name)
+        W, H = fx["W"], fx["H"]
+        setup = pyoracle.load_setup(name)
+        rows = [y for y0, y1 in shard.owned_bands(H, band_rows, world, rank) for y in range(y0, y1)]
+        assert len(rows) == shard.slab_rows(H, band_rows, world, rank)
+        pad = shard.max_slab_rows(H, band_rows, world)
+        slab = torch.zeros((pad, W, 4), dtype=torch.float32)
+        st = {"max_depth": -1, "closest": float(np.finfo(np.float32).max), "rays": 0}
+        if rows:
+            r = pyoracle.render(setup, rows=rows, threads=1)
+            slab[:len(rows)] = torch.from_numpy(r["pos4"])
+            st = r["stats"]
+        frame = shard.gather_frame(slab, H, band_rows)
+        md, cl, ry = shard.reduce_stats(st["max_depth"], st["closest"], len(rows) * W)
+        if rank == 0:
+            ref = load_npz(name)
+            assert frame.shape == (H, W, 4)
+            assert np.array_equal(frame.numpy().view(np.uint32), ref["pos4"].view(np.uint32))
+            assert ry == W * H
+            assert md == fx["stats"]["max_depth"]
+            assert np.float32(cl) == np.float32(ref["minT"].min())
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # report to the parent, which fails the test
+        errq.put(f"rank {rank}: {type(e).__name__}: {e}")
+        raise
+
+
+def _run(world, name, band_rows):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    mp.start_processes(_worker, args=(world, _free_port(), name, band_rows, errq), nprocs=world,
+                       start_method="spawn", join=True)
+    assert errq.empty(), errq.get()
+
+
+@pytest.mark.parametrize("world,name,band_rows", [(2, "t2", 8), (3, "t3", 8), (2, "t1", 16)])
+def test_gloo_band_gather_reassembles_frame(world, name, band_rows):
+    _run(world, name, band_rows)
+
+
+@pytest.mark.parametrize("H,band,world", [(1080, 8, 8), (2160, 8, 8), (36, 16, 2), (7, 8, 3), (1, 8, 2),
+                                          (16384, 64, 8)])
+def test_slab_rows_mirror_c_abi(H, band, world):
+    from sphereflake_amd import lib
+    total = 0
+    for r in range(world):
+        n = shard.slab_rows(H, band, world, r)
+        assert n == lib().sf_slab_rows(H, band, world, r)
+        total += n
+    assert total == H
+
+
+def test_reassemble_inverts_banding():
+    H, W, band, world = 53, 5, 8, 3
+    frame = np.arange(H * W, dtype=np.int32).reshape(H, W)
+    slabs = []
+    for r in range(world):
+        rows = [y for y0, y1 in shard.owned_bands(H, band, world, r) for y in range(y0, y1)]
+        s = np.full((shard.max_slab_rows(H, band, world), W), -1, np.int32)
+        s[:len(rows)] = frame[rows]
+        slabs.append(s)
+    assert np.array_equal(shard.reassemble(slabs, H, band), frame)
+
+
+def test_band_rows_validation():
+    with pytest.raises(ValueError):
+        shard.owned_bands(100, 12, 2, 0)
+    with pytest.raises(ValueError):
+        shard.owned_bands(100, 8, 2, 2)
