@@ -18,6 +18,9 @@
 extern "C" __global__ void sf_trace_wave1(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
 extern "C" __global__ void sf_trace_wave2(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
 extern "C" __global__ void sf_trace_wave4(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
+extern "C" __global__ void sf_trace_queue1(FrameArgs a, uint32_t* overflow_list, uint32_t* counters, uint32_t parity);
+extern "C" __global__ void sf_trace_queue2(FrameArgs a, uint32_t* overflow_list, uint32_t* counters, uint32_t parity);
+extern "C" __global__ void sf_trace_queue4(FrameArgs a, uint32_t* overflow_list, uint32_t* counters, uint32_t parity);
 extern "C" __global__ void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list, uint32_t* counters,
                                          uint32_t parity);
 extern "C" __global__ void sf_trace_ray(FrameArgs a);
@@ -59,7 +62,7 @@ struct sf_ctx {
     float* min_t = nullptr;
     uint32_t* hit_index = nullptr;
     int32_t* stats = nullptr;          // [0] max depth, [1] closest key, [2] unrecoverable overflow
-    uint32_t* ovf_counters = nullptr;  // [2], alternating per render
+    uint32_t* ovf_counters = nullptr;  // [0,1] overflow counts, [2,3] tile queues; alternating per render
     uint32_t* ovf_list = nullptr;      // tiles_x * tiles_y entries
     DeviceConsts* consts = nullptr;
     DeviceConsts host_consts;
@@ -73,6 +76,10 @@ struct sf_ctx {
     int fixup_blocks = 256;
     uint32_t waves_per_block = SF_TRACE_WAVES;   // tuning knob: env SF_TRACE_WAVES = 1 | 2 | 4
     uint32_t levels_override = 0;                // tuning knob: env SF_LEVELS (LDS levels, 0 = adaptive)
+    bool persistent = true;                      // tuning knob: env SF_PERSISTENT=0 -> one workgroup per tile group
+    uint32_t flags = 0;                          // SF_FLAG_* A/B switches: env SF_FLAGS
+    int cus = 256;
+    int occ_key = -1, occ_blocks = 0;            // cached occupancy (waves per block, levels) -> blocks per CU
     // frame-less progressive mode
     uint32_t* mt_state = nullptr;      // 624 words + next index (std::mt19937 layout)
     uint32_t* draws = nullptr;         // 2 per packet
@@ -193,6 +200,9 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     c->W = width;
     c->H = height;
     c->fixup_blocks = prop.multiProcessorCount;
+    c->cus = prop.multiProcessorCount;
+    if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_FLAGS")) c->flags = (uint32_t)std::strtoul(ev, nullptr, 0);
     if (const char* ev = std::getenv("SF_TRACE_WAVES")) {
         const int w = std::atoi(ev);
         c->waves_per_block = (w == 1 || w == 2 || w == 4) ? (uint32_t)w : SF_TRACE_WAVES;
@@ -216,7 +226,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if ((e = hipMalloc(&c->min_t, npx * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->hit_index, npx * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->stats, 16)) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&c->ovf_counters, 8)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->ovf_counters, 16)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->ovf_list, ntiles * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->consts, sizeof(DeviceConsts))) != hipSuccess) return fail(e);
     if ((e = hipHostMalloc(&c->h_depth, 4, hipHostMallocDefault)) != hipSuccess) return fail(e);
@@ -227,7 +237,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if ((e = hipMemsetAsync(c->min_t, 0, npx * 4, c->stream)) != hipSuccess) return fail(e);
     if ((e = hipMemsetAsync(c->hit_index, 0xff, npx * 4, c->stream)) != hipSuccess) return fail(e);
     if ((e = hipMemsetAsync(c->stats, 0, 16, c->stream)) != hipSuccess) return fail(e);
-    if ((e = hipMemsetAsync(c->ovf_counters, 0, 8, c->stream)) != hipSuccess) return fail(e);
+    if ((e = hipMemsetAsync(c->ovf_counters, 0, 16, c->stream)) != hipSuccess) return fail(e);
     sfhost::child_transforms(c->child);
     int rc = upload_consts(c);
     if (rc == SF_OK) rc = reset_stats_dev(c, 3);
@@ -302,6 +312,7 @@ static FrameArgs frame_args(const sf_ctx* c)
     a.band_count = 1;
     a.consts = c->consts;
     a.stats = c->stats;
+    a.flags = c->flags;
     return a;
 }
 
@@ -364,10 +375,30 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
         const size_t lds = (size_t)SF_LDS_WAVE_FLOATS(a.max_depth) * 4;
         uint32_t* cnt = c->ovf_counters + c->parity;
         const uint32_t wpb = c->waves_per_block;
-        const dim3 grid((ntiles + wpb - 1) / wpb), block(64 * wpb);
-        if (wpb == 1) hipLaunchKernelGGL(sf_trace_wave1, grid, block, lds, s, a, c->ovf_list, cnt);
-        else if (wpb == 2) hipLaunchKernelGGL(sf_trace_wave2, grid, block, 2 * lds, s, a, c->ovf_list, cnt);
-        else hipLaunchKernelGGL(sf_trace_wave4, grid, block, 4 * lds, s, a, c->ovf_list, cnt);
+        const dim3 block(64 * wpb);
+        if (c->persistent) {
+            const void* kern = wpb == 1 ? (const void*)sf_trace_queue1
+                             : wpb == 2 ? (const void*)sf_trace_queue2 : (const void*)sf_trace_queue4;
+            const int key = (int)(wpb * 64 + a.max_depth);
+            if (c->occ_key != key) {
+                int nb = 0;
+                SF_HIP(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, (int)block.x, wpb * lds));
+                c->occ_blocks = nb < 1 ? 1 : nb;
+                c->occ_key = key;
+            }
+            uint32_t nblk = (uint32_t)c->occ_blocks * (uint32_t)c->cus;
+            const uint32_t need = (ntiles + wpb - 1) / wpb;
+            if (nblk > need) nblk = need;
+            const dim3 grid(nblk);
+            if (wpb == 1) hipLaunchKernelGGL(sf_trace_queue1, grid, block, lds, s, a, c->ovf_list, c->ovf_counters, c->parity);
+            else if (wpb == 2) hipLaunchKernelGGL(sf_trace_queue2, grid, block, 2 * lds, s, a, c->ovf_list, c->ovf_counters, c->parity);
+            else hipLaunchKernelGGL(sf_trace_queue4, grid, block, 4 * lds, s, a, c->ovf_list, c->ovf_counters, c->parity);
+        } else {
+            const dim3 grid((ntiles + wpb - 1) / wpb);
+            if (wpb == 1) hipLaunchKernelGGL(sf_trace_wave1, grid, block, lds, s, a, c->ovf_list, cnt);
+            else if (wpb == 2) hipLaunchKernelGGL(sf_trace_wave2, grid, block, 2 * lds, s, a, c->ovf_list, cnt);
+            else hipLaunchKernelGGL(sf_trace_wave4, grid, block, 4 * lds, s, a, c->ovf_list, cnt);
+        }
         SF_HIP(c, hipGetLastError());
         const size_t lds_fix = (size_t)SF_LDS_WAVE_FLOATS(SF_MAX_DEPTH_LIMIT) * 4;
         hipLaunchKernelGGL(sf_fixup_wave, dim3(4 * c->fixup_blocks), dim3(64), lds_fix, s, a,

@@ -14,7 +14,7 @@
 #define SF_TILE 8              // a wave64 traces one 8x8 pixel tile
 #define SF_WAVES_PER_BLOCK 4   // 256-thread workgroups (per-ray kernel)
 #ifndef SF_TRACE_WAVES
-#define SF_TRACE_WAVES 4       // independent waves (tiles) per workgroup of the wave kernel
+#define SF_TRACE_WAVES 2       // independent waves per workgroup of the wave kernels
 #endif
 // Wave-coherent traversal LDS image, per wave (units: floats):
 //   [root: 16][tables: levels x 144][E: levels x 32][stack: levels x 4]
@@ -27,6 +27,8 @@
 #define SF_LDS_LEVEL (SF_LDS_TABLE + SF_LDS_E + SF_LDS_STACK)
 #define SF_LDS_DEPTH (4 * SF_DEPTH_TABLE)   // per-depth constants, staged in front of the image
 #define SF_LDS_WAVE_FLOATS(levels) (SF_LDS_DEPTH + SF_LDS_ROOT + (levels) * SF_LDS_LEVEL)
+
+#define SF_FLAG_NO_LOD_CULL 1u   // disable the per-child LOD reachability cull (A/B only; results identical)
 
 struct DepthTables {
     float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)
@@ -63,6 +65,7 @@ struct FrameArgs {
     uint32_t compact;                 // write rows packed into the shard's slab
     uint32_t max_depth;               // traversal levels provisioned (<= SF_MAX_DEPTH_LIMIT)
     uint32_t emit_aux;
+    uint32_t flags;                   // SF_FLAG_* (A/B switches for diagnostics; 0 = product default)
     const DeviceConsts* consts;
     float* pos;                       // G-buffer positions (float4 x,y,z,1 per pixel)
     float* nrm;                       // G-buffer normals

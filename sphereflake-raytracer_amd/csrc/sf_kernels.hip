@@ -225,7 +225,8 @@ __device__ __forceinline__ void lds_fence()
 template <bool PACKET>
 __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ Lbase,
                                          uint32_t levels, float dx, float dy, float dz, bool valid, HitState& h,
-                                         int32_t& maxd, bool& overflowed, uint64_t* phase_sums = nullptr)
+                                         int32_t& maxd, bool& overflowed, uint32_t K_flags,
+                                         uint64_t* phase_sums = nullptr)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const TraverseLds L{ Lbase, levels };
@@ -268,9 +269,13 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         L.root()[lane] = v;
     }
 
-    // this lane's column of the cooperative child build: child i = lane / 4, column c = lane % 4
+    // this lane's column of the cooperative child build: column c = lane / 9, child i = lane % 9, so
+    // lanes 27..35 hold the 9 child centres and one ballot yields a per-child mask (bits 27..35)
     const bool builder = lane < 36u;
-    const uint32_t bi = builder ? lane >> 2 : 0u, bc = lane & 3u;
+    const uint32_t bi = builder ? lane % 9u : 0u, bc = builder ? lane / 9u : 0u;
+    // per-ray semantics only: in packet semantics a lane with tca < 0 can pass LOD through another
+    // lane's bounding hit (SIMD_AVX.h:254), which the reachability bound below does not cover
+    const bool lod_cull = !PACKET && (K_flags & SF_FLAG_NO_LOD_CULL) == 0u;
     float b[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) b[j] = K->child[bi][4u * bc + j];
@@ -281,6 +286,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     auto expand = [&](const float* node, uint32_t d, bool act, uint32_t& pend) -> uint32_t {
         d = __builtin_amdgcn_readfirstlane(d);   // wave-uniform: depth tables come by scalar loads
         lds_fence();
+        bool reach = true;
         const float4 pc = *reinterpret_cast<const float4*>(node);
         const float4 p0 = *reinterpret_cast<const float4*>(node + 4);
         const float4 p1 = *reinterpret_cast<const float4*>(node + 8);
@@ -297,9 +303,27 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             const float z = ((p0.z * b0 + p1.z * b1) + p2.z * b2) + pc.z * b[3];
             const float w = bc == 3u ? (x * x + y * y) + z * z : 0.0f;
             *reinterpret_cast<float4*>(slot_base + d * SF_LDS_TABLE) = make_float4(x, y, z, w);
+            // LOD reachability of child bi (centre lanes): any lane's float t satisfies
+            // t >= sqrt(|c|^2 - R^2 - dl) - sqrt(R^2 + dl) (1 - O(2^-22)), dl = 2^-16 |c|^2 bounding
+            // the rounding of tca, d2 and the direction's length (SIMD_AVX.h:244-267). If that bound
+            // is >= T (with 2^-12 slack), no lane can pass the LOD test (Sphereflake.h:146-153), so
+            // the child does nothing in the reference for any lane: skip it for the whole wave.
+            if (bc == 3u) {
+                const float R2c = dtc.x, Tc = dtc.w;
+                const float dl = w * 0x1p-16f;
+                const float a = (w - R2c) - dl;
+                const float rhs = (Tc + __builtin_sqrtf(R2c + dl)) * (1.0f + 0x1p-12f);
+                reach = !(a > 0.0f && __builtin_sqrtf(a) > rhs);
+            }
         }
+        uint32_t M = lod_cull ? (uint32_t)(wave_ballot(reach) >> 27) & 0x1ffu : 0x1ffu;
+        M = __builtin_amdgcn_readfirstlane(M);
         lds_fence();
         SF_STAMP(6);
+        if (M == 0u) {   // no child reachable for any lane (e.g. every child of a deepest-level node)
+            pend = 0u;
+            return 0u;
+        }
         const float* tab = L.table(d);
         const float R2b = dtc.x;
         const float T = dtc.w;
@@ -310,6 +334,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         uint32_t e = 0, pm = 0;
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
+            if (((M >> i) & 1u) == 0u) continue;   // uniform: unreachable for every lane
             const float tca = (c[i].x * dx + c[i].y * dy) + c[i].z * dz;
             const float d2 = c[i].w - tca * tca;
             const bool hb = act & group_any<PACKET>(tca >= 0.0f) & group_any<PACKET>(d2 <= R2b);
@@ -358,12 +383,9 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 continue;
             }
             // save the open node's state, enter child c
-            if (lane == 0u) {
+            {   // every lane writes the same words (no lane-0-only region inside the DFS loop)
                 uint32_t* st = L.stack(d);
-                st[0] = pend;
-                st[1] = cN;
-                st[2] = (uint32_t)idxN;
-                st[3] = (uint32_t)(idxN >> 32);
+                *reinterpret_cast<uint4*>(st) = make_uint4(pend, cN, (uint32_t)idxN, (uint32_t)(idxN >> 32));
             }
             L.E(d)[lane] = (uint16_t)eN;
             const bool a = ((eN >> c) & 1u) != 0u;
@@ -455,9 +477,37 @@ __device__ __forceinline__ void write_pixel(const FrameArgs& a, const Tile& t, f
     }
 }
 
+struct TileStats {
+    int32_t maxd;       // uniform: deepest expanded node (-1: none)
+    float closest;      // uniform: min minT over the tile's valid rays
+    bool overflowed;    // uniform: the tile needs more LDS levels than provisioned
+};
+
+// One lane's global atomic add on behalf of the wave, result broadcast to every lane. EXEC is set to
+// lane 0 inside the asm block, so the compiler's CFG has no lane-0-only region: such regions inside a
+// loop let the structurizer run lanes in different iterations, which breaks wave-uniform code.
+__device__ __forceinline__ uint32_t wave_fetch_add(uint32_t* p, uint32_t v)
+{
+    uint32_t r, out;
+    uint64_t saved;
+    const uint32_t zero = 0u;
+    __asm__ volatile(
+        "s_mov_b64 %1, exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "global_atomic_add %0, %3, %4, %5 sc0\n\t"
+        "s_waitcnt vmcnt(0)\n\t"
+        "s_mov_b64 exec, %1\n\t"
+        "s_nop 4\n\t"
+        "v_readlane_b32 %2, %0, 0\n\t"
+        : "=&v"(r), "=&s"(saved), "=s"(out)
+        : "v"(zero), "v"(v), "s"(p)
+        : "memory");
+    return out;
+}
+
 template <bool FIXUP>
-__device__ __forceinline__ void trace_tile(const FrameArgs& a, float* __restrict__ L, uint32_t tile, uint32_t levels,
-                                           uint32_t* overflow_list, uint32_t* overflow_count)
+__device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __restrict__ L, uint32_t tile,
+                                                uint32_t levels, uint32_t* overflow_list, uint32_t* overflow_count)
 {
     const DeviceConsts* __restrict__ K = a.consts;
     const uint32_t lane = threadIdx.x & 63u;
@@ -469,9 +519,11 @@ __device__ __forceinline__ void trace_tile(const FrameArgs& a, float* __restrict
     HitState h;
     int32_t maxd = -1;
     bool overflowed = false;
-    traverse<false>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed, FIXUP ? nullptr : a.phase_sums);
-    if (a.tile_trace && lane == 0u && !FIXUP) {
-        // diagnostics only: never read by the kernel, never feeds an output value
+    traverse<false>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed, a.flags,
+                    FIXUP ? nullptr : a.phase_sums);
+    if (!FIXUP && a.tile_trace) {
+        // diagnostics only: never read by the kernel, never feeds an output value. Every lane stores
+        // the same (uniform) words: no lane-0-only region.
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         uint32_t hw;
         __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -482,19 +534,28 @@ __device__ __forceinline__ void trace_tile(const FrameArgs& a, float* __restrict
         a.tile_trace[3u * tile + 2u] = ((uint64_t)xcc << 32) | hw;
     }
 
-    if (!FIXUP && overflowed && lane == 0u) {
+    if (!FIXUP && overflowed) {
         // a deeper re-trace (sf_fixup_wave) rewrites this whole tile
-        const uint32_t slot = atomicAdd(overflow_count, 1u);
-        overflow_list[slot] = tile;
+        const uint32_t slot = wave_fetch_add(overflow_count, 1u);
+        overflow_list[slot] = tile;   // uniform value and address
     }
     if (t.valid) write_pixel(a, t, dx, dy, dz, h, K->lut);
 
     // stats: max depth reached, closest sphere distance (Sphereflake.h:157-160, Sphereflake.cpp:197-200)
-    const float closest = wave_min(t.valid ? h.minT : FLT_MAX);
-    if (lane == 0u) {
+    TileStats st;
+    st.maxd = maxd;
+    st.closest = wave_min(t.valid ? h.minT : FLT_MAX);
+    st.overflowed = overflowed;
+    return st;
+}
+
+// Publish one wave's stats (outside any loop: lane-0 regions are harmless here).
+__device__ __forceinline__ void publish_stats(const FrameArgs& a, int32_t maxd, float closest, uint32_t unresolved)
+{
+    if ((threadIdx.x & 63u) == 0u) {
         if (maxd >= 0) atomicMax(&a.stats[0], maxd);
         atomicMin(&a.stats[1], sf_float_key(closest));
-        if (FIXUP && overflowed) atomicAdd(&a.stats[2], 1);
+        if (unresolved) atomicAdd(&a.stats[2], (int32_t)unresolved);
     }
 }
 
@@ -509,7 +570,9 @@ __device__ __forceinline__ void trace_wave_body(const FrameArgs& a, uint32_t* ov
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t tile = blockIdx.x * WAVES + wv;
     if (tile >= a.tiles_x * a.tile_rows) return;
-    trace_tile<false>(a, lds + wv * SF_LDS_WAVE_FLOATS(a.max_depth), tile, a.max_depth, overflow_list, overflow_count);
+    const TileStats st = trace_tile<false>(a, lds + wv * SF_LDS_WAVE_FLOATS(a.max_depth), tile, a.max_depth,
+                                           overflow_list, overflow_count);
+    publish_stats(a, st.maxd, st.closest, 0u);
 }
 
 extern "C" __global__ __launch_bounds__(64) void sf_trace_wave1(FrameArgs a, uint32_t* ol, uint32_t* oc)
@@ -525,6 +588,46 @@ extern "C" __global__ __launch_bounds__(256) void sf_trace_wave4(FrameArgs a, ui
     trace_wave_body<4>(a, ol, oc);
 }
 
+// Persistent variant: a grid of resident workgroups; each wave pulls 8x8 tiles from a frame-wide
+// atomic queue until it runs dry. Dynamic balancing: tile costs vary ~100x (sky vs. deep flake),
+// and the in-order workgroup dispatcher otherwise idles CUs behind long tiles. counters: [0,1]
+// overflow counts, [2,3] tile queues, alternating per render (this render zeroes the next one's).
+template <int WAVES>
+__device__ __forceinline__ void trace_queue_body(const FrameArgs& a, uint32_t* overflow_list, uint32_t* counters,
+                                                 uint32_t parity)
+{
+    extern __shared__ float lds[];
+    const uint32_t wv = threadIdx.x >> 6;
+    if (blockIdx.x == 0 && threadIdx.x == 0) counters[2u + (parity ^ 1u)] = 0u;
+    uint32_t* const queue = counters + 2u + parity;
+    uint32_t* const ovc = counters + parity;
+    float* const L = lds + wv * SF_LDS_WAVE_FLOATS(a.max_depth);
+    const uint32_t ntiles = a.tiles_x * a.tile_rows;
+    int32_t maxd = -1;
+    float closest = FLT_MAX;
+    for (;;) {
+        const uint32_t t = wave_fetch_add(queue, 1u);   // uniform
+        if (t >= ntiles) break;   // every wave reaches this: the queue only grows
+        const TileStats st = trace_tile<false>(a, L, t, a.max_depth, overflow_list, ovc);
+        maxd = st.maxd > maxd ? st.maxd : maxd;
+        closest = fminf(closest, st.closest);
+    }
+    publish_stats(a, maxd, closest, 0u);
+}
+
+extern "C" __global__ __launch_bounds__(64) void sf_trace_queue1(FrameArgs a, uint32_t* ol, uint32_t* cnt, uint32_t parity)
+{
+    trace_queue_body<1>(a, ol, cnt, parity);
+}
+extern "C" __global__ __launch_bounds__(128) void sf_trace_queue2(FrameArgs a, uint32_t* ol, uint32_t* cnt, uint32_t parity)
+{
+    trace_queue_body<2>(a, ol, cnt, parity);
+}
+extern "C" __global__ __launch_bounds__(256) void sf_trace_queue4(FrameArgs a, uint32_t* ol, uint32_t* cnt, uint32_t parity)
+{
+    trace_queue_body<4>(a, ol, cnt, parity);
+}
+
 // Re-traces flagged tiles with SF_MAX_LEVELS levels. Grid-stride over the list; reads this
 // render's counter and zeroes the other one (the next render's), so no memset is needed.
 extern "C" __global__ __launch_bounds__(64) void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list,
@@ -533,8 +636,16 @@ extern "C" __global__ __launch_bounds__(64) void sf_fixup_wave(FrameArgs a, cons
     extern __shared__ float lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) counters[parity ^ 1u] = 0u;
     const uint32_t n = counters[parity];
-    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x)
-        trace_tile<true>(a, lds, overflow_list[i], SF_MAX_LEVELS, nullptr, nullptr);
+    int32_t maxd = -1;
+    float closest = FLT_MAX;
+    uint32_t unresolved = 0u;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const TileStats st = trace_tile<true>(a, lds, overflow_list[i], SF_MAX_LEVELS, nullptr, nullptr);
+        maxd = st.maxd > maxd ? st.maxd : maxd;
+        closest = fminf(closest, st.closest);
+        unresolved += st.overflowed ? 1u : 0u;
+    }
+    publish_stats(a, maxd, closest, unresolved);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -740,7 +851,7 @@ extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace(FrameArgs 
     HitState h;
     int32_t maxd = -1;
     bool overflowed = false;
-    traverse<true>(K, a.root, lds, SF_PROGRESSIVE_LEVELS, dx, dy, dz, valid, h, maxd, overflowed);
+    traverse<true>(K, a.root, lds, SF_PROGRESSIVE_LEVELS, dx, dy, dz, valid, h, maxd, overflowed, a.flags);
 
     PacketLane out;
     shade(dx, dy, dz, h, K->lut, out.px, out.py, out.pz, out.nx, out.ny, out.nz);
