@@ -1,6 +1,7 @@
 set -e
-mkdir -p gpurun_out/diag
-timeout -k 10 120 python scripts/tile_schedule.py --out gpurun_out/diag/tt_w4.npy > gpurun_out/diag/tt_w4.txt 2>&1
-SF_TRACE_WAVES=1 timeout -k 10 120 python scripts/tile_schedule.py --out gpurun_out/diag/tt_w1.npy > gpurun_out/diag/tt_w1.txt 2>&1
-SF_TRACE_WAVES=1 SF_LIB=$PWD/sphereflake-raytracer_amd/build_phases/libsphereflake_hip.so timeout -k 10 120 python scripts/tile_schedule.py --out gpurun_out/diag/tt_ph.npy > gpurun_out/diag/tt_ph.txt 2>&1
-cat gpurun_out/diag/*.txt
+T=${1:-diag}
+mkdir -p gpurun_out/$T
+timeout -k 10 120 python scripts/tile_schedule.py --out gpurun_out/$T/tt.npy > gpurun_out/$T/tt.txt 2>&1
+cat gpurun_out/$T/tt.txt
+scripts/prof_pmc.sh $T/pmc
+python3 scripts/pmc_summary.py gpurun_out/$T/pmc/* > gpurun_out/$T/pmc_summary.txt

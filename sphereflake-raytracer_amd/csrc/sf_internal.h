@@ -14,19 +14,18 @@
 #define SF_TILE 8              // a wave64 traces one 8x8 pixel tile
 #define SF_WAVES_PER_BLOCK 4   // 256-thread workgroups (per-ray kernel)
 #ifndef SF_TRACE_WAVES
-#define SF_TRACE_WAVES 2       // independent waves per workgroup of the wave kernels
+#define SF_TRACE_WAVES 1       // independent waves per workgroup of the wave kernels
 #endif
 // Wave-coherent traversal LDS image, per wave (units: floats):
-//   [root: 16][tables: levels x 144][E: levels x 32][stack: levels x 4]
+//   [root: 16][(levels - 1) x (table 144 | E 32)]
 // A transform is 16 floats: [cx cy cz cc | col0.xyz - | col1.xyz - | col2.xyz -] (cc = Dot(centre, centre)).
 #define SF_LDS_ROOT 16
 #define SF_LDS_CHILD 16
 #define SF_LDS_TABLE (9 * SF_LDS_CHILD)   // the 9 child transforms of the node open at a level
 #define SF_LDS_E 32                       // 64 lanes x u16: per-lane child-expand bits of that node
-#define SF_LDS_STACK 4                    // pending children, child cursor, heap index lo/hi
-#define SF_LDS_LEVEL (SF_LDS_TABLE + SF_LDS_E + SF_LDS_STACK)
-#define SF_LDS_DEPTH (4 * SF_DEPTH_TABLE)   // per-depth constants, staged in front of the image
-#define SF_LDS_WAVE_FLOATS(levels) (SF_LDS_DEPTH + SF_LDS_ROOT + (levels) * SF_LDS_LEVEL)
+#define SF_LDS_LEVEL (SF_LDS_TABLE + SF_LDS_E)
+// levels - 1 level images: the deepest provisioned level's table is never read (see traverse)
+#define SF_LDS_WAVE_FLOATS(levels) (SF_LDS_ROOT + ((levels) - 1) * SF_LDS_LEVEL)
 
 #define SF_FLAG_NO_LOD_CULL 1u   // disable the per-child LOD reachability cull (A/B only; results identical)
 

@@ -166,21 +166,15 @@ __device__ __forceinline__ bool group_any(bool p)
 //   self       hs = active && any_g(tca >= 0) && any_g(d2 <= r^2); accept lanes with d2 <= r^2 && t < minT
 // For per-ray groups these are exactly the reference's per-lane tests.
 // ------------------------------------------------------------------------------------------
+// Per-wave LDS image (floats): [root: 16][per level: table 9 x 16 | E 32]. A transform is 16 floats:
+// [cx cy cz cc | col0.xyz - | col1.xyz - | col2.xyz -] (cc = Dot(centre, centre)).
 struct TraverseLds {
     float* base;
-    uint32_t levels;
-    // {(2r)^2, r^2, (4/3) r, T} of a depth: one uniform ds_read_b128
-    __device__ __forceinline__ float4 depth(uint32_t d) const { return reinterpret_cast<const float4*>(base)[d]; }
-    __device__ __forceinline__ float* img() const { return base + SF_LDS_DEPTH; }
-    __device__ __forceinline__ float* root() const { return img(); }
-    __device__ __forceinline__ float* table(uint32_t lvl) const { return img() + SF_LDS_ROOT + lvl * SF_LDS_TABLE; }
+    __device__ __forceinline__ float* root() const { return base; }
+    __device__ __forceinline__ float* table(uint32_t lvl) const { return base + SF_LDS_ROOT + lvl * SF_LDS_LEVEL; }
     __device__ __forceinline__ uint16_t* E(uint32_t lvl) const
     {
-        return reinterpret_cast<uint16_t*>(img() + SF_LDS_ROOT + levels * SF_LDS_TABLE + lvl * SF_LDS_E);
-    }
-    __device__ __forceinline__ uint32_t* stack(uint32_t lvl) const
-    {
-        return reinterpret_cast<uint32_t*>(img() + SF_LDS_ROOT + levels * (SF_LDS_TABLE + SF_LDS_E) + lvl * SF_LDS_STACK);
+        return reinterpret_cast<uint16_t*>(base + SF_LDS_ROOT + lvl * SF_LDS_LEVEL + SF_LDS_TABLE);
     }
 };
 
@@ -188,6 +182,32 @@ __device__ __forceinline__ void lds_fence()
 {
     __builtin_amdgcn_wave_barrier();
     __asm__ volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ float readlane_f(float v, uint32_t l)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
+}
+// Lane l of `old` := v (uniform v and l) as a per-lane select: no divergent region, no asm.
+__device__ __forceinline__ uint32_t writelane_u(uint32_t v, uint32_t l, uint32_t old)
+{
+    return (threadIdx.x & 63u) == l ? v : old;
+}
+
+// One lane's 64-bit global atomic add on behalf of the wave (EXEC forced to lane 0 inside the asm).
+__device__ __forceinline__ void wave_atomic_add_u64(uint64_t* p, uint64_t v)
+{
+    uint64_t saved;
+    const uint32_t zero = 0u;
+    __asm__ volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "global_atomic_add_x2 %1, %2, %3\n\t"
+        "s_waitcnt vmcnt(0)\n\t"
+        "s_mov_b64 exec, %0\n\t"
+        : "=&s"(saved)
+        : "v"(zero), "v"(v), "s"(p)
+        : "memory");
 }
 
 // Diagnostic build only (make PHASES=1): s_memtime stamps at the DFS segment boundaries, summed per
@@ -207,13 +227,8 @@ __device__ __forceinline__ void lds_fence()
     } while (0)
 #define SF_STAMP_FLUSH(p)                                                                      \
     do {                                                                                       \
-        if ((p) && lane == 0u) {                                                               \
-            atomicAdd((unsigned long long*)(p) + 1, ph_sum[1]);                                \
-            atomicAdd((unsigned long long*)(p) + 2, ph_sum[2]);                                \
-            atomicAdd((unsigned long long*)(p) + 3, ph_sum[3]);                                \
-            atomicAdd((unsigned long long*)(p) + 4, ph_sum[4]);                                \
-            atomicAdd((unsigned long long*)(p) + 5, ph_sum[5]);                                \
-            atomicAdd((unsigned long long*)(p) + 6, ph_sum[6]);                                \
+        if (p) {                                                                               \
+            for (int k_ = 1; k_ < 7; ++k_) wave_atomic_add_u64((uint64_t*)(p) + k_, ph_sum[k_]);  \
         }                                                                                      \
     } while (0)
 #else
@@ -222,6 +237,39 @@ __device__ __forceinline__ void lds_fence()
 #define SF_STAMP_FLUSH(p) (void)(p)
 #endif
 
+// Per-depth constants {(2r)^2, r^2, (4/3) r, T} through the constant address space, so a uniform depth
+// gives one s_load_dwordx4 from the scalar cache. Through a generic pointer the compiler cannot rule
+// out aliasing with the kernel's global stores and emits a vector load plus a vmcnt wait instead.
+__device__ __forceinline__ float4 depth_consts(const DeviceConsts* K, uint32_t d)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) float4* ConstF4;
+    return ((ConstF4)(const void*)K->depth4)[d];
+#else
+    return reinterpret_cast<const float4*>(K->depth4)[d];   // host pass: never executed
+#endif
+}
+
+// Root transform -> the wave's LDS image in the transform layout (Sphereflake.cpp:83). The same for
+// every tile of a frame: kernels stage it once per wave, before any tile loop.
+__device__ __forceinline__ void stage_root(float* __restrict__ Lbase, const float* root)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    if (lane < 16u) {
+        const float rcc = (root[9] * root[9] + root[10] * root[10]) + root[11] * root[11];
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            float rk = 0.f;
+            if (k < 3) rk = root[9 + k];
+            else if (k == 3) rk = rcc;
+            else if ((k & 3) != 3) rk = root[3 * ((k >> 2) - 1) + (k & 3)];
+            v = (lane == (uint32_t)k) ? rk : v;
+        }
+        Lbase[lane] = v;   // TraverseLds::root()
+    }
+}
+
 template <bool PACKET>
 __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ Lbase,
                                          uint32_t levels, float dx, float dy, float dz, bool valid, HitState& h,
@@ -229,12 +277,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                                          uint64_t* phase_sums = nullptr)
 {
     const uint32_t lane = threadIdx.x & 63u;
-    const TraverseLds L{ Lbase, levels };
+    const TraverseLds L{ Lbase };
     SF_STAMP_DECL;
-
-    // per-depth constants -> LDS (lanes 0..32): uniform reads later cost one ds_read_b128
-    if (lane < (uint32_t)SF_DEPTH_TABLE)
-        reinterpret_cast<float4*>(Lbase)[lane] = reinterpret_cast<const float4*>(K->depth4)[lane];
 
     h.minT = FLT_MAX;
     h.cx = h.cy = h.cz = 0.f;
@@ -246,117 +290,138 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     const float rcc = (rcx * rcx + rcy * rcy) + rcz * rcz;
     bool ex0;
     {
+        const float4 dt0 = depth_consts(K, 0u);
         const float tca = (rcx * dx + rcy * dy) + rcz * dz;
         const float d2 = rcc - tca * tca;
-        const float R2b = K->dt.r2_bound[0];
-        const bool hb = valid && group_any<PACKET>(tca >= 0.0f) && group_any<PACKET>(d2 <= R2b);
-        ex0 = hb && group_any<PACKET>(near_root(tca, d2, R2b) < K->dt.lod[0]);
+        const bool hb = valid && group_any<PACKET>(tca >= 0.0f) && group_any<PACKET>(d2 <= dt0.x);
+        ex0 = hb && group_any<PACKET>(near_root(tca, d2, dt0.x) < dt0.w);
     }
     if (!wave_ballot(ex0)) return;
     maxd = 0;
 
-    // root transform -> LDS in the transform layout (lanes 0..15)
-    if (lane < 16u) {
-        float v = 0.f;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            float rk = 0.f;
-            if (k < 3) rk = root[9 + k];
-            else if (k == 3) rk = rcc;
-            else if ((k & 3) != 3) rk = root[3 * ((k >> 2) - 1) + (k & 3)];
-            v = (lane == (uint32_t)k) ? rk : v;
-        }
-        L.root()[lane] = v;
-    }
-
-    // this lane's column of the cooperative child build: column c = lane / 9, child i = lane % 9, so
-    // lanes 27..35 hold the 9 child centres and one ballot yields a per-child mask (bits 27..35)
-    const bool builder = lane < 36u;
-    const uint32_t bi = builder ? lane % 9u : 0u, bc = builder ? lane / 9u : 0u;
+    // This lane's column of the cooperative child build: column c = lane / 9, child i = lane % 9, so
+    // lanes 27..35 hold the 9 child centres (read back by v_readlane, no LDS round trip) and one ballot
+    // yields a per-child mask (bits 27..35).
+    // Lanes 36..63 mirror lanes 0..27 (same column, same value, same address), so the build has no
+    // divergent region; its VALU cost is per wave either way.
+    const uint32_t bl = lane < 36u ? lane : lane - 36u;
+    const uint32_t bi = bl % 9u, bc = bl / 9u;
     // per-ray semantics only: in packet semantics a lane with tca < 0 can pass LOD through another
     // lane's bounding hit (SIMD_AVX.h:254), which the reachability bound below does not cover
     const bool lod_cull = !PACKET && (K_flags & SF_FLAG_NO_LOD_CULL) == 0u;
     float b[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) b[j] = K->child[bi][4u * bc + j];
-    float* const slot_base = L.table(0) + bi * SF_LDS_CHILD + (bc == 3u ? 0u : 4u + 4u * bc);
+    const uint32_t slot = bi * SF_LDS_CHILD + (bc == 3u ? 0u : 4u + 4u * bc);
 
-    // ---- expand: build the children of the node at `node` (depth d) into table(d), then batch-
-    // evaluate them (depth d+1) for the lanes in `act`. Returns this lane's 9-bit E; *pend = wave mask.
+    // ---- expand the node at `node` (depth d, transform in LDS): build its 9 child transforms into
+    // table(d), then test the children (depth d+1) for the lanes in `act`. Returns this lane's 9-bit
+    // "child expands" vector; *pend = the wave's mask of children some lane expands.
     auto expand = [&](const float* node, uint32_t d, bool act, uint32_t& pend) -> uint32_t {
-        d = __builtin_amdgcn_readfirstlane(d);   // wave-uniform: depth tables come by scalar loads
+        d = __builtin_amdgcn_readfirstlane(d);   // wave-uniform: depth constants come by scalar loads
         lds_fence();
-        bool reach = true;
         const float4 pc = *reinterpret_cast<const float4*>(node);
         const float4 p0 = *reinterpret_cast<const float4*>(node + 4);
         const float4 p1 = *reinterpret_cast<const float4*>(node + 8);
         const float4 p2 = *reinterpret_cast<const float4*>(node + 12);
-        const float4 dtn = L.depth(d);            // this node's depth: (4/3) r
-        const float4 dtc = L.depth(d + 1u);       // its children's: (2r)^2, T
-        if (builder) {
-            const float s = dtn.z;
-            const float b0 = bc == 3u ? b[0] * s : b[0];
-            const float b1 = bc == 3u ? b[1] * s : b[1];
-            const float b2 = bc == 3u ? b[2] * s : b[2];
-            const float x = ((p0.x * b0 + p1.x * b1) + p2.x * b2) + pc.x * b[3];
-            const float y = ((p0.y * b0 + p1.y * b1) + p2.y * b2) + pc.y * b[3];
-            const float z = ((p0.z * b0 + p1.z * b1) + p2.z * b2) + pc.z * b[3];
-            const float w = bc == 3u ? (x * x + y * y) + z * z : 0.0f;
-            *reinterpret_cast<float4*>(slot_base + d * SF_LDS_TABLE) = make_float4(x, y, z, w);
-            // LOD reachability of child bi (centre lanes): any lane's float t satisfies
-            // t >= sqrt(|c|^2 - R^2 - dl) - sqrt(R^2 + dl) (1 - O(2^-22)), dl = 2^-16 |c|^2 bounding
-            // the rounding of tca, d2 and the direction's length (SIMD_AVX.h:244-267). If that bound
-            // is >= T (with 2^-12 slack), no lane can pass the LOD test (Sphereflake.h:146-153), so
-            // the child does nothing in the reference for any lane: skip it for the whole wave.
-            if (bc == 3u) {
-                const float R2c = dtc.x, Tc = dtc.w;
-                const float dl = w * 0x1p-16f;
-                const float a = (w - R2c) - dl;
-                const float rhs = (Tc + __builtin_sqrtf(R2c + dl)) * (1.0f + 0x1p-12f);
-                reach = !(a > 0.0f && __builtin_sqrtf(a) > rhs);
-            }
-        }
-        uint32_t M = lod_cull ? (uint32_t)(wave_ballot(reach) >> 27) & 0x1ffu : 0x1ffu;
-        M = __builtin_amdgcn_readfirstlane(M);
-        lds_fence();
-        SF_STAMP(6);
-        if (M == 0u) {   // no child reachable for any lane (e.g. every child of a deepest-level node)
-            pend = 0u;
-            return 0u;
-        }
-        const float* tab = L.table(d);
+        const float4 dtn = depth_consts(K, d);        // (4/3) r of this node
+        const float4 dtc = depth_consts(K, d + 1u);   // children: (2r)^2, T
+        // world = parent * child (SIMD_AVX.h:59-81), child translation scaled by (4/3) r (Sphereflake.h:162-172):
+        // column 3 lanes multiply b0..b2 by s, the others by 1 (exact)
+        const float sm = bc == 3u ? dtn.z : 1.0f;
+        const float b0 = b[0] * sm, b1 = b[1] * sm, b2 = b[2] * sm;
+        const float x = ((p0.x * b0 + p1.x * b1) + p2.x * b2) + pc.x * b[3];
+        const float y = ((p0.y * b0 + p1.y * b1) + p2.y * b2) + pc.y * b[3];
+        const float z = ((p0.z * b0 + p1.z * b1) + p2.z * b2) + pc.z * b[3];
+        const float w = (x * x + y * y) + z * z;   // Dot(centre, centre) on the centre lanes (bc = 3)
+        // table(levels-1) is never read: entering a child of the deepest provisioned level overflows
+        // first. Not allocated, not stored (uniform branch).
+        if (d + 1u < levels) *reinterpret_cast<float4*>(L.table(d) + slot) = make_float4(x, y, z, w);
         const float R2b = dtc.x;
         const float T = dtc.w;
-        // all 9 centres first: straight-line code, so the reads overlap and the tests interleave
-        float4 c[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) c[i] = *reinterpret_cast<const float4*>(tab + i * SF_LDS_CHILD);
+        uint32_t M = 0x1ffu;
+        if (lod_cull) {
+            // LOD reachability of child bi (centre lanes 27..35): any lane's float t satisfies
+            // t >= sqrt(|c|^2 - R^2 - dl) - sqrt(R^2 + dl) (1 - O(2^-22)), dl = 2^-16 |c|^2 bounding
+            // the rounding of tca, d2 and the direction's length (SIMD_AVX.h:244-267). If that bound
+            // is >= T, i.e. |c|^2 - R^2 - dl > rhs^2, no lane can pass the LOD test
+            // (Sphereflake.h:146-153), so the child does nothing in the reference for any lane: skip
+            // it for the whole wave. The 2^-12 slack in rhs covers the rounding of this test itself
+            // (hardware sqrt, squares), so no correctly rounded operation is needed here.
+            const float dl = w * 0x1p-16f;
+            const float ra = (w - R2b) - dl;
+            const float rhs = (T + __builtin_amdgcn_sqrtf(R2b + dl)) * (1.0f + 0x1p-12f);
+            const uint64_t skip = wave_ballot(ra > 0.0f) & wave_ballot(ra > rhs * rhs);
+            M = (uint32_t)(~skip >> 27) & 0x1ffu;
+        }
+        M = __builtin_amdgcn_readfirstlane(M);
+        SF_STAMP(6);
         uint32_t e = 0, pm = 0;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) {
-            if (((M >> i) & 1u) == 0u) continue;   // uniform: unreachable for every lane
-            const float tca = (c[i].x * dx + c[i].y * dy) + c[i].z * dz;
-            const float d2 = c[i].w - tca * tca;
-            const bool hb = act & group_any<PACKET>(tca >= 0.0f) & group_any<PACKET>(d2 <= R2b);
-            if (wave_ballot(hb)) {   // ~1/3 of the children: only then the LOD test
+        if constexpr (!PACKET) {
+            // Per-ray semantics. "Any lane" tests are scalar ANDs of ballots of single compares
+            // (each ballot is the compare's own lane mask: no bool materialisation); per-lane bools
+            // are formed only where a lane's own bit is needed (its E bit).
+            const uint64_t actm = wave_ballot(act);
+            while (M) {   // uniform loop over the children some lane can reach, in index order
+                const uint32_t i = __builtin_ctz(M);
+                M &= M - 1u;
+                const float cx = readlane_f(x, 27u + i), cy = readlane_f(y, 27u + i);
+                const float cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
+                const float tca = (cx * dx + cy * dy) + cz * dz;
+                const float d2 = cc - tca * tca;
+                const bool f0 = tca >= 0.0f, f1 = d2 <= R2b;
+                const uint64_t hbm = actm & wave_ballot(f0) & wave_ballot(f1);   // bounding (SIMD_AVX.h:247-258)
+                if (hbm == 0ull) continue;
                 // LOD on t = fl(tca - sqrt_rn(R2b - d2)) (SIMD_AVX.h:260-267; t0 <= t1 picks t1 for
                 // thc >= 0). Fast bracket: the hardware sqrt is within 2 ulp of sqrt_rn and t is
-                // monotone in it, so [fl(tca - (s + 2ulp)), fl(tca - (s - 2ulp))] contains t; the
-                // exact path runs only when T falls inside (or the sqrt argument is tiny).
-                const float x = R2b - d2;
-                const float s = __builtin_amdgcn_sqrtf(x);
-                const float s_lo = __uint_as_float((uint32_t)max((int32_t)__float_as_uint(s) - 2, 0));
-                const float s_hi = __uint_as_float(__float_as_uint(s) + 2u);
-                const float t_hi = tca - s_lo;           // >= t
-                const float t_lo = tca - s_hi;           // <= t
-                // a stand-in for t on the same side of T as t whenever the bracket decides
-                float t_dec = t_hi < T ? t_hi : t_lo;
-                const bool undecided = hb & ((!(t_hi < T) & !(t_lo >= T)) | (x < 0x1p-96f));
-                if (wave_ballot(undecided)) t_dec = undecided ? near_root_exact(tca, d2, R2b) : t_dec;
-                const bool exi = hb & group_any<PACKET>(t_dec < T);
-                const uint64_t mi = wave_ballot(exi);
-                e |= exi ? (1u << i) : 0u;
-                pm |= (mi != 0ull ? 1u : 0u) << i;
+                // monotone in it, so t_lo = fl(tca - (s + 2ulp)) <= t <= t_hi = fl(tca - (s - 2ulp)):
+                // t_hi < T decides "expands", t_lo >= T decides "does not"; the exact path runs only
+                // for lanes in between (or with a tiny sqrt argument).
+                const float xs = R2b - d2;
+                const float sq = __builtin_amdgcn_sqrtf(xs);
+                const float s_lo = __uint_as_float((uint32_t)max((int32_t)__float_as_uint(sq) - 2, 0));
+                const float s_hi = __uint_as_float(__float_as_uint(sq) + 2u);
+                const float t_hi = tca - s_lo;
+                const float t_lo = tca - s_hi;
+                const bool yes = t_hi < T, maybe = t_lo < T, tiny = xs < 0x1p-96f;
+                const uint64_t tinym = wave_ballot(tiny);
+                uint64_t exm = hbm & wave_ballot(yes) & ~tinym;
+                const uint64_t undm = hbm & ((wave_ballot(maybe) & ~wave_ballot(yes)) | tinym);
+                bool exi = act & f0 & f1 & yes & !tiny;
+                if (undm) {   // rare: exact IEEE root for the undecided lanes
+                    const bool und = act & f0 & f1 & ((maybe & !yes) | tiny);
+                    const float te = near_root_exact(tca, d2, R2b);
+                    exi = und ? (te < T) : exi;
+                    exm = wave_ballot(exi);
+                }
+                e = exi ? (e | (1u << i)) : e;
+                pm |= (exm != 0ull ? 1u : 0u) << i;
+            }
+        } else {
+            // Packet semantics (frame-less mode): early-outs over the 8 lanes of a reference packet.
+            while (M) {
+                const uint32_t i = __builtin_ctz(M);
+                M &= M - 1u;
+                const float cx = readlane_f(x, 27u + i), cy = readlane_f(y, 27u + i);
+                const float cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
+                const float tca = (cx * dx + cy * dy) + cz * dz;
+                const float d2 = cc - tca * tca;
+                const bool hb = act & group_any<PACKET>(tca >= 0.0f) & group_any<PACKET>(d2 <= R2b);
+                if (wave_ballot(hb)) {
+                    const float xs = R2b - d2;
+                    const float sq = __builtin_amdgcn_sqrtf(xs);
+                    const float s_lo = __uint_as_float((uint32_t)max((int32_t)__float_as_uint(sq) - 2, 0));
+                    const float s_hi = __uint_as_float(__float_as_uint(sq) + 2u);
+                    const float t_hi = tca - s_lo;           // >= t
+                    const float t_lo = tca - s_hi;           // <= t
+                    float t_dec = t_hi < T ? t_hi : t_lo;    // on the same side of T as t when decided
+                    const bool undecided = hb & ((!(t_hi < T) & !(t_lo >= T)) | (xs < 0x1p-96f));
+                    if (wave_ballot(undecided)) t_dec = undecided ? near_root_exact(tca, d2, R2b) : t_dec;
+                    const bool exi = hb & group_any<PACKET>(t_dec < T);
+                    const uint64_t mi = wave_ballot(exi);
+                    e |= exi ? (1u << i) : 0u;
+                    pm |= (mi != 0ull ? 1u : 0u) << i;
+                }
             }
         }
         pend = pm;
@@ -368,6 +433,9 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     uint64_t idxN = 0;              // uniform: its heap index (root 0, child i of n: 9n+1+i)
     const float* node = L.root();   // uniform: its transform
     uint32_t actbits = ex0 ? 1u : 0u;   // per lane: bit L = active at the open node of depth L
+    // DFS stack in VGPR lanes (lane L = level L): {pending children | cursor << 16}, heap index lo/hi.
+    // v_writelane / v_readlane: no LDS traffic and no lane-0-only region in the loop.
+    uint32_t stk_pc = 0u, stk_lo = 0u, stk_hi = 0u;
     uint32_t pend;
     uint32_t eN = expand(node, 0u, ex0, pend);
 
@@ -383,10 +451,9 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 continue;
             }
             // save the open node's state, enter child c
-            {   // every lane writes the same words (no lane-0-only region inside the DFS loop)
-                uint32_t* st = L.stack(d);
-                *reinterpret_cast<uint4*>(st) = make_uint4(pend, cN, (uint32_t)idxN, (uint32_t)(idxN >> 32));
-            }
+            stk_pc = writelane_u(pend | (cN << 16), d, stk_pc);
+            stk_lo = writelane_u((uint32_t)idxN, d, stk_lo);
+            stk_hi = writelane_u((uint32_t)(idxN >> 32), d, stk_hi);
             L.E(d)[lane] = (uint16_t)eN;
             const bool a = ((eN >> c) & 1u) != 0u;
             const uint32_t bit = 1u << (d + 1u);
@@ -408,7 +475,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             const float4 c = *reinterpret_cast<const float4*>(node);
             const float tca = (c.x * dx + c.y * dy) + c.z * dz;
             const float d2 = c.w - tca * tca;
-            const float R2s = L.depth(d).y;
+            const float R2s = depth_consts(K, d).y;
             const bool in = d2 <= R2s;
             const bool hs = act && group_any<PACKET>(tca >= 0.0f) && group_any<PACKET>(in);
             if (wave_ballot(hs)) {
@@ -430,10 +497,11 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         d -= 1u;
         lds_fence();
         {
-            const uint32_t* st = L.stack(d);
-            pend = __builtin_amdgcn_readfirstlane(st[0]);
-            cN = __builtin_amdgcn_readfirstlane(st[1]);
-            idxN = (uint64_t)__builtin_amdgcn_readfirstlane(st[2]) | ((uint64_t)__builtin_amdgcn_readfirstlane(st[3]) << 32);
+            const uint32_t pc = __builtin_amdgcn_readlane(stk_pc, d);
+            pend = pc & 0xffffu;
+            cN = pc >> 16;
+            idxN = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(stk_lo, d) |
+                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(stk_hi, d) << 32);
         }
         eN = L.E(d)[lane];
         node = d == 0u ? L.root() : L.table(d - 1u) + cN * SF_LDS_CHILD;
@@ -570,8 +638,9 @@ __device__ __forceinline__ void trace_wave_body(const FrameArgs& a, uint32_t* ov
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t tile = blockIdx.x * WAVES + wv;
     if (tile >= a.tiles_x * a.tile_rows) return;
-    const TileStats st = trace_tile<false>(a, lds + wv * SF_LDS_WAVE_FLOATS(a.max_depth), tile, a.max_depth,
-                                           overflow_list, overflow_count);
+    float* const L = lds + wv * SF_LDS_WAVE_FLOATS(a.max_depth);
+    stage_root(L, a.root);
+    const TileStats st = trace_tile<false>(a, L, tile, a.max_depth, overflow_list, overflow_count);
     publish_stats(a, st.maxd, st.closest, 0u);
 }
 
@@ -603,27 +672,42 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a, uint32_t* o
     uint32_t* const ovc = counters + parity;
     float* const L = lds + wv * SF_LDS_WAVE_FLOATS(a.max_depth);
     const uint32_t ntiles = a.tiles_x * a.tile_rows;
+    stage_root(L, a.root);
     int32_t maxd = -1;
     float closest = FLT_MAX;
     for (;;) {
         const uint32_t t = wave_fetch_add(queue, 1u);   // uniform
         if (t >= ntiles) break;   // every wave reaches this: the queue only grows
-        const TileStats st = trace_tile<false>(a, L, t, a.max_depth, overflow_list, ovc);
+        // Re-read the launch arguments every tile (scalar loads from the kernarg segment) instead of
+        // keeping ~40 of them live in SGPRs across the whole persistent loop.
+        // (FrameArgs is the first kernel argument: offset 0 of the kernarg segment)
+        FrameArgs at;
+#if defined(__HIP_DEVICE_COMPILE__)
+        {
+            typedef const __attribute__((address_space(4))) FrameArgs* KernargArgs;
+            KernargArgs pa = (KernargArgs)__builtin_amdgcn_kernarg_segment_ptr();
+            __asm__ volatile("" : "+s"(pa));
+            __builtin_memcpy(&at, (const FrameArgs*)pa, sizeof(FrameArgs));
+        }
+#else
+        at = a;
+#endif
+        const TileStats st = trace_tile<false>(at, L, t, at.max_depth, overflow_list, ovc);
         maxd = st.maxd > maxd ? st.maxd : maxd;
         closest = fminf(closest, st.closest);
     }
     publish_stats(a, maxd, closest, 0u);
 }
 
-extern "C" __global__ __launch_bounds__(64) void sf_trace_queue1(FrameArgs a, uint32_t* ol, uint32_t* cnt, uint32_t parity)
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_trace_queue1(FrameArgs a, uint32_t* ol, uint32_t* cnt, uint32_t parity)
 {
     trace_queue_body<1>(a, ol, cnt, parity);
 }
-extern "C" __global__ __launch_bounds__(128) void sf_trace_queue2(FrameArgs a, uint32_t* ol, uint32_t* cnt, uint32_t parity)
+extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_trace_queue2(FrameArgs a, uint32_t* ol, uint32_t* cnt, uint32_t parity)
 {
     trace_queue_body<2>(a, ol, cnt, parity);
 }
-extern "C" __global__ __launch_bounds__(256) void sf_trace_queue4(FrameArgs a, uint32_t* ol, uint32_t* cnt, uint32_t parity)
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_trace_queue4(FrameArgs a, uint32_t* ol, uint32_t* cnt, uint32_t parity)
 {
     trace_queue_body<4>(a, ol, cnt, parity);
 }
@@ -639,6 +723,7 @@ extern "C" __global__ __launch_bounds__(64) void sf_fixup_wave(FrameArgs a, cons
     int32_t maxd = -1;
     float closest = FLT_MAX;
     uint32_t unresolved = 0u;
+    stage_root(lds, a.root);
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const TileStats st = trace_tile<true>(a, lds, overflow_list[i], SF_MAX_LEVELS, nullptr, nullptr);
         maxd = st.maxd > maxd ? st.maxd : maxd;
@@ -851,6 +936,7 @@ extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace(FrameArgs 
     HitState h;
     int32_t maxd = -1;
     bool overflowed = false;
+    stage_root(lds, a.root);
     traverse<true>(K, a.root, lds, SF_PROGRESSIVE_LEVELS, dx, dy, dz, valid, h, maxd, overflowed, a.flags);
 
     PacketLane out;
