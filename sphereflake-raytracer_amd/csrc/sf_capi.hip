@@ -62,7 +62,7 @@ struct sf_ctx {
     float* min_t = nullptr;
     uint32_t* hit_index = nullptr;
     int32_t* stats = nullptr;          // [0] max depth, [1] closest key, [2] unrecoverable overflow
-    uint32_t* ovf_counters = nullptr;  // [0,1] overflow counts, [2,3] tile queues; alternating per render
+    uint32_t* ovf_counters = nullptr;  // [0,1] overflow counts, then the tile queues (SF_QUEUE_WORD); alternating per render
     uint32_t* ovf_list = nullptr;      // tiles_x * tiles_y entries
     DeviceConsts* consts = nullptr;
     DeviceConsts host_consts;
@@ -226,7 +226,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if ((e = hipMalloc(&c->min_t, npx * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->hit_index, npx * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->stats, 16)) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&c->ovf_counters, 16)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->ovf_counters, SF_COUNTER_WORDS * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->ovf_list, ntiles * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->consts, sizeof(DeviceConsts))) != hipSuccess) return fail(e);
     if ((e = hipHostMalloc(&c->h_depth, 4, hipHostMallocDefault)) != hipSuccess) return fail(e);
@@ -237,7 +237,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if ((e = hipMemsetAsync(c->min_t, 0, npx * 4, c->stream)) != hipSuccess) return fail(e);
     if ((e = hipMemsetAsync(c->hit_index, 0xff, npx * 4, c->stream)) != hipSuccess) return fail(e);
     if ((e = hipMemsetAsync(c->stats, 0, 16, c->stream)) != hipSuccess) return fail(e);
-    if ((e = hipMemsetAsync(c->ovf_counters, 0, 16, c->stream)) != hipSuccess) return fail(e);
+    if ((e = hipMemsetAsync(c->ovf_counters, 0, SF_COUNTER_WORDS * 4, c->stream)) != hipSuccess) return fail(e);
     sfhost::child_transforms(c->child);
     int rc = upload_consts(c);
     if (rc == SF_OK) rc = reset_stats_dev(c, 3);

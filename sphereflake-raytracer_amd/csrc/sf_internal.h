@@ -27,6 +27,13 @@
 // levels - 1 level images: the deepest provisioned level's table is never read (see traverse)
 #define SF_LDS_WAVE_FLOATS(levels) (SF_LDS_ROOT + ((levels) - 1) * SF_LDS_LEVEL)
 
+// Persistent-kernel tile queues: SF_QUEUES counters per render parity, one 128-byte line each, after
+// the two overflow counters (u32 words).
+#define SF_QUEUES 8u
+#define SF_QUEUE_STRIDE 32u
+#define SF_QUEUE_WORD(parity, k) (SF_QUEUE_STRIDE + ((parity) * SF_QUEUES + (k)) * SF_QUEUE_STRIDE)
+#define SF_COUNTER_WORDS (SF_QUEUE_STRIDE + 2u * SF_QUEUES * SF_QUEUE_STRIDE)
+
 #define SF_FLAG_NO_LOD_CULL 1u   // disable the per-child LOD reachability cull (A/B only; results identical)
 
 struct DepthTables {

@@ -94,6 +94,7 @@ struct HitState {
     float minT;
     float cx, cy, cz;     // centre of the nearest accepted sphere
     uint32_t index;       // its heap index (low 32 bits)
+    int32_t depth;        // its depth (wave traversal: tie-breaking, see traverse)
     bool hit;
 };
 
@@ -283,7 +284,10 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     h.minT = FLT_MAX;
     h.cx = h.cy = h.cz = 0.f;
     h.index = 0xffffffffu;
+    h.depth = -1;
     h.hit = false;
+    // Per lane: the current best sphere is an ancestor of the node being expanded (see the self test).
+    bool anc = false;
 
     // ---- root node (depth 0): bounding sphere + LOD, centre straight from the kernel arguments
     const float rcx = root[9], rcy = root[10], rcz = root[11];
@@ -314,6 +318,10 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     for (int j = 0; j < 4; ++j) b[j] = K->child[bi][4u * bc + j];
     const uint32_t slot = bi * SF_LDS_CHILD + (bc == 3u ? 0u : 4u + 4u * bc);
 
+    uint32_t d = 0;                 // uniform: depth of the open (expanded) node
+    uint32_t cN = 0;                // uniform: its index in the parent's table
+    uint64_t idxN = 0;              // uniform: its heap index (root 0, child i of n: 9n+1+i)
+
     // ---- expand the node at `node` (depth d, transform in LDS): build its 9 child transforms into
     // table(d), then test the children (depth d+1) for the lanes in `act`. Returns this lane's 9-bit
     // "child expands" vector; *pend = the wave's mask of children some lane expands.
@@ -324,8 +332,38 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         const float4 p0 = *reinterpret_cast<const float4*>(node + 4);
         const float4 p1 = *reinterpret_cast<const float4*>(node + 8);
         const float4 p2 = *reinterpret_cast<const float4*>(node + 12);
-        const float4 dtn = depth_consts(K, d);        // (4/3) r of this node
+        const float4 dtn = depth_consts(K, d);        // this node: r^2, (4/3) r
         const float4 dtc = depth_consts(K, d + 1u);   // children: (2r)^2, T
+        // ---- the node's own sphere (Sphereflake.h:174-224), tested here, when the node opens, with
+        // the centre already in registers. The reference tests it after the children (post-order)
+        // and accepts strictly smaller t, so on an exact tie the earlier node in post-order wins.
+        // Pre-order differs from post-order only for ancestor/descendant pairs, hence: a tie is
+        // accepted iff the current best is an ancestor of this node (`anc`). Same result as the
+        // reference's order in every case.
+        {
+            const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
+            const float d2 = pc.w - tca * tca;
+            const float R2s = dtn.y;
+            const bool f0 = tca >= 0.0f, in = d2 <= R2s;
+            bool hs;
+            if constexpr (PACKET) hs = act && group_any<PACKET>(f0) && group_any<PACKET>(in);
+            else hs = act & f0 & in;
+            const uint64_t hsm = PACKET ? wave_ballot(hs) : (wave_ballot(act) & wave_ballot(f0) & wave_ballot(in));
+            if (hsm) {
+                const float ts = near_root(tca, d2, R2s);
+                const bool acc = hs && in && ((ts < h.minT) || ((ts == h.minT) && anc));
+                if (acc) {
+                    h.minT = ts;
+                    h.cx = pc.x;
+                    h.cy = pc.y;
+                    h.cz = pc.z;
+                    h.index = (uint32_t)idxN;
+                    h.depth = (int32_t)d;
+                    h.hit = true;
+                }
+                anc = anc | acc;
+            }
+        }
         // world = parent * child (SIMD_AVX.h:59-81), child translation scaled by (4/3) r (Sphereflake.h:162-172):
         // column 3 lanes multiply b0..b2 by s, the others by 1 (exact)
         const float sm = bc == 3u ? dtn.z : 1.0f;
@@ -428,16 +466,11 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         return e;
     };
 
-    uint32_t d = 0;                 // uniform: depth of the open (expanded) node
-    uint32_t cN = 0;                // uniform: its index in the parent's table
-    uint64_t idxN = 0;              // uniform: its heap index (root 0, child i of n: 9n+1+i)
-    const float* node = L.root();   // uniform: its transform
-    uint32_t actbits = ex0 ? 1u : 0u;   // per lane: bit L = active at the open node of depth L
     // DFS stack in VGPR lanes (lane L = level L): {pending children | cursor << 16}, heap index lo/hi.
-    // v_writelane / v_readlane: no LDS traffic and no lane-0-only region in the loop.
+    // Lane selects: no LDS traffic and no lane-0-only region in the loop.
     uint32_t stk_pc = 0u, stk_lo = 0u, stk_hi = 0u;
     uint32_t pend;
-    uint32_t eN = expand(node, 0u, ex0, pend);
+    uint32_t eN = expand(L.root(), 0u, ex0, pend);
 
     for (;;) {
         d = __builtin_amdgcn_readfirstlane(d);
@@ -456,11 +489,9 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             stk_hi = writelane_u((uint32_t)(idxN >> 32), d, stk_hi);
             L.E(d)[lane] = (uint16_t)eN;
             const bool a = ((eN >> c) & 1u) != 0u;
-            const uint32_t bit = 1u << (d + 1u);
-            actbits = a ? (actbits | bit) : (actbits & ~bit);
+            const float* node = L.table(d) + c * SF_LDS_CHILD;
             idxN = 9u * idxN + 1u + c;
             cN = c;
-            node = L.table(d) + c * SF_LDS_CHILD;
             d += 1u;
             maxd = (int32_t)d > maxd ? (int32_t)d : maxd;            // Sphereflake.h:157-160
             SF_STAMP(1);
@@ -468,29 +499,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             SF_STAMP(2);
             continue;
         }
-        // ---- all children done: the open node's own sphere (Sphereflake.h:174-224)
-        SF_STAMP(3);
-        {
-            const bool act = ((actbits >> d) & 1u) != 0u;
-            const float4 c = *reinterpret_cast<const float4*>(node);
-            const float tca = (c.x * dx + c.y * dy) + c.z * dz;
-            const float d2 = c.w - tca * tca;
-            const float R2s = depth_consts(K, d).y;
-            const bool in = d2 <= R2s;
-            const bool hs = act && group_any<PACKET>(tca >= 0.0f) && group_any<PACKET>(in);
-            if (wave_ballot(hs)) {
-                const float ts = near_root(tca, d2, R2s);
-                const bool acc = hs && in && (ts < h.minT);           // strict: the first wins ties
-                if (acc) {
-                    h.minT = ts;
-                    h.cx = c.x;
-                    h.cy = c.y;
-                    h.cz = c.z;
-                    h.index = (uint32_t)idxN;
-                    h.hit = true;
-                }
-            }
-        }
+        // ---- the node at depth d is finished: a best sphere at depth d is no longer an ancestor
+        anc = anc & (h.depth != (int32_t)d);
         SF_STAMP(4);
         if (d == 0u) break;
         // ---- back to the parent
@@ -504,7 +514,6 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(stk_hi, d) << 32);
         }
         eN = L.E(d)[lane];
-        node = d == 0u ? L.root() : L.table(d - 1u) + cN * SF_LDS_CHILD;
         (void)__builtin_amdgcn_readfirstlane(eN);   // (stamp builds: close the pop segment after its reads)
         SF_STAMP(5);
     }
@@ -547,7 +556,7 @@ __device__ __forceinline__ void write_pixel(const FrameArgs& a, const Tile& t, f
 
 struct TileStats {
     int32_t maxd;       // uniform: deepest expanded node (-1: none)
-    float closest;      // uniform: min minT over the tile's valid rays
+    float closest;      // per lane: its minT (FLT_MAX for invalid lanes); reduced in publish_stats
     bool overflowed;    // uniform: the tile needs more LDS levels than provisioned
 };
 
@@ -570,7 +579,7 @@ __device__ __forceinline__ uint32_t wave_fetch_add(uint32_t* p, uint32_t v)
         : "=&v"(r), "=&s"(saved), "=s"(out)
         : "v"(zero), "v"(v), "s"(p)
         : "memory");
-    return out;
+    return __builtin_amdgcn_readfirstlane(out);   // asm results count as divergent: say it is uniform
 }
 
 template <bool FIXUP>
@@ -612,14 +621,15 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     // stats: max depth reached, closest sphere distance (Sphereflake.h:157-160, Sphereflake.cpp:197-200)
     TileStats st;
     st.maxd = maxd;
-    st.closest = wave_min(t.valid ? h.minT : FLT_MAX);
+    st.closest = t.valid ? h.minT : FLT_MAX;
     st.overflowed = overflowed;
     return st;
 }
 
-// Publish one wave's stats (outside any loop: lane-0 regions are harmless here).
+// Publish one wave's stats (outside any loop: lane-0 regions are harmless here). `closest` per lane.
 __device__ __forceinline__ void publish_stats(const FrameArgs& a, int32_t maxd, float closest, uint32_t unresolved)
 {
+    closest = wave_min(closest);
     if ((threadIdx.x & 63u) == 0u) {
         if (maxd >= 0) atomicMax(&a.stats[0], maxd);
         atomicMin(&a.stats[1], sf_float_key(closest));
@@ -667,17 +677,28 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a, uint32_t* o
 {
     extern __shared__ float lds[];
     const uint32_t wv = threadIdx.x >> 6;
-    if (blockIdx.x == 0 && threadIdx.x == 0) counters[2u + (parity ^ 1u)] = 0u;
-    uint32_t* const queue = counters + 2u + parity;
+    // SF_QUEUES tile queues per render, one cache line each: queue k hands out tiles k, k + 8, k + 16, ...
+    // A wave starts on its own XCD's queue and moves on to the next one when it runs dry. One queue
+    // for the whole chip serialises ~100 atomics/us on one address (measured: ~11 us per fetch).
+    if (blockIdx.x == 0 && threadIdx.x < SF_QUEUES)
+        counters[SF_QUEUE_WORD(parity ^ 1u, threadIdx.x)] = 0u;   // the next render's queues
     uint32_t* const ovc = counters + parity;
     float* const L = lds + wv * SF_LDS_WAVE_FLOATS(a.max_depth);
     const uint32_t ntiles = a.tiles_x * a.tile_rows;
     stage_root(L, a.root);
+    uint32_t xcc;
+    __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    uint32_t k = __builtin_amdgcn_readfirstlane(xcc) & (SF_QUEUES - 1u), dry = 0u;
     int32_t maxd = -1;
-    float closest = FLT_MAX;
+    float closest = FLT_MAX;   // per lane
     for (;;) {
-        const uint32_t t = wave_fetch_add(queue, 1u);   // uniform
-        if (t >= ntiles) break;   // every wave reaches this: the queue only grows
+        const uint32_t q = wave_fetch_add(counters + SF_QUEUE_WORD(parity, k), 1u);   // uniform
+        const uint32_t t = q * SF_QUEUES + k;
+        if (t >= ntiles) {        // queue k is empty: the next one; done when all are
+            if (++dry == SF_QUEUES) break;
+            k = (k + 1u) & (SF_QUEUES - 1u);
+            continue;
+        }
         // Re-read the launch arguments every tile (scalar loads from the kernarg segment) instead of
         // keeping ~40 of them live in SGPRs across the whole persistent loop.
         // (FrameArgs is the first kernel argument: offset 0 of the kernarg segment)
