@@ -181,6 +181,15 @@ float sf_rsqrtps(float x);
 int sf_set_tile_trace(sf_ctx* ctx, int enable);
 int sf_get_tile_trace(sf_ctx* ctx, uint64_t* out, size_t n);   /* n >= 3 * tiles; synchronises */
 
+/* --- measurement ---------------------------------------------------------- */
+
+/* When enabled, every full-frame render records HIP events on its launch stream around its main
+   trace kernel (the dominant kernel; the roofline in bench.py is priced on it). */
+int sf_set_kernel_timing(sf_ctx* ctx, int enable);
+/* Durations (ms) of the main trace kernel of the last min(n, 64) timed renders, oldest first;
+   returns how many were written (>= 0) or a negative SF_E*. Synchronises. */
+int sf_kernel_times(sf_ctx* ctx, float* ms, uint32_t n);
+
 /* --- misc ---------------------------------------------------------------- */
 
 const char* sf_strerror(int status);

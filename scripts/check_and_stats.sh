@@ -1,0 +1,3 @@
+set -e
+bash scripts/run_check.sh
+bash scripts/stats_run.sh st10

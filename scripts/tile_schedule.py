@@ -22,6 +22,8 @@ def main():
     a = ap.parse_args()
     with sf.Sphereflake(a.width, a.height) as s:
         s.SetCamera(sf.config_camera(a.width, a.height, a.K))
+        s.Render()
+        s.Synchronize()   # settle the adaptive LDS levels (host hint) before the traced renders
         s.tile_trace(True)
         for _ in range(a.reps):
             s.Render()

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -18,9 +19,12 @@
 extern "C" __global__ void sf_trace_wave1(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
 extern "C" __global__ void sf_trace_wave2(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
 extern "C" __global__ void sf_trace_wave4(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
-extern "C" __global__ void sf_trace_queue1(FrameArgs a, uint32_t* overflow_list, uint32_t* counters, uint32_t parity);
-extern "C" __global__ void sf_trace_queue2(FrameArgs a, uint32_t* overflow_list, uint32_t* counters, uint32_t parity);
-extern "C" __global__ void sf_trace_queue4(FrameArgs a, uint32_t* overflow_list, uint32_t* counters, uint32_t parity);
+extern "C" __global__ void sf_trace_queue1(FrameArgs a);
+extern "C" __global__ void sf_trace_queue2(FrameArgs a);
+extern "C" __global__ void sf_trace_queue4(FrameArgs a);
+extern "C" __global__ void sf_order_scan(const uint32_t* chunk_cnt, uint32_t nc, uint32_t* chunk_off);
+extern "C" __global__ void sf_order_scatter(const uint32_t* cost, uint32_t n, uint32_t* chunk_cnt,
+                                            const uint32_t* chunk_off, uint32_t* order);
 extern "C" __global__ void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list, uint32_t* counters,
                                          uint32_t parity);
 extern "C" __global__ void sf_trace_ray(FrameArgs a);
@@ -95,6 +99,21 @@ struct sf_ctx {
     // a tile that needs more is re-traced by sf_fixup_wave, so a stale hint costs time, never results.
     int32_t* h_depth = nullptr;
     uint64_t* tile_trace = nullptr;    // diagnostics: per tile {start, end, hw id}
+    // Heavy-first tile scheduling: every persistent render records per-tile cycles; sf_tile_order
+    // turns them into the next render's tile permutation (heaviest first), so the tail of the
+    // persistent kernel drains light tiles. Results never depend on the order.
+    uint32_t* tile_cost = nullptr;
+    uint32_t* tile_order = nullptr;
+    uint32_t* chunk_cnt = nullptr;     // per 64-tile chunk x SF_ORDER_BUCKETS (zeroed by sf_order_scatter)
+    uint32_t* chunk_off = nullptr;
+    uint32_t order_n = 0;              // tile count the current tile_order is a permutation of (0: none)
+    hipStream_t order_stream = nullptr;   // the stream it was computed on (used only on the same stream)
+    bool use_order = true;             // env SF_ORDER=0: row-major order always
+    // Measurement: HIP events around the main trace kernel of each render (sf_set_kernel_timing)
+    static constexpr int kTimed = 64;
+    hipEvent_t ev[kTimed][2] = {};
+    bool timing = false;
+    uint32_t ev_next = 0, ev_count = 0;
 };
 
 #define SF_HIP(ctx, expr)                                        \
@@ -125,6 +144,13 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->owner);
     if (c->h_depth) (void)hipHostFree(c->h_depth);
     (void)hipFree(c->tile_trace);
+    (void)hipFree(c->tile_cost);
+    (void)hipFree(c->tile_order);
+    (void)hipFree(c->chunk_cnt);
+    (void)hipFree(c->chunk_off);
+    for (int i = 0; i < sf_ctx::kTimed; ++i)
+        for (int j = 0; j < 2; ++j)
+            if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -134,10 +160,13 @@ static int upload_consts(sf_ctx* c)
     std::memcpy(c->host_consts.child, c->child, sizeof c->child);
     sfhost::depth_tables(&c->host_consts.dt);
     for (int d = 0; d < SF_DEPTH_TABLE; ++d) {
-        c->host_consts.depth4[d][0] = c->host_consts.dt.r2_bound[d];
-        c->host_consts.depth4[d][1] = c->host_consts.dt.r2_self[d];
-        c->host_consts.depth4[d][2] = c->host_consts.dt.scale[d];
-        c->host_consts.depth4[d][3] = c->host_consts.dt.lod[d];
+        float* e = c->host_consts.depth8[d];
+        e[0] = c->host_consts.dt.r2_bound[d];
+        e[1] = c->host_consts.dt.r2_self[d];
+        e[2] = c->host_consts.dt.scale[d];
+        e[3] = c->host_consts.dt.lod[d];
+        e[4] = sfhost::leaf_threshold(&c->host_consts.dt, (uint32_t)d);
+        e[5] = e[6] = e[7] = 0.0f;
     }
     std::memcpy(c->host_consts.lut, kLut, sizeof kLut);
     sfhost::sobol_matrices(c->host_consts.sobol);
@@ -202,6 +231,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     c->fixup_blocks = prop.multiProcessorCount;
     c->cus = prop.multiProcessorCount;
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_ORDER")) c->use_order = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_FLAGS")) c->flags = (uint32_t)std::strtoul(ev, nullptr, 0);
     if (const char* ev = std::getenv("SF_TRACE_WAVES")) {
         const int w = std::atoi(ev);
@@ -228,6 +258,12 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if ((e = hipMalloc(&c->stats, 16)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->ovf_counters, SF_COUNTER_WORDS * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->ovf_list, ntiles * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->tile_cost, ntiles * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->tile_order, ntiles * 4)) != hipSuccess) return fail(e);
+    const size_t nchunks = (ntiles + 63) / 64;
+    if ((e = hipMalloc(&c->chunk_cnt, nchunks * SF_ORDER_BUCKETS * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->chunk_off, nchunks * SF_ORDER_BUCKETS * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMemsetAsync(c->chunk_cnt, 0, nchunks * SF_ORDER_BUCKETS * 4, c->stream)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->consts, sizeof(DeviceConsts))) != hipSuccess) return fail(e);
     if ((e = hipHostMalloc(&c->h_depth, 4, hipHostMallocDefault)) != hipSuccess) return fail(e);
     *c->h_depth = -1;
@@ -353,6 +389,9 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
     a.min_t = min_t;
     a.hit_index = hidx;
     a.tile_trace = c->tile_trace;
+    a.counters = c->ovf_counters;
+    a.overflow_list = c->ovf_list;
+    a.parity = c->parity;
     if (c->tile_trace) {
         const size_t ntr = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8);
         a.phase_sums = c->tile_trace + 3 * ntr;
@@ -367,10 +406,31 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
     } else {
         const bool autod = p.max_depth == 0;
         uint32_t levels = kDefaultLevels;
-        const int32_t seen = *(volatile int32_t*)c->h_depth;
-        if (seen >= 0) levels = (uint32_t)seen + 1u < 4u ? 4u : (uint32_t)seen + 1u;
+        // Geometric bound: every sphere lies inside the root's bounding sphere (radius 2 around the
+        // root centre), so a depth-d node can pass the LOD test (t < T_d, Sphereflake.h:146) only if
+        // |root centre| - 2 < T_d. The deepest such d + 1 levels suffice; a bound that is off only
+        // costs a re-trace of the affected tiles (sf_fixup_wave), never results.
+        const float rc = std::sqrt(c->root[12] * c->root[12] + c->root[13] * c->root[13] + c->root[14] * c->root[14]);
+        const float gap = (rc - 2.0f) * (1.0f - 1e-3f);
+        bool bounded = false;   // levels proven sufficient: no tile can overflow
+        if (gap > 0.0f) {
+            uint32_t dmax = 0;
+            while (dmax + 1u < SF_DEPTH_TABLE && c->host_consts.dt.lod[dmax + 1u] > gap) ++dmax;
+            levels = dmax + 1u;
+            bounded = levels <= SF_MAX_DEPTH_LIMIT;
+        }
+        const int32_t seen = *(volatile int32_t*)c->h_depth;   // max depth of a finished render
+        if (seen >= 0 && (uint32_t)seen + 1u < levels) {
+            levels = (uint32_t)seen + 1u;
+            bounded = false;
+        }
+        if (levels < 4u) levels = 4u;
         if (levels > SF_MAX_DEPTH_LIMIT) levels = SF_MAX_DEPTH_LIMIT;
-        if (c->levels_override) levels = c->levels_override;
+        if (c->levels_override) {
+            levels = c->levels_override;
+            bounded = false;
+        }
+        if (!autod) bounded = bounded && p.max_depth >= levels;
         a.max_depth = autod ? levels : p.max_depth;
         const size_t lds = (size_t)SF_LDS_WAVE_FLOATS(a.max_depth) * 4;
         uint32_t* cnt = c->ovf_counters + c->parity;
@@ -390,9 +450,31 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             const uint32_t need = (ntiles + wpb - 1) / wpb;
             if (nblk > need) nblk = need;
             const dim3 grid(nblk);
-            if (wpb == 1) hipLaunchKernelGGL(sf_trace_queue1, grid, block, lds, s, a, c->ovf_list, c->ovf_counters, c->parity);
-            else if (wpb == 2) hipLaunchKernelGGL(sf_trace_queue2, grid, block, 2 * lds, s, a, c->ovf_list, c->ovf_counters, c->parity);
-            else hipLaunchKernelGGL(sf_trace_queue4, grid, block, 4 * lds, s, a, c->ovf_list, c->ovf_counters, c->parity);
+            if (c->use_order) {
+                a.tile_cost = c->tile_cost;
+                a.chunk_cnt = c->chunk_cnt;
+                a.tile_order = (c->order_n == ntiles && c->order_stream == s) ? c->tile_order : nullptr;
+            }
+            if (c->timing) SF_HIP(c, hipEventRecord(c->ev[c->ev_next][0], s));
+            if (wpb == 1) hipLaunchKernelGGL(sf_trace_queue1, grid, block, lds, s, a);
+            else if (wpb == 2) hipLaunchKernelGGL(sf_trace_queue2, grid, block, 2 * lds, s, a);
+            else hipLaunchKernelGGL(sf_trace_queue4, grid, block, 4 * lds, s, a);
+            SF_HIP(c, hipGetLastError());
+            if (c->timing) {
+                SF_HIP(c, hipEventRecord(c->ev[c->ev_next][1], s));
+                c->ev_next = (c->ev_next + 1u) % sf_ctx::kTimed;
+                c->ev_count = c->ev_count < (uint32_t)sf_ctx::kTimed ? c->ev_count + 1u : c->ev_count;
+            }
+            if (c->use_order) {   // the next render's tile order, from this render's tile costs
+                const uint32_t nc = (ntiles + 63u) / 64u;
+                hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->chunk_cnt, nc, c->chunk_off);
+                SF_HIP(c, hipGetLastError());
+                hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost, ntiles,
+                                   c->chunk_cnt, (const uint32_t*)c->chunk_off, c->tile_order);
+                SF_HIP(c, hipGetLastError());
+                c->order_n = ntiles;
+                c->order_stream = s;
+            }
         } else {
             const dim3 grid((ntiles + wpb - 1) / wpb);
             if (wpb == 1) hipLaunchKernelGGL(sf_trace_wave1, grid, block, lds, s, a, c->ovf_list, cnt);
@@ -400,12 +482,17 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             else hipLaunchKernelGGL(sf_trace_wave4, grid, block, 4 * lds, s, a, c->ovf_list, cnt);
         }
         SF_HIP(c, hipGetLastError());
-        const size_t lds_fix = (size_t)SF_LDS_WAVE_FLOATS(SF_MAX_DEPTH_LIMIT) * 4;
-        hipLaunchKernelGGL(sf_fixup_wave, dim3(4 * c->fixup_blocks), dim3(64), lds_fix, s, a,
-                           (const uint32_t*)c->ovf_list, c->ovf_counters, c->parity);
-        SF_HIP(c, hipGetLastError());
+        // Re-trace of overflowed tiles, unless the levels are proven sufficient (persistent kernel;
+        // it also zeroes the next render's overflow counter itself).
+        if (!(bounded && c->persistent)) {
+            const size_t lds_fix = (size_t)SF_LDS_WAVE_FLOATS(SF_MAX_DEPTH_LIMIT) * 4;
+            hipLaunchKernelGGL(sf_fixup_wave, dim3(4 * c->fixup_blocks), dim3(64), lds_fix, s, a,
+                               (const uint32_t*)c->ovf_list, c->ovf_counters, c->parity);
+            SF_HIP(c, hipGetLastError());
+        }
         c->parity ^= 1u;
-        SF_HIP(c, hipMemcpyAsync(c->h_depth, c->stats, 4, hipMemcpyDeviceToHost, s));
+        // LDS-level hint for later renders: only needed when the geometric bound is unavailable
+        if (!bounded) SF_HIP(c, hipMemcpyAsync(c->h_depth, c->stats, 4, hipMemcpyDeviceToHost, s));
     }
     uint32_t rows = 0;
     for (uint32_t b = p.band_index; b < bands; b += band_count) {
@@ -554,6 +641,33 @@ int sf_device_buffers(sf_ctx* c, float** pos4, float** nrm4, float** min_t, uint
     if (min_t) *min_t = c->min_t;
     if (hidx) *hidx = c->hit_index;
     return SF_OK;
+}
+
+int sf_set_kernel_timing(sf_ctx* c, int enable)
+{
+    if (!c) return SF_EINVAL;
+    DevGuard g(c->device);
+    if (enable && !c->ev[0][0]) {
+        for (int i = 0; i < sf_ctx::kTimed; ++i)
+            for (int j = 0; j < 2; ++j) SF_HIP(c, hipEventCreate(&c->ev[i][j]));
+    }
+    c->timing = enable != 0;
+    c->ev_next = c->ev_count = 0;
+    return SF_OK;
+}
+
+int sf_kernel_times(sf_ctx* c, float* ms, uint32_t n)
+{
+    if (!c || !ms) return SF_EINVAL;
+    DevGuard g(c->device);
+    SF_HIP(c, hipStreamSynchronize(c->stream));
+    const uint32_t k = n < c->ev_count ? n : c->ev_count;
+    for (uint32_t i = 0; i < k; ++i) {   // the k most recent, oldest first
+        const uint32_t slot = (c->ev_next + sf_ctx::kTimed - k + i) % sf_ctx::kTimed;
+        SF_HIP(c, hipEventSynchronize(c->ev[slot][1]));
+        SF_HIP(c, hipEventElapsedTime(&ms[i], c->ev[slot][0], c->ev[slot][1]));
+    }
+    return (int)k;
 }
 
 int sf_get_stats(sf_ctx* c, sf_stats* out)

@@ -14,7 +14,7 @@
 #define SF_TILE 8              // a wave64 traces one 8x8 pixel tile
 #define SF_WAVES_PER_BLOCK 4   // 256-thread workgroups (per-ray kernel)
 #ifndef SF_TRACE_WAVES
-#define SF_TRACE_WAVES 1       // independent waves per workgroup of the wave kernels
+#define SF_TRACE_WAVES 2       // independent waves per workgroup of the wave kernels
 #endif
 // Wave-coherent traversal LDS image, per wave (units: floats):
 //   [root: 16][(levels - 1) x (table 144 | E 32)]
@@ -47,7 +47,10 @@ struct DepthTables {
 struct DeviceConsts {
     float child[9][16];               // unit child frames, glm column-major (Sphereflake.cpp:216-249)
     DepthTables dt;
-    float depth4[SF_DEPTH_TABLE][4];  // the same, interleaved {r2_bound, r2_self, scale, lod} (staged into LDS)
+    // the same interleaved per depth d, one scalar load: {r2_bound, r2_self, scale, lod,
+    // leaf, 0, 0, 0}; leaf = |c|^2 threshold beyond which no child of a depth-d node centred at c can
+    // pass the LOD test for any ray (sfhost::leaf_threshold)
+    float depth8[SF_DEPTH_TABLE][8];
     uint32_t lut[2048];               // x86 rsqrtps table (rsqrtps_lut.inc)
     uint32_t sobol[2][52];            // Sobol direction numbers, dims 0 and 1 (Sobol.cpp:34-39, 57-162)
 };
@@ -80,7 +83,15 @@ struct FrameArgs {
     int32_t* stats;                   // [0] max depth (atomicMax), [1] closest key (atomicMin), [2] overflow count
     uint64_t* tile_trace;             // diagnostics (NULL = off): per tile {start, end} s_memrealtime, hw id
     uint64_t* phase_sums;             // diagnostics, stamp builds only (make PHASES=1): 8 segment sums
+    uint32_t* counters;               // overflow counts + tile queues (SF_QUEUE_WORD), alternating per render
+    uint32_t* overflow_list;          // tiles to re-trace with SF_MAX_DEPTH_LIMIT levels
+    uint32_t parity;                  // which half of `counters` this render uses
+    uint32_t* tile_cost;              // out (NULL = off): per tile, shader cycles of its traversal
+    const uint32_t* tile_order;       // in (NULL = row-major): tile permutation, heaviest first
+    uint32_t* chunk_cnt;              // out (with tile_cost): per 64-tile chunk, cost-bucket histogram
 };
+
+#define SF_ORDER_BUCKETS 32u           // log-spaced cost buckets of sf_tile_order (2 per octave from 2^8 cycles)
 
 namespace sfhost {
 void child_transforms(float child[9][16]);
@@ -90,6 +101,7 @@ void camera_corners(uint32_t W, uint32_t H, const float pos[3], float pitch, flo
 float radius(uint32_t depth);
 float lod_threshold(float r);
 void depth_tables(DepthTables* t);
+float leaf_threshold(const DepthTables* t, uint32_t depth);
 void sobol_matrices(uint32_t out[2][52]);
 void mt19937_seed(uint32_t seed, uint32_t state[625]);
 }  // namespace sfhost

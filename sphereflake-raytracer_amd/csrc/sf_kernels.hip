@@ -245,9 +245,19 @@ __device__ __forceinline__ float4 depth_consts(const DeviceConsts* K, uint32_t d
 {
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef const __attribute__((address_space(4))) float4* ConstF4;
-    return ((ConstF4)(const void*)K->depth4)[d];
+    return ((ConstF4)(const void*)K->depth8)[2u * d];
 #else
-    return reinterpret_cast<const float4*>(K->depth4)[d];   // host pass: never executed
+    return reinterpret_cast<const float4*>(K->depth8)[2u * d];   // host pass: never executed
+#endif
+}
+// {leaf, 0, 0, 0} of depth d (see DeviceConsts::depth8)
+__device__ __forceinline__ float depth_leaf(const DeviceConsts* K, uint32_t d)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) float4* ConstF4;
+    return ((ConstF4)(const void*)K->depth8)[2u * d + 1u].x;
+#else
+    return reinterpret_cast<const float4*>(K->depth8)[2u * d + 1u].x;
 #endif
 }
 
@@ -320,7 +330,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
 
     uint32_t d = 0;                 // uniform: depth of the open (expanded) node
     uint32_t cN = 0;                // uniform: its index in the parent's table
-    uint64_t idxN = 0;              // uniform: its heap index (root 0, child i of n: 9n+1+i)
+    uint32_t idxN = 0;              // uniform: its heap index mod 2^32 (root 0, child i of n: 9n+1+i)
 
     // ---- expand the node at `node` (depth d, transform in LDS): build its 9 child transforms into
     // table(d), then test the children (depth d+1) for the lanes in `act`. Returns this lane's 9-bit
@@ -357,11 +367,20 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                     h.cx = pc.x;
                     h.cy = pc.y;
                     h.cz = pc.z;
-                    h.index = (uint32_t)idxN;
+                    h.index = idxN;
                     h.depth = (int32_t)d;
                     h.hit = true;
                 }
                 anc = anc | acc;
+            }
+        }
+        // No child of this node can pass the LOD test for any ray (sfhost::leaf_threshold): skip the
+        // build and the child tests (per-ray semantics only, like the reachability cull below).
+        if (lod_cull) {
+            const float leaf = depth_leaf(K, d);
+            if (__builtin_amdgcn_readfirstlane((int)(pc.w > leaf))) {
+                pend = 0u;
+                return 0u;
             }
         }
         // world = parent * child (SIMD_AVX.h:59-81), child translation scaled by (4/3) r (Sphereflake.h:162-172):
@@ -466,9 +485,9 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         return e;
     };
 
-    // DFS stack in VGPR lanes (lane L = level L): {pending children | cursor << 16}, heap index lo/hi.
+    // DFS stack in VGPR lanes (lane L = level L): {pending children | cursor << 16}, heap index.
     // Lane selects: no LDS traffic and no lane-0-only region in the loop.
-    uint32_t stk_pc = 0u, stk_lo = 0u, stk_hi = 0u;
+    uint32_t stk_pc = 0u, stk_ix = 0u;
     uint32_t pend;
     uint32_t eN = expand(L.root(), 0u, ex0, pend);
 
@@ -485,8 +504,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             }
             // save the open node's state, enter child c
             stk_pc = writelane_u(pend | (cN << 16), d, stk_pc);
-            stk_lo = writelane_u((uint32_t)idxN, d, stk_lo);
-            stk_hi = writelane_u((uint32_t)(idxN >> 32), d, stk_hi);
+            stk_ix = writelane_u(idxN, d, stk_ix);
             L.E(d)[lane] = (uint16_t)eN;
             const bool a = ((eN >> c) & 1u) != 0u;
             const float* node = L.table(d) + c * SF_LDS_CHILD;
@@ -510,8 +528,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             const uint32_t pc = __builtin_amdgcn_readlane(stk_pc, d);
             pend = pc & 0xffffu;
             cN = pc >> 16;
-            idxN = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(stk_lo, d) |
-                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(stk_hi, d) << 32);
+            idxN = (uint32_t)__builtin_amdgcn_readlane(stk_ix, d);
         }
         eN = L.E(d)[lane];
         (void)__builtin_amdgcn_readfirstlane(eN);   // (stamp builds: close the pop segment after its reads)
@@ -531,11 +548,15 @@ __device__ __forceinline__ Tile tile_of(const FrameArgs& a, uint32_t tile, uint3
     const uint32_t tx = tile % a.tiles_x, k = tile / a.tiles_x;
     const uint32_t band = a.band_index + (k / a.tiles_per_band) * a.band_count;
     const uint32_t ty = band * a.tiles_per_band + k % a.tiles_per_band;
+    // (opaque copy: recompute the lane's column/row per tile rather than keep them live, or spilled,
+    // across a persistent loop)
+    uint32_t l = lane;
+    __asm__ volatile("" : "+v"(l));
     Tile t;
-    t.x = tx * SF_TILE + (lane & 7u);
-    t.y = ty * SF_TILE + (lane >> 3);
+    t.x = tx * SF_TILE + (l & 7u);
+    t.y = ty * SF_TILE + (l >> 3);
     t.valid = t.x < a.W && t.y < a.H;
-    t.orow = a.compact ? (k * SF_TILE + (lane >> 3)) : t.y;
+    t.orow = a.compact ? (k * SF_TILE + (l >> 3)) : t.y;
     return t;
 }
 
@@ -582,6 +603,30 @@ __device__ __forceinline__ uint32_t wave_fetch_add(uint32_t* p, uint32_t v)
     return __builtin_amdgcn_readfirstlane(out);   // asm results count as divergent: say it is uniform
 }
 
+// One lane's global atomic increment on behalf of the wave, fire and forget (no return, no wait):
+// EXEC is forced to lane 0 inside the asm. The op stays counted in vmcnt, which only makes the
+// compiler's own later waits stricter.
+__device__ __forceinline__ void wave_atomic_inc_nowait(uint32_t* p)
+{
+    uint64_t saved;
+    const uint32_t zero = 0u, one = 1u;
+    __asm__ volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "global_atomic_add %1, %2, %3\n\t"
+        "s_mov_b64 exec, %0\n\t"
+        : "=&s"(saved)
+        : "v"(zero), "v"(one), "s"(p)
+        : "memory");
+}
+
+__device__ __forceinline__ uint32_t cost_bucket(uint32_t c)
+{
+    const uint32_t k = __float_as_uint((float)(c | 1u)) >> 22;   // exponent and 1 mantissa bit
+    const uint32_t b = k - (135u << 1);                            // c < 2^8 -> 0
+    return b < SF_ORDER_BUCKETS ? b : (k < (135u << 1) ? 0u : SF_ORDER_BUCKETS - 1u);
+}
+
 template <bool FIXUP>
 __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __restrict__ L, uint32_t tile,
                                                 uint32_t levels, uint32_t* overflow_list, uint32_t* overflow_count)
@@ -590,6 +635,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     const uint32_t lane = threadIdx.x & 63u;
     const Tile t = tile_of(a, tile, lane);
     const uint64_t t_start = a.tile_trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const uint64_t c_start = (!FIXUP && a.tile_cost) ? __builtin_amdgcn_s_memtime() : 0ull;
     float dx, dy, dz;
     ray_dir(a, (float)t.x, (float)t.y, dx, dy, dz, K->lut);
 
@@ -611,6 +657,14 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
         a.tile_trace[3u * tile + 2u] = ((uint64_t)xcc << 32) | hw;
     }
 
+    if (!FIXUP && a.tile_cost) {
+        // scheduling hint for the next render (sf_order_scan / sf_order_scatter); uniform values
+        const uint64_t cyc = __builtin_amdgcn_s_memtime() - c_start;
+        const uint32_t cost = cyc > 0xffffffffull ? 0xffffffffu : (uint32_t)cyc;
+        a.tile_cost[tile] = cost;
+        const uint32_t slot = __builtin_amdgcn_readfirstlane((tile >> 6) * SF_ORDER_BUCKETS + cost_bucket(cost));
+        wave_atomic_inc_nowait(a.chunk_cnt + slot);
+    }
     if (!FIXUP && overflowed) {
         // a deeper re-trace (sf_fixup_wave) rewrites this whole tile
         const uint32_t slot = wave_fetch_add(overflow_count, 1u);
@@ -627,12 +681,18 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
 }
 
 // Publish one wave's stats (outside any loop: lane-0 regions are harmless here). `closest` per lane.
+// Thousands of waves end together and atomics on one address serialise (~10 ns each), so a wave
+// first reads the current value and issues the atomic only if it would change it. The read may be
+// stale, never wrong: the values only move one way within a render.
 __device__ __forceinline__ void publish_stats(const FrameArgs& a, int32_t maxd, float closest, uint32_t unresolved)
 {
     closest = wave_min(closest);
     if ((threadIdx.x & 63u) == 0u) {
-        if (maxd >= 0) atomicMax(&a.stats[0], maxd);
-        atomicMin(&a.stats[1], sf_float_key(closest));
+        const int32_t key = sf_float_key(closest);
+        const int32_t cur_d = __hip_atomic_load(&a.stats[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int32_t cur_k = __hip_atomic_load(&a.stats[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (maxd > cur_d) atomicMax(&a.stats[0], maxd);
+        if (key < cur_k) atomicMin(&a.stats[1], key);
         if (unresolved) atomicAdd(&a.stats[2], (int32_t)unresolved);
     }
 }
@@ -672,8 +732,7 @@ extern "C" __global__ __launch_bounds__(256) void sf_trace_wave4(FrameArgs a, ui
 // and the in-order workgroup dispatcher otherwise idles CUs behind long tiles. counters: [0,1]
 // overflow counts, [2,3] tile queues, alternating per render (this render zeroes the next one's).
 template <int WAVES>
-__device__ __forceinline__ void trace_queue_body(const FrameArgs& a, uint32_t* overflow_list, uint32_t* counters,
-                                                 uint32_t parity)
+__device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 {
     extern __shared__ float lds[];
     const uint32_t wv = threadIdx.x >> 6;
@@ -681,8 +740,8 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a, uint32_t* o
     // A wave starts on its own XCD's queue and moves on to the next one when it runs dry. One queue
     // for the whole chip serialises ~100 atomics/us on one address (measured: ~11 us per fetch).
     if (blockIdx.x == 0 && threadIdx.x < SF_QUEUES)
-        counters[SF_QUEUE_WORD(parity ^ 1u, threadIdx.x)] = 0u;   // the next render's queues
-    uint32_t* const ovc = counters + parity;
+        a.counters[SF_QUEUE_WORD(a.parity ^ 1u, threadIdx.x)] = 0u;   // the next render's queues
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[a.parity ^ 1u] = 0u;   // and overflow count
     float* const L = lds + wv * SF_LDS_WAVE_FLOATS(a.max_depth);
     const uint32_t ntiles = a.tiles_x * a.tile_rows;
     stage_root(L, a.root);
@@ -692,16 +751,9 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a, uint32_t* o
     int32_t maxd = -1;
     float closest = FLT_MAX;   // per lane
     for (;;) {
-        const uint32_t q = wave_fetch_add(counters + SF_QUEUE_WORD(parity, k), 1u);   // uniform
-        const uint32_t t = q * SF_QUEUES + k;
-        if (t >= ntiles) {        // queue k is empty: the next one; done when all are
-            if (++dry == SF_QUEUES) break;
-            k = (k + 1u) & (SF_QUEUES - 1u);
-            continue;
-        }
         // Re-read the launch arguments every tile (scalar loads from the kernarg segment) instead of
         // keeping ~40 of them live in SGPRs across the whole persistent loop.
-        // (FrameArgs is the first kernel argument: offset 0 of the kernarg segment)
+        // (FrameArgs is the only kernel argument: offset 0 of the kernarg segment)
         FrameArgs at;
 #if defined(__HIP_DEVICE_COMPILE__)
         {
@@ -713,24 +765,119 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a, uint32_t* o
 #else
         at = a;
 #endif
-        const TileStats st = trace_tile<false>(at, L, t, at.max_depth, overflow_list, ovc);
+        const uint32_t q = wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u);   // uniform
+        const uint32_t g = q * SF_QUEUES + k;   // position in the render's tile order
+        if (g >= ntiles) {        // queue k is empty: the next one; done when all are
+            if (++dry == SF_QUEUES) break;
+            k = (k + 1u) & (SF_QUEUES - 1u);
+            continue;
+        }
+        uint32_t t = g;
+        if (at.tile_order) {      // heaviest tiles of the previous render first (scalar load)
+#if defined(__HIP_DEVICE_COMPILE__)
+            typedef const __attribute__((address_space(4))) uint32_t* ConstU32;
+            t = ((ConstU32)(const void*)at.tile_order)[g];
+#else
+            t = at.tile_order[g];
+#endif
+        }
+        const TileStats st = trace_tile<false>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity);
         maxd = st.maxd > maxd ? st.maxd : maxd;
         closest = fminf(closest, st.closest);
     }
     publish_stats(a, maxd, closest, 0u);
 }
 
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_trace_queue1(FrameArgs a, uint32_t* ol, uint32_t* cnt, uint32_t parity)
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_trace_queue1(FrameArgs a)
 {
-    trace_queue_body<1>(a, ol, cnt, parity);
+    trace_queue_body<1>(a);
 }
-extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_trace_queue2(FrameArgs a, uint32_t* ol, uint32_t* cnt, uint32_t parity)
+extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_trace_queue2(FrameArgs a)
 {
-    trace_queue_body<2>(a, ol, cnt, parity);
+    trace_queue_body<2>(a);
 }
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_trace_queue4(FrameArgs a, uint32_t* ol, uint32_t* cnt, uint32_t parity)
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_trace_queue4(FrameArgs a)
 {
-    trace_queue_body<4>(a, ol, cnt, parity);
+    trace_queue_body<4>(a);
+}
+
+// Tile order for the next render: tiles sorted by this render's cost, heaviest first (LPT list
+// scheduling of the persistent kernel), as a counting sort over SF_ORDER_BUCKETS log-spaced cost
+// buckets (2 per octave of cycles). The trace kernel counts every finished tile into its 64-tile
+// chunk's bucket histogram (one fire-and-forget atomic); sf_order_scan turns the histograms into
+// per-(chunk, bucket) output offsets, heaviest bucket first and chunks in order within a bucket;
+// sf_order_scatter (one wave per chunk) writes the permutation and clears the histograms. Stable and
+// deterministic. Any permutation gives the same image: only the schedule changes.
+#define SF_SCAN_BATCH 16   // chunk counts a scan thread loads at once (independent loads, one wait)
+
+extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t* __restrict__ chunk_cnt, uint32_t nc,
+                                                                   uint32_t* __restrict__ chunk_off)
+{
+    // thread = (bucket b = tid % 32, slice k = tid / 32): chunks [k * per, (k + 1) * per) of bucket b
+    __shared__ uint32_t part[32][SF_ORDER_BUCKETS + 1];
+    __shared__ uint32_t tot[SF_ORDER_BUCKETS];
+    const uint32_t tid = threadIdx.x, b = tid % SF_ORDER_BUCKETS, k = tid / SF_ORDER_BUCKETS;
+    const uint32_t per = (nc + 31u) / 32u, c0 = k * per, c1 = min(nc, c0 + per);
+    uint32_t s_ = 0u;
+    for (uint32_t cb = c0; cb < c1; cb += SF_SCAN_BATCH) {
+        uint32_t v[SF_SCAN_BATCH];
+#pragma unroll
+        for (int j = 0; j < SF_SCAN_BATCH; ++j) v[j] = cb + j < c1 ? chunk_cnt[(cb + j) * SF_ORDER_BUCKETS + b] : 0u;
+#pragma unroll
+        for (int j = 0; j < SF_SCAN_BATCH; ++j) s_ += v[j];
+    }
+    part[k][b] = s_;
+    __syncthreads();
+    if (tid < SF_ORDER_BUCKETS) {   // per bucket: slices -> exclusive prefix; bucket total
+        uint32_t acc = 0u;
+        for (uint32_t j = 0; j < 32u; ++j) {
+            const uint32_t x = part[j][tid];
+            part[j][tid] = acc;
+            acc += x;
+        }
+        tot[tid] = acc;
+    }
+    __syncthreads();
+    if (tid == 0) {   // bucket totals -> exclusive offsets, heaviest bucket first
+        uint32_t acc = 0u;
+        for (int bb = (int)SF_ORDER_BUCKETS - 1; bb >= 0; --bb) {
+            const uint32_t x = tot[bb];
+            tot[bb] = acc;
+            acc += x;
+        }
+    }
+    __syncthreads();
+    uint32_t off = tot[b] + part[k][b];
+    for (uint32_t cb = c0; cb < c1; cb += SF_SCAN_BATCH) {
+        uint32_t v[SF_SCAN_BATCH];
+#pragma unroll
+        for (int j = 0; j < SF_SCAN_BATCH; ++j) v[j] = cb + j < c1 ? chunk_cnt[(cb + j) * SF_ORDER_BUCKETS + b] : 0u;
+#pragma unroll
+        for (int j = 0; j < SF_SCAN_BATCH; ++j) {
+            if (cb + j < c1) chunk_off[(cb + j) * SF_ORDER_BUCKETS + b] = off;
+            off += v[j];
+        }
+    }
+}
+
+extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t* __restrict__ cost, uint32_t n,
+                                                                    uint32_t* __restrict__ chunk_cnt,
+                                                                    const uint32_t* __restrict__ chunk_off,
+                                                                    uint32_t* __restrict__ order)
+{
+    const uint32_t c = blockIdx.x, lane = threadIdx.x, i = c * 64u + lane;
+    const uint32_t bk = i < n ? cost_bucket(cost[i]) : SF_ORDER_BUCKETS;   // sentinel: no tile
+    const uint32_t offs = chunk_off[c * SF_ORDER_BUCKETS + (lane & (SF_ORDER_BUCKETS - 1u))];   // lane b: bucket b
+    uint64_t pending = __builtin_amdgcn_ballot_w64(bk < SF_ORDER_BUCKETS);
+    while (pending) {   // one round per distinct bucket in the chunk
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)bk, (int)__builtin_ctzll(pending));
+        const uint64_t m = __builtin_amdgcn_ballot_w64(bk == b);
+        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)offs, (int)b);
+        if (bk == b)
+            order[off + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
+        pending &= ~m;
+    }
+    if (lane < SF_ORDER_BUCKETS) chunk_cnt[c * SF_ORDER_BUCKETS + lane] = 0u;   // for the next render
 }
 
 // Re-traces flagged tiles with SF_MAX_LEVELS levels. Grid-stride over the list; reads this

@@ -245,6 +245,23 @@ void depth_tables(DepthTables* t)
     }
 }
 
+// Leaf threshold of depth d (kernel: skip building/testing the children of a node whose |c|^2 exceeds
+// it). Every child C of a depth-d node N lies at |c_C - c_N| = s = (4/3) r_d and has bounding radius
+// R = 2 r_{d+1}. A lane's float near root t for C is at least sqrt(|c_C|^2 - R^2 - dl) - sqrt(R^2 + dl),
+// dl = 2^-16 |c_C|^2 (the reachability bound of the kernel), hence at least
+// |c_N| (1 - 2^-16 - 2^-8) - 2R - s (1 + 2^-8). If |c_N| >= (T_{d+1} (1 + 2^-12) + 2R + s (1 + 2^-8)) / (1 - 2^-7),
+// that exceeds T_{d+1} and no child can pass the LOD test (Sphereflake.h:146) for any ray. The extra
+// 2^-8 on s and 2^-10 on the square cover the rounding of the unit offsets, the parent rotation and
+// the kernel's own |c|^2. Doubles here; the float result rounds up by construction of the slack.
+float leaf_threshold(const DepthTables* t, uint32_t d)
+{
+    if (d + 1u >= SF_DEPTH_TABLE) return INFINITY;
+    const double T = t->lod[d + 1u], R = std::sqrt((double)t->r2_bound[d + 1u]), s = t->scale[d];
+    const double rhs = T * (1.0 + 0x1p-12) + 2.0 * R + s * (1.0 + 0x1p-8);
+    const double th = rhs / (1.0 - 0x1p-7);
+    return (float)(th * th * (1.0 + 0x1p-10));
+}
+
 // Sobol direction numbers of dims 0 and 1 (the only dims the reference samples, Sphereflake.cpp:139-140),
 // generated algorithmically; tests pin them against the reference table (tests/golden/sobol.json).
 //   dim 0: van der Corput, M[k] = 2^(31-k) for k < 32, 0 beyond (the table stores 52 entries per dim)

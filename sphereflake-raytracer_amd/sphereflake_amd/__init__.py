@@ -89,6 +89,8 @@ SIGNATURES = {
     "sf_rsqrtps": (ctypes.c_float, [ctypes.c_float]),
     "sf_set_tile_trace": (ctypes.c_int, [_CTX, ctypes.c_int]),
     "sf_get_tile_trace": (ctypes.c_int, [_CTX, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]),
+    "sf_set_kernel_timing": (ctypes.c_int, [_CTX, ctypes.c_int]),
+    "sf_kernel_times": (ctypes.c_int, [_CTX, _F, ctypes.c_uint32]),
     "sf_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "sf_last_hip_error": (ctypes.c_int, [_CTX]),
     "sf_abi_version": (ctypes.c_int, []),
@@ -353,6 +355,18 @@ class Sphereflake:
                "sf_get_tile_trace", self._ctx)
         self.phase_sums = out[3 * n:]          # segment cycle sums of stamp builds (zeros otherwise)
         return out[:3 * n].reshape(n, 3)
+
+    def kernel_timing(self, enable: bool | None = None, n: int = 64):
+        """Measurement: enable HIP events around each render's main trace kernel, or (enable=None)
+        return the durations (ms) of the last n timed renders, oldest first."""
+        if enable is not None:
+            _check(lib().sf_set_kernel_timing(self._ctx, int(bool(enable))), "sf_set_kernel_timing", self._ctx)
+            return None
+        out = np.zeros(n, np.float32)
+        k = lib().sf_kernel_times(self._ctx, out.ctypes.data_as(_F), n)
+        if k < 0:
+            _check(k, "sf_kernel_times", self._ctx)
+        return out[:k]
 
     # stats (Sphereflake.h:30-58) --------------------------------------------
     def stats(self) -> sf_stats:

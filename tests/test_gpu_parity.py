@@ -223,3 +223,39 @@ def test_progressive_reseed_skip_ahead():
     w = epos[..., 3] == 1.0
     assert np.array_equal(pos[w].view(np.uint32), epos[w].view(np.uint32))
     assert np.array_equal(nrm[w].view(np.uint32), enrm[w].view(np.uint32))
+
+
+def test_repeat_renders_heavy_first_order_bit_exact():
+    """From the second render on, the persistent kernel takes its tiles heaviest-first (costs of the
+    previous render, sf_tile_order). The image must not depend on the order: renders 2 and 3 of c3
+    equal the golden digests, and kernel timing reports one duration per render."""
+    fx = load_frame("c3")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        s.kernel_timing(True)
+        for k in range(3):
+            s.Render(emit_aux=True)
+            pos, nrm, mint, idx = s.download(aux=True)
+            assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == [], f"render {k}"
+            assert bad_rows(fx["row_digest_aux"], aux_digests(mint, idx)) == [], f"render {k}"
+        ms = s.kernel_timing()
+        st = s.stats()
+    assert len(ms) == 3 and np.all(ms > 0)
+    assert st.max_depth == fx["stats"]["max_depth"] and st.overflow_tiles == 0
+
+
+def test_camera_inside_bounding_ball_uses_fixup_levels():
+    """K = 0.2 puts the camera inside the flake's bounding ball: no geometric level bound, so the
+    adaptive levels and the overflow re-trace path carry the frame (c5's camera on a small frame)."""
+    W, H, K = 256, 256, 0.2
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        s.Render(emit_aux=True)
+        a = s.download(aux=True)
+        s.Render(emit_aux=True)
+        b = s.download(aux=True)
+        st = s.stats()
+    for x, y in zip(a, b):
+        assert np.array_equal(np.ascontiguousarray(x).view(np.uint8), np.ascontiguousarray(y).view(np.uint8))
+    assert st.overflow_tiles == 0
