@@ -38,7 +38,7 @@ from sphereflake_amd import shard  # noqa: E402
 W, H, K = 1920, 1080, 0.25          # BASELINE configs[2]
 BYTES_PER_RAY = 32                  # two float4 G-buffer stores
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz (non-FMA fp32)
+TRACE_KERNEL = "sf_trace_queue2"    # the dominant kernel (persistent wave-coherent trace, 2 waves/workgroup)
 
 
 def parse():
@@ -65,16 +65,33 @@ def frame_camera(width, height, k, frame):
     return cam
 
 
+CPU_REPS = 40                        # ~1.2 s wall x 16 threads: ~20 s of CPU work
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (scripts/prof_pmc.sh ->
+    scripts/pmc_summary.py --json, separate rocprofv3 --pmc passes of this same bench command):
+    WRITE_SIZE + 2 x FETCH_SIZE (gfx950 FETCH_SIZE counts half of a streaming read), KB -> bytes."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            j = json.load(f)
+        c = j["kernels"][kernel]
+        return (c["WRITE_SIZE"] + 2.0 * c["FETCH_SIZE"]) * 1024.0, j.get("source", path)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def cpu_baseline(width, height, k, threads):
     """The reference AVX packet path (oracle/_ref/ref_bench, built from /root/reference) on host cores.
     Falls back to the oracle C restatement (per ray, 1 thread) if the reference build is absent."""
     from oracle import pyoracle
     ref = os.path.join(pyoracle.REF_DIR, "ref_bench")
     if os.path.exists(ref):
-        r = pyoracle.ref_bench(width, height, k, threads, 5)
+        r = pyoracle.ref_bench(width, height, k, threads, CPU_REPS)
         return {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
-                "sample": f"5 full {width}x{height} K={k} frames (reference 8-ray packet footprint, 8/9 pixel "
-                          f"coverage), median; reference AVX path -O3 -mavx, {threads} threads",
+                "sample": f"{CPU_REPS} full {width}x{height} K={k} frames (reference 8-ray packet footprint, 8/9 "
+                          f"pixel coverage), median; reference AVX path -O3 -mavx, {threads} threads",
                 "frame_ms": round(r["median_s"] * 1e3, 2)}
     setup = {"W": width, "H": height}
     cam = sf.config_camera(width, height, k)
@@ -133,6 +150,7 @@ def main():
     if args.mode == "frames":
         o, tl, tr, bl = views[0]
         ctx.SetView(o, tl, tr, bl)
+    ctx.kernel_timing(True)   # HIP events around the dominant (trace) kernel of every render
 
     ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -171,13 +189,15 @@ def main():
     st = ctx.stats()
     if st.overflow_tiles:
         raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
-    kern_ms = float(np.mean([ev_s[i].elapsed_time(ev_e[i]) for i in range(args.steps)]))
+    kern_ms = float(np.mean([ev_s[i].elapsed_time(ev_e[i]) for i in range(args.steps)]))   # whole render
+    tk = ctx.kernel_timing(n=min(args.steps, 64))        # the trace kernel alone, last timed renders
+    trace_ms = float(np.mean(tk)) if len(tk) else kern_ms
 
     t_step = dt / args.steps
     if dist_on:
-        tt = torch.tensor([t_step, kern_ms], dtype=torch.float64, device=dev)
+        tt = torch.tensor([t_step, kern_ms, trace_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_step, kern_ms_max = float(tt[0]), float(tt[1])
+        t_step, kern_ms_max, trace_ms = float(tt[0]), float(tt[1]), float(tt[2])
     else:
         kern_ms_max = kern_ms
     total_rays = rays_per_step_rank * n if args.mode == "frames" else width * height
@@ -204,7 +224,8 @@ def main():
 
     if rank == 0:
         per_launch_bytes = BYTES_PER_RAY * rays_per_step_rank
-        achieved = per_launch_bytes / (kern_ms_max * 1e-3) / 1e9
+        achieved = per_launch_bytes / (trace_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(TRACE_KERNEL)
         out = {
             "metric": "Mrays/sec into G-buffer at 1920x1080 depth-8; frame time ms",
             "value": round(value, 2),
@@ -226,9 +247,12 @@ def main():
             "kernel_ms": round(kern_ms_max, 4),
             "d2h_ms": round(d2h_ms, 3) if d2h_ms is not None else None,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "note": "path is VALU-bound (SURVEY.md §8(d)); achieved = 32 B/ray x rays per launch / "
-                                 "mean render time (trace + fixup kernels, HIP events on the launch stream)"},
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": round(traffic) if traffic else None,
+                         "kernel": TRACE_KERNEL, "kernel_ms": round(trace_ms, 4),
+                         "note": "path is VALU-bound (SURVEY.md §8(d)); achieved = 32 B/ray x rays per launch / mean "
+                                 "duration of the trace kernel (HIP events around it on its launch stream); traffic = "
+                                 "PMC WRITE_SIZE + 2 x FETCH_SIZE per launch from " + str(traffic_src)},
         }
         if check is not None:
             out["check_rows_bit_exact"] = check

@@ -1,14 +1,20 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc counter CSVs per kernel (mean per dispatch). Usage: pmc_summary.py <dir>..."""
+"""Summarise rocprofv3 --pmc counter CSVs per kernel (mean per dispatch).
+Usage: pmc_summary.py [--json OUT] <dir>...   (--json also writes the means, for bench.py's roofline traffic)"""
 import csv
 import glob
+import json
 import os
 import sys
 from collections import defaultdict
 
+args = sys.argv[1:]
+out_json = None
+if args and args[0] == "--json":
+    out_json, args = args[1], args[2:]
 acc = defaultdict(lambda: defaultdict(list))
 dur = defaultdict(list)
-for d in sys.argv[1:]:
+for d in args:
     for f in glob.glob(os.path.join(d, "**", "run_counter_collection.csv"), recursive=True):
         seen = set()
         for r in csv.DictReader(open(f)):
@@ -18,10 +24,16 @@ for d in sys.argv[1:]:
             if key not in seen:
                 seen.add(key)
                 dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+means = {}
 for k, cs in acc.items():
     if "fill" in k or "copy" in k:
         continue
-    print(f"== {k}  (profiled dispatch mean {sum(dur[k]) / len(dur[k]):.1f} us)")
+    means[k] = {c: sum(v) / len(v) for c, v in cs.items()}
+    means[k]["profiled_dispatch_us"] = sum(dur[k]) / len(dur[k])
+    print(f"== {k}  (profiled dispatch mean {means[k]['profiled_dispatch_us']:.1f} us)")
     for c in sorted(cs):
-        v = cs[c]
-        print(f"   {c:28s} {sum(v) / len(v):16.1f}")
+        print(f"   {c:28s} {means[k][c]:16.1f}")
+if out_json:
+    with open(out_json, "w") as f:
+        json.dump({"source": "rocprofv3 --pmc passes of scripts/prof_pmc.sh (" + ", ".join(args) + "); "
+                             "FETCH_SIZE/WRITE_SIZE in KB per dispatch", "kernels": means}, f, indent=1)
