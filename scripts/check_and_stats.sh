@@ -1,3 +1,3 @@
 set -e
 bash scripts/run_check.sh
-bash scripts/stats_run.sh st10
+bash scripts/stats_run.sh st11

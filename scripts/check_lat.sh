@@ -1,4 +1,4 @@
 set -e
 bash scripts/run_check.sh
 bash scripts/stats_run.sh ${1:-st}
-bash scripts/diag_tiles.sh ${2:-d}
+bash scripts/occ_latency.sh

@@ -84,6 +84,7 @@ struct sf_ctx {
     uint32_t flags = 0;                          // SF_FLAG_* A/B switches: env SF_FLAGS
     int cus = 256;
     int occ_key = -1, occ_blocks = 0;            // cached occupancy (waves per block, levels) -> blocks per CU
+    uint32_t max_blocks = 0;                     // diagnostics: env SF_MAX_BLOCKS caps the persistent grid
     // frame-less progressive mode
     uint32_t* mt_state = nullptr;      // 624 words + next index (std::mt19937 layout)
     uint32_t* draws = nullptr;         // 2 per packet
@@ -232,6 +233,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     c->cus = prop.multiProcessorCount;
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_ORDER")) c->use_order = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_FLAGS")) c->flags = (uint32_t)std::strtoul(ev, nullptr, 0);
     if (const char* ev = std::getenv("SF_TRACE_WAVES")) {
         const int w = std::atoi(ev);
@@ -449,6 +451,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             uint32_t nblk = (uint32_t)c->occ_blocks * (uint32_t)c->cus;
             const uint32_t need = (ntiles + wpb - 1) / wpb;
             if (nblk > need) nblk = need;
+            if (c->max_blocks && nblk > c->max_blocks) nblk = c->max_blocks;
             const dim3 grid(nblk);
             if (c->use_order) {
                 a.tile_cost = c->tile_cost;
