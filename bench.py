@@ -105,6 +105,58 @@ def cpu_baseline(width, height, k, threads):
             "sample": f"every 8th row of a {width}x{height} K={k} frame, oracle C restatement, 1 thread"}
 
 
+def transfer_rates(ctx, torch, dev, stream, width, height, kernel, frames=8):
+    """G-buffer D2H cost (positions + normals, 32 B/pixel). Pageable synchronous
+    download (sf_download, what the reference-style GetGBuffer pays unpinned), stream-ordered copy into
+    page-locked host memory (sf_download_async), and a double-buffered pipeline -- render frame i+1 into
+    one device slab while slab i drains over PCIe on a copy stream -- giving the PCIe-inclusive frame
+    rate an interactive viewer would see."""
+    nbytes = width * height * 32
+    ctx.Synchronize()
+    t = time.perf_counter()
+    ctx.download()
+    pageable_ms = (time.perf_counter() - t) * 1e3
+    g = ctx.pinned_gbuffer()
+    ctx.download_async(g)
+    ctx.Synchronize()
+    t = time.perf_counter()
+    for _ in range(frames):
+        ctx.download_async(g)
+    ctx.Synchronize()
+    pinned_ms = (time.perf_counter() - t) * 1e3 / frames
+    ctx.release_pinned()
+    # double-buffered render -> D2H pipeline
+    copy = torch.cuda.Stream(device=dev)
+    slabs = [[torch.empty((height, width, 4), dtype=torch.float32, device=dev) for _ in range(2)] for _ in range(2)]
+    host = [[torch.empty((height, width, 4), dtype=torch.float32, pin_memory=True) for _ in range(2)] for _ in range(2)]
+    done = [torch.cuda.Event() for _ in range(2)]
+    drained = [torch.cuda.Event() for _ in range(2)]
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    for i in range(frames + 1):
+        b = i & 1
+        if i < frames:
+            with torch.cuda.stream(stream):
+                if i >= 2:
+                    stream.wait_event(drained[b])
+                ctx.render_to(slabs[b][0].data_ptr(), slabs[b][1].data_ptr(), kernel=kernel, stream=stream.cuda_stream)
+                done[b].record(stream)
+        if i >= 1:
+            p = (i - 1) & 1
+            with torch.cuda.stream(copy):
+                copy.wait_event(done[p])
+                host[p][0].copy_(slabs[p][0], non_blocking=True)
+                host[p][1].copy_(slabs[p][1], non_blocking=True)
+                drained[p].record(copy)
+    torch.cuda.synchronize(dev)
+    pipe_ms = (time.perf_counter() - t) * 1e3 / frames
+    return {"bytes": nbytes, "pageable_ms": round(pageable_ms, 3), "pinned_ms": round(pinned_ms, 3),
+            "pinned_GBps": round(nbytes / (pinned_ms * 1e-3) / 1e9, 2),
+            "pipelined_frame_ms": round(pipe_ms, 3),
+            "pcie_inclusive_Mrays": round(width * height / (pipe_ms * 1e-3) / 1e6, 2),
+            "note": "PCIe-inclusive figures; `value` is the HBM-resident render rate"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -203,12 +255,10 @@ def main():
     total_rays = rays_per_step_rank * n if args.mode == "frames" else width * height
     value = total_rays / t_step / 1e6
 
-    # D2H into the host GBuffer (PCIe-inclusive frame rate, reported separately)
-    d2h_ms = None
+    # D2H into the host GBuffer (PCIe-inclusive, reported separately -- never `value`)
+    d2h = None
     if rank == 0 and args.mode == "frames":
-        t1 = time.perf_counter()
-        ctx.download()
-        d2h_ms = (time.perf_counter() - t1) * 1e3
+        d2h = transfer_rates(ctx, torch, dev, stream, width, height, kernel)
 
     check = None
     if args.check and rank == 0 and args.mode == "frames":
@@ -245,7 +295,7 @@ def main():
                        "parallelism": f"frames x{n}" if args.mode == "frames" else f"row-bands x{n} + RCCL gather"},
             "frame_ms": round(t_step * 1e3, 4),
             "kernel_ms": round(kern_ms_max, 4),
-            "d2h_ms": round(d2h_ms, 3) if d2h_ms is not None else None,
+            "d2h": d2h,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": round(traffic) if traffic else None,

@@ -129,6 +129,53 @@ uint32_t sf_slab_rows(uint32_t height, uint32_t band_rows, uint32_t band_count, 
    float4 arrays of W*H elements. Any pointer may be NULL to skip that channel. */
 int sf_download(sf_ctx* ctx, float* pos4, float* nrm4, float* min_t, uint32_t* hit_index);
 
+/* Stream-ordered D2H of the context G-buffer (and aux channels) on `stream` (NULL = the context
+   stream); returns at once. With page-locked destinations (sf_host_register) it runs at PCIe DMA
+   rate and overlaps host work; completion: sf_synchronize (context stream) or the caller's stream. */
+int sf_download_async(sf_ctx* ctx, float* pos4, float* nrm4, float* min_t, uint32_t* hit_index, void* stream);
+
+/* Page-lock existing host memory (e.g. the std::vector storage of the C++ class's GBuffer, which the
+   reference's PBO upload reads, GLPixelBufferObject.h:24-29) so device copies into it use DMA. */
+int sf_host_register(void* ptr, size_t bytes);
+int sf_host_unregister(void* ptr);
+
+/* --- SSAO post-process ---------------------------------- */
+/* The reference's GL passes over the G-buffer (SSAO.cpp:106-142: SSAO, blur x, blur y;
+   main.cpp:312-330: final composite), run headless as HIP kernels. Output: RGBA8 image, W*H*4
+   bytes, row j = G-buffer row j (GL framebuffer row j counted from the bottom). */
+#define SF_POST_GENERAL      1u   /* always run the multi-pass path (A/B; results identical) */
+#define SF_POST_UNIT_NORMALS 2u   /* caller's external normals have length <= 1.004 (enables fusion) */
+
+typedef struct sf_post_params {
+    float sample_radius;      /* SSAOSampleRadius; < 0: 8 x GetClosestSphereDistance() of this
+                                 context, read on the device (main.cpp:316, SSAO.h:15-18) */
+    float intensity;          /* SSAO.cpp:51   0.51 */
+    float scale;              /* SSAO.cpp:52   3.28 */
+    float bias;               /* SSAO.cpp:53   0.23 */
+    float normal_threshold;   /* SSAO.cpp:54   2.47 */
+    float depth_threshold;    /* SSAO.cpp:55   0.01 */
+    float camera_position[3]; /* post_final.glsl cameraPosition (main.cpp:325: the view origin) */
+    uint32_t downscale;       /* SSAO target = (W / d, H / d) (SSAO ctor, main.cpp:118 uses 1) */
+    uint32_t flags;           /* SF_POST_* */
+    void* stream;             /* NULL = the context stream */
+} sf_post_params;
+
+/* Reference defaults; camera_position = the context's SetView origin. */
+int sf_post_defaults(const sf_ctx* ctx, sf_post_params* params);
+
+/* Post-process a G-buffer on the device. pos4 / nrm4: device float4 G-buffer of W*H pixels (NULL =
+   the context's). rgba: device output W*H*4 bytes (NULL = the context's image buffer, see
+   sf_download_image). ao: optional device output of the SSAO target before blurring
+   ((W/d)*(H/d) bytes, the r channel). Asynchronous on the stream. */
+int sf_post_process(sf_ctx* ctx, const sf_post_params* params, const float* pos4, const float* nrm4,
+                    uint8_t* rgba, uint8_t* ao);
+
+/* Synchronous D2H of the context image buffer (W*H*4 bytes) written by sf_post_process. */
+int sf_download_image(sf_ctx* ctx, uint8_t* rgba);
+
+/* The SSAO noise texture (SSAO.cpp:144-164): 64*64 RGBA32F texels into out[16384]. Host only. */
+int sf_ssao_noise(float* out);
+
 /* Device pointers of the context buffers (any out-pointer may be NULL). */
 int sf_device_buffers(sf_ctx* ctx, float** pos4, float** nrm4, float** min_t, uint32_t** hit_index);
 

@@ -18,6 +18,11 @@ Sphereflake::Sphereflake(size_t width, size_t height, int device) : m_Width(widt
     // reference: m_GBuffer.positions/normals.resize(W*H) of zero vec4 (Sphereflake.cpp:48-49)
     m_GBuffer.positions.resize(width * height);
     m_GBuffer.normals.resize(width * height);
+    // page-lock the vectors' storage (they stay std::vector for the PBO upload, GLPixelBufferObject.h:24-29)
+    // so GetGBuffer's D2H runs as DMA straight into them; not fatal when the host refuses to pin
+    const size_t bytes = width * height * sizeof(sf_vec4);
+    m_Pinned = bytes && sf_host_register(m_GBuffer.positions.data(), bytes) == SF_OK &&
+               sf_host_register(m_GBuffer.normals.data(), bytes) == SF_OK;
 }
 
 Sphereflake::~Sphereflake()
@@ -25,6 +30,10 @@ Sphereflake::~Sphereflake()
     m_Deinitialize = true;
     if (m_Worker.joinable()) m_Worker.join();
     sf_destroy(m_Ctx);
+    if (m_Pinned) {
+        sf_host_unregister(m_GBuffer.positions.data());
+        sf_host_unregister(m_GBuffer.normals.data());
+    }
 }
 
 void Sphereflake::SetView(const sf_vec3& origin, const sf_vec3& topLeft, const sf_vec3& topRight, const sf_vec3& bottomLeft)

@@ -13,7 +13,8 @@
 //   - Rendering is an explicit full frame: Render() traces every pixel once, deterministically.
 //     Initialize() keeps the reference's frame-less progressive mode (Sphereflake.cpp:67-74) on the
 //     device: a host thread keeps launching batches of random 8-ray packets until destruction.
-//   - GetGBuffer() downloads the device G-buffer (hipMemcpy D2H) when it is stale.
+//   - GetGBuffer() downloads the device G-buffer (D2H) when it is stale, by DMA into the vectors'
+//     storage, page-locked at construction (sf_host_register).
 //   - Errors throw std::runtime_error carrying sf_strerror() (the reference had no error path).
 #pragma once
 
@@ -84,6 +85,7 @@ private:
     sf_ctx* m_Ctx = nullptr;
     mutable GBuffer m_GBuffer;
     mutable bool m_Stale = true;
+    bool m_Pinned = false;
     mutable std::mutex m_Mutex;
     std::thread m_Worker;
     std::atomic<bool> m_Deinitialize{ false };

@@ -28,6 +28,10 @@ extern "C" __global__ void sf_order_scatter(const uint32_t* cost, uint32_t n, ui
 extern "C" __global__ void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list, uint32_t* counters,
                                          uint32_t parity);
 extern "C" __global__ void sf_trace_ray(FrameArgs a);
+extern "C" __global__ void sf_post_ssao(PostArgs a);
+extern "C" __global__ void sf_post_blur(PostArgs a, uint32_t dir);
+extern "C" __global__ void sf_post_final(PostArgs a);
+extern "C" __global__ void sf_post_fused(PostArgs a);
 extern "C" __global__ void sf_mt_draws(uint32_t* state, uint32_t* out, uint32_t n);
 extern "C" __global__ void sf_progressive_trace(FrameArgs a, const uint32_t* draws, uint64_t counter0, uint32_t packets,
                                                 uint64_t ticket0, PacketLane* lanes, unsigned long long* owner);
@@ -115,6 +119,14 @@ struct sf_ctx {
     hipEvent_t ev[kTimed][2] = {};
     bool timing = false;
     uint32_t ev_next = 0, ev_count = 0;
+    // SSAO post-process (sf_post_process): lazily allocated
+    float* noise = nullptr;            // 64x64 float4
+    uint8_t* ao = nullptr;             // SSAO target, sized for post_ao_px pixels
+    size_t post_ao_px = 0;
+    uint8_t* blur_h = nullptr;         // W x H
+    uint8_t* blur_v = nullptr;
+    uint8_t* image = nullptr;          // W x H RGBA8
+    int centre_exact = -1;             // sfhost::post_centre_exact(W) && (H), cached
 };
 
 #define SF_HIP(ctx, expr)                                        \
@@ -149,6 +161,11 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->tile_order);
     (void)hipFree(c->chunk_cnt);
     (void)hipFree(c->chunk_off);
+    (void)hipFree(c->noise);
+    (void)hipFree(c->ao);
+    (void)hipFree(c->blur_h);
+    (void)hipFree(c->blur_v);
+    (void)hipFree(c->image);
     for (int i = 0; i < sf_ctx::kTimed; ++i)
         for (int j = 0; j < 2; ++j)
             if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
@@ -602,6 +619,139 @@ int sf_download(sf_ctx* c, float* pos4, float* nrm4, float* min_t, uint32_t* hid
     if (nrm4) SF_HIP(c, hipMemcpy(nrm4, c->nrm, npx * 16, hipMemcpyDeviceToHost));
     if (min_t) SF_HIP(c, hipMemcpy(min_t, c->min_t, npx * 4, hipMemcpyDeviceToHost));
     if (hidx) SF_HIP(c, hipMemcpy(hidx, c->hit_index, npx * 4, hipMemcpyDeviceToHost));
+    return SF_OK;
+}
+
+// Transfer/interop: stream-ordered D2H into host memory. With page-locked
+// destinations (sf_host_register) the copy runs at PCIe DMA rate and overlaps
+// whatever the host does until sf_synchronize (context stream) or the caller syncs `stream`.
+int sf_download_async(sf_ctx* c, float* pos4, float* nrm4, float* min_t, uint32_t* hidx, void* stream)
+{
+    if (!c) return SF_EINVAL;
+    DevGuard g(c->device);
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const size_t npx = (size_t)c->W * c->H;
+    if (pos4) SF_HIP(c, hipMemcpyAsync(pos4, c->pos, npx * 16, hipMemcpyDeviceToHost, s));
+    if (nrm4) SF_HIP(c, hipMemcpyAsync(nrm4, c->nrm, npx * 16, hipMemcpyDeviceToHost, s));
+    if (min_t) SF_HIP(c, hipMemcpyAsync(min_t, c->min_t, npx * 4, hipMemcpyDeviceToHost, s));
+    if (hidx) SF_HIP(c, hipMemcpyAsync(hidx, c->hit_index, npx * 4, hipMemcpyDeviceToHost, s));
+    return SF_OK;
+}
+
+int sf_host_register(void* ptr, size_t bytes)
+{
+    if (!ptr || !bytes) return SF_EINVAL;
+    return hipHostRegister(ptr, bytes, hipHostRegisterDefault) == hipSuccess ? SF_OK : SF_EHIP;
+}
+
+int sf_host_unregister(void* ptr)
+{
+    if (!ptr) return SF_EINVAL;
+    return hipHostUnregister(ptr) == hipSuccess ? SF_OK : SF_EHIP;
+}
+
+int sf_post_defaults(const sf_ctx* c, sf_post_params* p)
+{
+    if (!c || !p) return SF_EINVAL;
+    std::memset(p, 0, sizeof *p);
+    p->sample_radius = -1.0f;
+    p->intensity = 0.51f;
+    p->scale = 3.28f;
+    p->bias = 0.23f;
+    p->normal_threshold = 2.47f;
+    p->depth_threshold = 0.01f;
+    std::memcpy(p->camera_position, c->o, 12);
+    p->downscale = 1;
+    return SF_OK;
+}
+
+int sf_ssao_noise(float* out)
+{
+    if (!out) return SF_EINVAL;
+    sfhost::ssao_noise(out);
+    return SF_OK;
+}
+
+int sf_post_process(sf_ctx* c, const sf_post_params* prm, const float* pos4, const float* nrm4, uint8_t* rgba,
+                    uint8_t* ao)
+{
+    if (!c || !prm || prm->downscale == 0) return SF_EINVAL;
+    const uint32_t aw = c->W / prm->downscale, ah = c->H / prm->downscale;
+    if (aw == 0 || ah == 0) return SF_EINVAL;
+    DevGuard g(c->device);
+    hipStream_t s = prm->stream ? (hipStream_t)prm->stream : c->stream;
+    const size_t npx = (size_t)c->W * c->H;
+    if (!c->noise) {
+        static float host_noise[SF_NOISE_SIZE * SF_NOISE_SIZE * 4];
+        sfhost::ssao_noise(host_noise);
+        SF_HIP(c, hipMalloc(&c->noise, sizeof host_noise));
+        SF_HIP(c, hipMemcpy(c->noise, host_noise, sizeof host_noise, hipMemcpyHostToDevice));
+    }
+    if (!c->image) SF_HIP(c, hipMalloc(&c->image, npx * 4));
+    if (c->centre_exact < 0) c->centre_exact = sfhost::post_centre_exact(c->W) && sfhost::post_centre_exact(c->H);
+    // Fusion is exact when no blur tap can be accepted: every |n| <= 1.004 (the tracer's normals are
+    // rsqrtps-normalised, |n| - 1 < 2^-11) bounds dot(n, n') < 1.01 <= normalThreshold
+    const bool own_gbuffer = (!pos4 || pos4 == c->pos) && (!nrm4 || nrm4 == c->nrm);
+    const bool fused = !(prm->flags & SF_POST_GENERAL) && prm->downscale == 1 && c->centre_exact &&
+                       prm->normal_threshold >= 1.01f && (own_gbuffer || (prm->flags & SF_POST_UNIT_NORMALS));
+    if (!fused) {
+        if (c->post_ao_px < (size_t)aw * ah) {
+            SF_HIP(c, hipFree(c->ao));
+            c->ao = nullptr;
+            SF_HIP(c, hipMalloc(&c->ao, (size_t)aw * ah));
+            c->post_ao_px = (size_t)aw * ah;
+        }
+        if (!c->blur_h) SF_HIP(c, hipMalloc(&c->blur_h, npx));
+        if (!c->blur_v) SF_HIP(c, hipMalloc(&c->blur_v, npx));
+    }
+    PostArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.W = c->W;
+    a.H = c->H;
+    a.aw = aw;
+    a.ah = ah;
+    a.fw = (float)c->W;
+    a.fh = (float)c->H;
+    a.faw = (float)aw;
+    a.fah = (float)ah;
+    a.pos = pos4 ? pos4 : c->pos;
+    a.nrm = nrm4 ? nrm4 : c->nrm;
+    a.noise = c->noise;
+    a.stats = c->stats;
+    a.radius = prm->sample_radius;
+    a.intensity = prm->intensity;
+    a.scale = prm->scale;
+    a.bias = prm->bias;
+    a.normal_thr = prm->normal_threshold;
+    a.depth_thr = prm->depth_threshold;
+    std::memcpy(a.cam, prm->camera_position, 12);
+    a.rgba = rgba ? rgba : c->image;
+    const dim3 blk(256);
+    const dim3 grid((c->W + 15) / 16, (c->H + 15) / 16);
+    if (fused) {
+        a.ao = ao;
+        hipLaunchKernelGGL(sf_post_fused, grid, blk, 0, s, a);
+    } else {
+        a.ao = ao ? ao : c->ao;
+        a.blur_h = c->blur_h;
+        a.blur_v = c->blur_v;
+        hipLaunchKernelGGL(sf_post_ssao, dim3((aw + 15) / 16, (ah + 15) / 16), blk, 0, s, a);
+        hipLaunchKernelGGL(sf_post_blur, grid, blk, 0, s, a, 0u);
+        hipLaunchKernelGGL(sf_post_blur, grid, blk, 0, s, a, 1u);
+        hipLaunchKernelGGL(sf_post_final, grid, blk, 0, s, a);
+    }
+    SF_HIP(c, hipGetLastError());
+    return SF_OK;
+}
+
+int sf_download_image(sf_ctx* c, uint8_t* rgba)
+{
+    if (!c || !rgba) return SF_EINVAL;
+    if (!c->image) return SF_ESTATE;
+    int rc = sf_synchronize(c);
+    if (rc != SF_OK) return rc;
+    DevGuard g(c->device);
+    SF_HIP(c, hipMemcpy(rgba, c->image, (size_t)c->W * c->H * 4, hipMemcpyDeviceToHost));
     return SF_OK;
 }
 

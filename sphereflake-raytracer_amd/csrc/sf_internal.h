@@ -91,6 +91,27 @@ struct FrameArgs {
     uint32_t* chunk_cnt;              // out (with tile_cost): per 64-tile chunk, cost-bucket histogram
 };
 
+// Headless SSAO post-process (Shaders/post_ssao.glsl, post_ssao_blur.glsl,
+// post_final.glsl, SSAO.cpp:106-142). Textures are modelled, not emulated: NEAREST/LINEAR filtering
+// with the texel coordinate snapped to 8 fractional bits (sf_post.hip).
+#define SF_NOISE_SIZE 64               // SSAO.h NOISE_TEXTURE_SIZE
+struct PostArgs {
+    uint32_t W, H;                    // G-buffer (= blur / final target) size
+    uint32_t aw, ah;                  // SSAO target size (W / downscale, H / downscale)
+    float fw, fh, faw, fah;
+    const float* pos;                 // float4 per pixel
+    const float* nrm;
+    const float* noise;               // SF_NOISE_SIZE^2 float4 (.xy read)
+    const int32_t* stats;             // [1] closest-hit key, for radius < 0
+    float radius;                     // SSAOSampleRadius, or < 0: 8 x closest (SSAO.h:15-18)
+    float intensity, scale, bias, normal_thr, depth_thr;
+    float cam[3];
+    uint8_t* ao;                      // SSAO target (aw x ah); RGBA8 FBO with r = g = b: one channel kept
+    uint8_t* blur_h;                  // horizontal blur target (W x H)
+    uint8_t* blur_v;                  // vertical blur target (W x H)
+    uint8_t* rgba;                    // final image, W x H x RGBA8, row j = G-buffer row j
+};
+
 #define SF_ORDER_BUCKETS 32u           // log-spaced cost buckets of sf_tile_order (2 per octave from 2^8 cycles)
 
 namespace sfhost {
@@ -104,6 +125,8 @@ void depth_tables(DepthTables* t);
 float leaf_threshold(const DepthTables* t, uint32_t depth);
 void sobol_matrices(uint32_t out[2][52]);
 void mt19937_seed(uint32_t seed, uint32_t state[625]);
+void ssao_noise(float out[SF_NOISE_SIZE * SF_NOISE_SIZE * 4]);
+bool post_centre_exact(uint32_t n);
 }  // namespace sfhost
 
 // Order-preserving map float <-> int32 for atomicMin on floats (negative values included).

@@ -1,0 +1,247 @@
+// sf_post.hip -- headless SSAO post-process of the G-buffer on gfx950.
+//
+// The reference runs three GL fullscreen passes plus a final pass on its G-buffer textures
+// (SSAO.cpp:106-142, main.cpp:312-330):
+//   SSAO           Shaders/post_ssao.glsl       16 position taps, noise-rotated kernel -> RGBA8 target
+//   blur x, blur y Shaders/post_ssao_blur.glsl  depth/normal-aware 5-tap Gaussian -> RGBA8 targets
+//   final          Shaders/post_final.glsl      colour = 0.5 + 0.5 (position + camera) times AO
+// Here each pass is a kernel over the same data in HBM, with the GL state it depends on restated:
+//   - G-buffer textures: RGBA32F, NEAREST, CLAMP_TO_EDGE (main.cpp:181-203)
+//   - FBO targets: RGBA8 unorm, LINEAR, CLAMP_TO_EDGE (GLFramebufferObject.cpp:41-45): every pass
+//     output is quantised to 8 bits; r = g = b, so one byte per pixel is kept
+//   - noise: RGBA32F 64x64, LINEAR, REPEAT (SSAO.cpp:166-174)
+// Texture filtering is a model, not a driver emulation: the texel-space coordinate is snapped to
+// 8 fractional bits (round to nearest even), NEAREST takes floor, LINEAR the GL bilinear blend
+// with those 1/256 weights. oracle/post.py restates the same formulas; the GPU result equals it bit
+// for bit (tests/test_gpu_post.py).
+//
+// With the reference's thresholds (normalThreshold 2.47 > any dot of two unit normals) no blur tap is
+// ever accepted, so both blurs collapse to a per-pixel weight: sf_post_fused does SSAO + blurs + final
+// in one pass (36 B/pixel of HBM). The host proves the conditions (sf_capi.hip); otherwise the
+// multi-pass kernels run.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "sf_internal.h"
+
+namespace {
+
+__device__ __constant__ float kOffset[3] = { 0.0f, 1.3846153846f, 3.2307692308f };   // post_ssao_blur.glsl:9
+__device__ __constant__ float kWeight[3] = { 0.2270270270f, 0.3162162162f, 0.0702702703f };   // :10
+
+__device__ inline float4 ld4(const float* p, uint32_t i) { return reinterpret_cast<const float4*>(p)[i]; }
+
+// texel-space coordinate snapped to 8 fractional bits; the clamp keeps NaN/inf offsets in int range
+__device__ inline float snap(float x, float lim) { return rintf(fminf(fmaxf(x, -2.0f), lim + 2.0f) * 256.0f); }
+
+__device__ inline int nearest(float u, float size, int n)   // NEAREST, CLAMP_TO_EDGE
+{
+    const int t = (int)floorf(snap(u * size, size) * (1.0f / 256.0f));
+    return min(max(t, 0), n - 1);
+}
+
+struct Lin {
+    int i0, i1;
+    float a;
+};
+
+__device__ inline Lin linear_clamp(float u, float size, int n)   // LINEAR, CLAMP_TO_EDGE
+{
+    const float c = snap(u * size - 0.5f, size);
+    const float f = floorf(c * (1.0f / 256.0f));
+    const int i = (int)f;
+    return { min(max(i, 0), n - 1), min(max(i + 1, 0), n - 1), (c - f * 256.0f) * (1.0f / 256.0f) };
+}
+
+__device__ inline float blend(float t00, float t10, float t01, float t11, float a, float b)
+{
+    const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+    return ((w00 * t00 + w10 * t10) + w01 * t01) + w11 * t11;
+}
+
+__device__ inline float unorm(uint8_t k) { return (float)k / 255.0f; }
+
+__device__ inline uint8_t quant(float x)   // float -> RGBA8 unorm channel (NaN -> 0)
+{
+    return (uint8_t)floorf(fminf(fmaxf(x, 0.0f), 1.0f) * 255.0f + 0.5f);
+}
+
+// texture(source, u, v) of an 8-bit single-channel target
+__device__ inline float sample_u8(const uint8_t* t, uint32_t w, uint32_t h, float fw, float fh, float u, float v)
+{
+    const Lin x = linear_clamp(u, fw, (int)w), y = linear_clamp(v, fh, (int)h);
+    return blend(unorm(t[y.i0 * w + x.i0]), unorm(t[y.i0 * w + x.i1]), unorm(t[y.i1 * w + x.i0]),
+                 unorm(t[y.i1 * w + x.i1]), x.a, y.a);
+}
+
+// texture(noiseTexture, uv * 0.1).xy: LINEAR, REPEAT over 64x64
+__device__ inline float2 sample_noise(const float* noise, float u, float v)
+{
+    const float cs = rintf((u * (float)SF_NOISE_SIZE - 0.5f) * 256.0f);
+    const float ct = rintf((v * (float)SF_NOISE_SIZE - 0.5f) * 256.0f);
+    const float fs = floorf(cs * (1.0f / 256.0f)), ft = floorf(ct * (1.0f / 256.0f));
+    const float a = (cs - fs * 256.0f) * (1.0f / 256.0f), b = (ct - ft * 256.0f) * (1.0f / 256.0f);
+    const int m = SF_NOISE_SIZE - 1;
+    const int x0 = (int)fs & m, x1 = ((int)fs + 1) & m, y0 = (int)ft & m, y1 = ((int)ft + 1) & m;
+    const float4 t00 = ld4(noise, y0 * SF_NOISE_SIZE + x0), t10 = ld4(noise, y0 * SF_NOISE_SIZE + x1);
+    const float4 t01 = ld4(noise, y1 * SF_NOISE_SIZE + x0), t11 = ld4(noise, y1 * SF_NOISE_SIZE + x1);
+    return make_float2(blend(t00.x, t10.x, t01.x, t11.x, a, b), blend(t00.y, t10.y, t01.y, t11.y, a, b));
+}
+
+__device__ inline bool is_background(float4 p) { return p.x * p.x + p.y * p.y + p.z * p.z == 0.0f; }   // length == 0
+
+// post_ssao.glsl:19-25 occlude()
+__device__ inline float occlude(const PostArgs& a, float fx, float fy, float ox, float oy, float4 p, float4 n)
+{
+    const int tx = nearest((fx + ox) / a.faw, a.fw, (int)a.W);
+    const int ty = nearest((fy + oy) / a.fah, a.fh, (int)a.H);
+    const float4 s = ld4(a.pos, (uint32_t)ty * a.W + (uint32_t)tx);
+    const float dx = s.x - p.x, dy = s.y - p.y, dz = s.z - p.z;
+    const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
+    const float t = n.x * (dx / dist) + n.y * (dy / dist) + n.z * (dz / dist);
+    const float m = t - a.bias;
+    const float c = m > 0.0f ? m : 0.0f;   // max(0.0, NaN) -> 0
+    return c * (1.0f / (1.0f + dist * dist * a.scale)) * a.intensity;
+}
+
+// post_ssao.glsl:27-61 at SSAO-target fragment (i, j); returns the 8-bit target value
+__device__ inline uint8_t ssao_at(const PostArgs& a, uint32_t i, uint32_t j)
+{
+    const float fx = (float)i + 0.5f, fy = (float)j + 0.5f;
+    const float u = fx / a.faw, v = fy / a.fah;
+    const uint32_t px = (uint32_t)nearest(v, a.fh, (int)a.H) * a.W + (uint32_t)nearest(u, a.fw, (int)a.W);
+    const float4 p = ld4(a.pos, px);
+    if (is_background(p)) return 0;   // vec4(0, 0, 0, 1)
+    const float4 n = ld4(a.nrm, px);
+    const float R = a.radius >= 0.0f ? a.radius : 8.0f * sf_key_float(a.stats[1]);
+    const float rad = R / sqrtf(fabsf(p.z));
+    const float2 nz = sample_noise(a.noise, u * 0.1f, v * 0.1f);
+    float rx = nz.x * 2.0f - 1.0f, ry = nz.y * 2.0f - 1.0f;
+    const float len = sqrtf(rx * rx + ry * ry);
+    rx = rx / len;
+    ry = ry / len;
+    float ao = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float kx = k == 0 ? 1.0f : k == 1 ? -1.0f : 0.0f;   // kernel[4] (post_ssao.glsl:15)
+        const float ky = k == 2 ? 1.0f : k == 3 ? -1.0f : 0.0f;
+        const float f = 2.0f * (rx * kx + ry * ky);                 // reflect(I, N) = I - 2 dot(N, I) N
+        const float c1x = (kx - f * rx) * rad, c1y = (ky - f * ry) * rad;
+        const float c2x = c1x * 0.707f - c1y * 0.707f, c2y = c1x * 0.707f + c1y * 0.707f;
+        ao += occlude(a, fx, fy, c1x * 0.25f, c1y * 0.25f, p, n);
+        ao += occlude(a, fx, fy, c1x * 0.75f, c1y * 0.75f, p, n);
+        ao += occlude(a, fx, fy, c2x * 0.5f, c2y * 0.5f, p, n);
+        ao += occlude(a, fx, fy, c2x, c2y, p, n);
+    }
+    ao = ao / 16.0f;
+    return quant(1.0f - ao);
+}
+
+// weight the centre tap gets when both taps of both offsets are rejected (post_ssao_blur.glsl:44-63)
+__device__ inline float rejected_weight()
+{
+    float lo = 0.0f;
+    lo += kWeight[1];
+    lo += kWeight[1];
+    lo += kWeight[2];
+    lo += kWeight[2];
+    return kWeight[0] + lo;
+}
+
+// post_final.glsl:15-28 given the AO value sampled at the fragment
+__device__ inline void final_store(const PostArgs& a, uint32_t px, float4 p, float ssao)
+{
+    uchar4 o;
+    if (is_background(p)) {
+        o = make_uchar4(0, 0, 0, 255);
+    } else {
+        o.x = quant((0.5f + 0.5f * (p.x + a.cam[0])) * ssao);
+        o.y = quant((0.5f + 0.5f * (p.y + a.cam[1])) * ssao);
+        o.z = quant((0.5f + 0.5f * (p.z + a.cam[2])) * ssao);
+        o.w = 255;
+    }
+    reinterpret_cast<uchar4*>(a.rgba)[px] = o;
+}
+
+// 16x16-pixel workgroups: a wave covers 16x4, so the SSAO taps (a few pixels around) share lines
+__device__ inline bool pixel(uint32_t w, uint32_t h, uint32_t& i, uint32_t& j)
+{
+    i = blockIdx.x * 16u + (threadIdx.x & 15u);
+    j = blockIdx.y * 16u + (threadIdx.x >> 4);
+    return i < w && j < h;
+}
+
+}  // namespace
+
+// SSAO pass into the SSAO target (aw x ah)
+extern "C" __global__ void __launch_bounds__(256) sf_post_ssao(PostArgs a)
+{
+    uint32_t i, j;
+    if (!pixel(a.aw, a.ah, i, j)) return;
+    a.ao[j * a.aw + i] = ssao_at(a, i, j);
+}
+
+// One blur pass (post_ssao_blur.glsl) over the W x H target: dir 0 = x (source: SSAO target),
+// dir 1 = y (source: x-blur target)
+extern "C" __global__ void __launch_bounds__(256) sf_post_blur(PostArgs a, uint32_t dir)
+{
+    uint32_t i, j;
+    if (!pixel(a.W, a.H, i, j)) return;
+    const uint8_t* src = dir ? a.blur_h : a.ao;
+    uint8_t* dst = dir ? a.blur_v : a.blur_h;
+    const uint32_t sw = dir ? a.W : a.aw, sh = dir ? a.H : a.ah;
+    const float fsw = dir ? a.fw : a.faw, fsh = dir ? a.fh : a.fah;
+    const float psx = 1.0f / a.fw, psy = 1.0f / a.fh;   // pixelSize = pixelSizeGBuffer (same size)
+    const float fx = (float)i + 0.5f, fy = (float)j + 0.5f;
+    const float ux = fx * psx, uy = fy * psy;
+    const uint32_t px = (uint32_t)nearest(uy, a.fh, (int)a.H) * a.W + (uint32_t)nearest(ux, a.fw, (int)a.W);
+    const float4 p = ld4(a.pos, px), n = ld4(a.nrm, px);
+    const float dx = dir ? 0.0f : 1.0f, dy = dir ? 1.0f : 0.0f;
+    float color = 0.0f, lo = 0.0f;
+#pragma unroll
+    for (int k = 1; k < 3; ++k) {
+        const float ox = dx * kOffset[k] * psx, oy = dy * kOffset[k] * psy;
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const float sx = side ? ux - ox : ux + ox, sy = side ? uy - oy : uy + oy;
+            const uint32_t q = (uint32_t)nearest(sy, a.fh, (int)a.H) * a.W + (uint32_t)nearest(sx, a.fw, (int)a.W);
+            const float4 sp = ld4(a.pos, q), sn = ld4(a.nrm, q);
+            if (n.x * sn.x + n.y * sn.y + n.z * sn.z >= a.normal_thr && fabsf(sp.z - p.z) >= a.depth_thr)
+                color += sample_u8(src, sw, sh, fsw, fsh, sx, sy) * kWeight[k];
+            else
+                lo += kWeight[k];
+        }
+    }
+    color += sample_u8(src, sw, sh, fsw, fsh, ux, uy) * (kWeight[0] + lo);
+    dst[j * a.W + i] = quant(color);
+}
+
+// Final pass (post_final.glsl) from the y-blur target
+extern "C" __global__ void __launch_bounds__(256) sf_post_final(PostArgs a)
+{
+    uint32_t i, j;
+    if (!pixel(a.W, a.H, i, j)) return;
+    const float u = ((float)i + 0.5f) / a.fw, v = ((float)j + 0.5f) / a.fh;
+    const uint32_t px = (uint32_t)nearest(v, a.fh, (int)a.H) * a.W + (uint32_t)nearest(u, a.fw, (int)a.W);
+    const float4 p = ld4(a.pos, px);
+    final_store(a, j * a.W + i, p, is_background(p) ? 0.0f : sample_u8(a.blur_v, a.W, a.H, a.fw, a.fh, u, v));
+}
+
+// All four passes in one, valid when the host has proven (sf_capi.hip post_fusable): SSAO target =
+// G-buffer size, no blur tap can pass the normal test, and every LINEAR centre sample is the
+// fragment's own texel. Each blur is then color = own * weight, and the final samples its own texel.
+extern "C" __global__ void __launch_bounds__(256) sf_post_fused(PostArgs a)
+{
+    uint32_t i, j;
+    if (!pixel(a.W, a.H, i, j)) return;
+    const uint32_t px = j * a.W + i;
+    const uint8_t s = ssao_at(a, i, j);
+    if (a.ao) a.ao[px] = s;
+    const float w = rejected_weight();
+    const uint8_t h = quant(unorm(s) * w);
+    const uint8_t v = quant(unorm(h) * w);
+    // nearest(own centre) == (i, j) for the final's uv in this regime, as in ssao_at
+    const float4 p = ld4(a.pos, px);
+    final_store(a, px, p, unorm(v));
+}

@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <random>
 
 #include "sf_internal.h"
 
@@ -283,6 +284,43 @@ void mt19937_seed(uint32_t seed, uint32_t state[625])
     state[0] = seed;
     for (uint32_t i = 1; i < 624; ++i) state[i] = 1812433253u * (state[i - 1] ^ (state[i - 1] >> 30)) + i;
     state[624] = 624;
+}
+
+// SSAO::GenerateNoiseTexture (SSAO.cpp:144-164): 64x64 RGBA32F texels, each glm::normalize(vec4) of
+// four std::uniform_real_distribution<float>(-1, 1) draws from std::mt19937 seeded 12512. The
+// standard library is the same one the reference links (libstdc++ here), so this is the reference's
+// own generator; glm 0.9.5 normalize(vec4) = x * (1 / sqrt(((x*x + y*y) + z*z) + w*w))
+// (func_geometric.inl:268-277, func_exponential.inl:226-229).
+void ssao_noise(float out[SF_NOISE_SIZE * SF_NOISE_SIZE * 4])
+{
+    std::mt19937 mt;
+    mt.seed(12512);
+    std::uniform_real_distribution<float> dist(-1, 1);
+    for (int i = 0; i < SF_NOISE_SIZE * SF_NOISE_SIZE; ++i) {
+        float v[4];
+        for (float& x : v) x = dist(mt);
+        const float sqr = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+        const float inv = 1.0f / std::sqrt(sqr);
+        for (int k = 0; k < 4; ++k) out[4 * i + k] = v[k] * inv;
+    }
+}
+
+// The final and blur passes sample their RGBA8 sources LINEAR at the fragment centre. In the
+// 8-bit-subtexel texture model (sf_post.hip) that is exactly the fragment's own texel iff the centre
+// coordinate snaps to an integer for every i < n in both shader forms: (i+0.5) * (1/n) * n - 0.5
+// (post_ssao_blur.glsl:26-29) and (i+0.5) / n * n - 0.5 (post_final.glsl:17). Then the blur passes
+// with no accepted tap reduce to a per-pixel weight, and the fused post kernel equals the multi-pass
+// one bit for bit.
+bool post_centre_exact(uint32_t n)
+{
+    const float fn = (float)n, ps = 1.0f / fn;
+    for (uint32_t i = 0; i < n; ++i) {
+        const float fc = (float)i + 0.5f;
+        const float a = std::rint((fc * ps * fn - 0.5f) * 256.0f);
+        const float b = std::rint((fc / fn * fn - 0.5f) * 256.0f);
+        if (a != 256.0f * (float)i || b != 256.0f * (float)i) return false;
+    }
+    return true;
 }
 
 }  // namespace sfhost

@@ -59,6 +59,16 @@ class sf_stats(ctypes.Structure):
                 ("rays", ctypes.c_int64), ("overflow_tiles", ctypes.c_int64)]
 
 
+class sf_post_params(ctypes.Structure):
+    _fields_ = [("sample_radius", ctypes.c_float), ("intensity", ctypes.c_float), ("scale", ctypes.c_float),
+                ("bias", ctypes.c_float), ("normal_threshold", ctypes.c_float), ("depth_threshold", ctypes.c_float),
+                ("camera_position", ctypes.c_float * 3), ("downscale", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("stream", ctypes.c_void_p)]
+
+
+SF_POST_GENERAL = 1
+SF_POST_UNIT_NORMALS = 2
+
 # exported symbol -> (restype, argtypes); checked against include/sphereflake/sf.h by the tests
 _F = ctypes.POINTER(ctypes.c_float)
 _U = ctypes.POINTER(ctypes.c_uint32)
@@ -74,6 +84,15 @@ SIGNATURES = {
                                     ctypes.c_void_p, ctypes.c_void_p]),
     "sf_slab_rows": (ctypes.c_uint32, [ctypes.c_uint32] * 4),
     "sf_download": (ctypes.c_int, [_CTX, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "sf_download_async": (ctypes.c_int, [_CTX, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
+    "sf_post_defaults": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_post_params)]),
+    "sf_post_process": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_post_params), ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p]),
+    "sf_download_image": (ctypes.c_int, [_CTX, ctypes.c_void_p]),
+    "sf_ssao_noise": (ctypes.c_int, [_F]),
+    "sf_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    "sf_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
     "sf_device_buffers": (ctypes.c_int, [_CTX] + [ctypes.POINTER(ctypes.c_void_p)] * 4),
     "sf_synchronize": (ctypes.c_int, [_CTX]),
     "sf_get_stats": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_stats)]),
@@ -263,6 +282,7 @@ class Sphereflake:
 
     # lifetime --------------------------------------------------------------
     def close(self):
+        self.release_pinned()
         self._stop.set()
         if self._worker is not None:
             self._worker.join()
@@ -342,6 +362,78 @@ class Sphereflake:
     def GetGBuffer(self) -> GBuffer:
         pos, nrm, _, _ = self.download()
         return GBuffer(pos, nrm)
+
+    # transfer/interop ------------------------------------
+    def pinned_gbuffer(self) -> GBuffer:
+        """Host G-buffer arrays in the reference layout, page-locked for DMA (sf_host_register).
+        Pass them to download_async; release with release_pinned()."""
+        H, W = self.height, self.width
+        g = GBuffer(np.zeros((H, W, 4), np.float32), np.zeros((H, W, 4), np.float32))
+        for a in (g.positions, g.normals):
+            _check(lib().sf_host_register(a.ctypes.data_as(ctypes.c_void_p), a.nbytes), "sf_host_register")
+        self._pinned = getattr(self, "_pinned", []) + [g.positions, g.normals]
+        return g
+
+    def release_pinned(self):
+        for a in getattr(self, "_pinned", []):
+            lib().sf_host_unregister(a.ctypes.data_as(ctypes.c_void_p))
+        self._pinned = []
+
+    def download_async(self, g: GBuffer, stream: int | None = None):
+        """Stream-ordered D2H of the G-buffer into `g` (pinned arrays from pinned_gbuffer());
+        complete after Synchronize() (or the given stream's synchronisation)."""
+        vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+        with self._mutex:
+            _check(lib().sf_download_async(self._ctx, vp(g.positions), vp(g.normals), None, None,
+                                           ctypes.c_void_p(stream) if stream else None), "download_async", self._ctx)
+
+    # SSAO post-process (SURVEY.md §8(f2)) -----------------------------------
+    def post_params(self, **kw) -> sf_post_params:
+        """Reference defaults (SSAO.cpp:50-55, radius from the closest-hit stat, camera = view origin),
+        overridden by keyword (sample_radius, intensity, scale, bias, normal_threshold, depth_threshold,
+        camera_position, downscale, flags, stream)."""
+        p = sf_post_params()
+        _check(lib().sf_post_defaults(self._ctx, ctypes.byref(p)), "sf_post_defaults")
+        for k, v in kw.items():
+            if k == "camera_position":
+                p.camera_position[:] = [float(x) for x in _f32(v, 3)]
+            elif k == "stream":
+                p.stream = v
+            else:
+                setattr(p, k, v)
+        return p
+
+    def PostProcess(self, pos_ptr: int = 0, nrm_ptr: int = 0, rgba_ptr: int = 0, ao_ptr: int = 0, **kw):
+        """SSAO + blur x + blur y + final composite on the device (asynchronous). Pointers are device
+        addresses (0 = the context's G-buffer / image buffer); ao_ptr receives the SSAO target."""
+        p = self.post_params(**kw)
+        vp = lambda x: ctypes.c_void_p(x) if x else None
+        with self._mutex:
+            _check(lib().sf_post_process(self._ctx, ctypes.byref(p), vp(pos_ptr), vp(nrm_ptr), vp(rgba_ptr),
+                                         vp(ao_ptr)), "sf_post_process", self._ctx)
+
+    def download_image(self) -> np.ndarray:
+        """[H, W, 4] uint8 RGBA of the last PostProcess into the context image buffer."""
+        img = np.empty((self.height, self.width, 4), np.uint8)
+        with self._mutex:
+            _check(lib().sf_download_image(self._ctx, img.ctypes.data_as(ctypes.c_void_p)), "sf_download_image",
+                   self._ctx)
+        return img
+
+    @staticmethod
+    def ssao_noise() -> np.ndarray:
+        out = np.empty((64 * 64, 4), np.float32)
+        _check(lib().sf_ssao_noise(_fp(out)), "sf_ssao_noise")
+        return out
+
+    @staticmethod
+    def save_ppm(path: str, rgb) -> None:
+        """Write an [H, W, 3] float image (0..1, clamped) as a binary PPM (8-bit), y = 0 on top."""
+        a = np.clip(np.asarray(rgb, np.float32), 0.0, 1.0)
+        b = (a * 255.0 + 0.5).astype(np.uint8)
+        with open(path, "wb") as f:
+            f.write(f"P6 {b.shape[1]} {b.shape[0]} 255\n".encode())
+            f.write(np.ascontiguousarray(b[:, :, :3]).tobytes())
 
     def tile_trace(self, enable: bool | None = None):
         """Diagnostics: enable per-tile timing, or (enable=None) fetch [tiles, 3] uint64

@@ -1,0 +1,54 @@
+// class_drive.cpp -- exercises the reference-compatible C++ class (Sphereflake.hpp) the way the
+// reference app drives SphereflakeRaytracer::Sphereflake (main.cpp: construct, SetView each frame,
+// GetGBuffer for the PBO upload, the stats getters for the overlay). Used by tests/test_gpu_class.py.
+//
+// usage: class_drive W H ox oy oz tlx tly tlz trx try trz blx bly blz out.bin [frames]
+//   corners as C99 hex floats (bit-exact hand-over); writes positions then normals (W*H vec4 each)
+//   of the last frame to out.bin and prints "max_depth rays closest(hex)" on stdout.
+#include <cstdio>
+#include <cstdlib>
+#include <exception>
+
+#include "Sphereflake.hpp"
+
+using namespace SphereflakeRaytracer;
+
+int main(int argc, char** argv)
+{
+    if (argc < 16) {
+        std::fprintf(stderr, "usage: %s W H o.xyz tl.xyz tr.xyz bl.xyz out.bin [frames]\n", argv[0]);
+        return 2;
+    }
+    try {
+        const size_t W = std::strtoul(argv[1], nullptr, 10), H = std::strtoul(argv[2], nullptr, 10);
+        float v[12];
+        for (int k = 0; k < 12; ++k) v[k] = std::strtof(argv[3 + k], nullptr);
+        const int frames = argc > 16 ? std::atoi(argv[16]) : 1;
+        Sphereflake flake(W, H);
+        long long rays = 0;
+        for (int f = 0; f < frames; ++f) {
+            flake.SetView(sf_vec3(v[0], v[1], v[2]), sf_vec3(v[3], v[4], v[5]), sf_vec3(v[6], v[7], v[8]),
+                          sf_vec3(v[9], v[10], v[11]));
+            flake.Render();
+            const GBuffer& g = flake.GetGBuffer();   // the reference reads it right after (main.cpp:306-310)
+            if (g.positions.size() != W * H || g.normals.size() != W * H) return 3;
+        }
+        rays = flake.GetRaysPerSecond();
+        const GBuffer& g = flake.GetGBuffer();
+        FILE* out = std::fopen(argv[15], "wb");
+        if (!out) return 4;
+        std::fwrite(g.positions.data(), sizeof(sf_vec4), g.positions.size(), out);
+        std::fwrite(g.normals.data(), sizeof(sf_vec4), g.normals.size(), out);
+        std::fclose(out);
+        std::printf("%d %lld %a\n", flake.GetMaxDepthReached(), rays, flake.GetClosestSphereDistance());
+        flake.ResetRaysPerSecond();
+        flake.ResetMaxDepthReached();
+        flake.ResetClosestSphereDistance();
+        std::printf("%d %lld %a\n", flake.GetMaxDepthReached(), flake.GetRaysPerSecond(),
+                    flake.GetClosestSphereDistance());
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "%s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

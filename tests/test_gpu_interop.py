@@ -1,0 +1,72 @@
+"""GPU tests of the drop-in surfaces either side of the trace:
+- the reference-compatible C++ class (csrc/Sphereflake.hpp) driven like the reference app drives
+  SphereflakeRaytracer::Sphereflake (tests/cpp/class_drive.cpp), bit-exact against the golden frames;
+- stream-ordered download into page-locked host buffers, bit-identical to the synchronous path."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PKG, load_frame, load_npz
+from sfcheck import FLT_MAX, frame_digest
+
+pytestmark = pytest.mark.gpu
+
+import sphereflake_amd as sf  # noqa: E402
+
+DRIVE = os.path.join(PKG, "build", "class_drive")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    sf.build()
+    assert sf.device_count() >= 1, "no HIP device visible: GPU tests must run on an MI355X"
+    assert os.path.exists(DRIVE), "class_drive not built (make -C sphereflake-raytracer_amd)"
+
+
+def drive(name, tmp_path, frames=1):
+    fx = load_frame(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    corners = sf.config_camera(W, H, K).corners()
+    args = [DRIVE, str(W), str(H)] + [float(x).hex() for c in corners for x in c]
+    out = tmp_path / f"{name}.bin"
+    r = subprocess.run(args + [str(out), str(frames)], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr
+    g = np.fromfile(out, np.float32).reshape(2, H, W, 4)
+    lines = r.stdout.split("\n")
+    return fx, g[0], g[1], lines[0].split(), lines[1].split()
+
+
+@pytest.mark.parametrize("name", ["t2", "t3"])
+def test_cpp_class_matches_golden(name, tmp_path):
+    fx, pos, nrm, st, reset = drive(name, tmp_path, frames=2)
+    exp = load_npz(name)
+    assert np.array_equal(pos.view(np.uint32), exp["pos4"].view(np.uint32))
+    assert np.array_equal(nrm.view(np.uint32), exp["nrm4"].view(np.uint32))
+    assert int(st[0]) == fx["stats"]["max_depth"]
+    assert int(st[1]) == 2 * fx["W"] * fx["H"]
+    assert np.float32(float.fromhex(st[2])) == np.float32(float.fromhex(fx["stats"]["closest"]))
+    assert int(reset[0]) == 0 and int(reset[1]) == 0 and np.float32(float.fromhex(reset[2])) == np.float32(FLT_MAX)
+
+
+def test_cpp_class_config_c1(tmp_path):
+    fx, pos, nrm, st, _ = drive("c1", tmp_path)
+    assert frame_digest(pos, nrm) == fx["frame_digest"]
+
+
+def test_async_pinned_download_equals_sync():
+    fx = load_frame("c1")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        s.Render()
+        ref = s.GetGBuffer()
+        g = s.pinned_gbuffer()
+        s.Render()
+        s.download_async(g)
+        s.Synchronize()
+        assert np.array_equal(g.positions.view(np.uint32), ref.positions.view(np.uint32))
+        assert np.array_equal(g.normals.view(np.uint32), ref.normals.view(np.uint32))
+        assert frame_digest(g.positions, g.normals) == fx["frame_digest"]
+        s.release_pinned()

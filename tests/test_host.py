@@ -155,3 +155,16 @@ def test_mt19937_known_answers():
         y ^= y >> 18
         out.append(y & 0xFFFFFFFF)
     assert out == j["draws"]
+
+
+def test_save_ppm_layout(tmp_path):
+    img = np.zeros((2, 3, 3), np.float32)
+    img[0, 0] = (1.0, 0.5, 0.0)
+    img[1, 2] = (2.0, -1.0, 0.25)   # clamped
+    p = tmp_path / "x.ppm"
+    sf.Sphereflake.save_ppm(str(p), img)
+    b = p.read_bytes()
+    head = b"P6 3 2 255\n"
+    assert b[:len(head)] == head
+    px = np.frombuffer(b[len(head):], np.uint8).reshape(2, 3, 3)
+    assert tuple(px[0, 0]) == (255, 128, 0) and tuple(px[1, 2]) == (255, 0, 64)
