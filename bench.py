@@ -105,6 +105,29 @@ def cpu_baseline(width, height, k, threads):
             "sample": f"every 8th row of a {width}x{height} K={k} frame, oracle C restatement, 1 thread"}
 
 
+POST_BYTES_PER_PIXEL = 36   # fused pass: position + normal in (32 B), RGBA8 out (4 B)
+
+
+def post_rates(ctx, torch, stream, width, height, reps=20):
+    """Mean device time of sf_post_process (fused single pass with the reference thresholds, and the
+    forced 4-pass chain) over `reps` launches, with HBM roofline of the fused kernel."""
+    out = {}
+    for name, flags in (("fused", 0), ("multipass", sf.SF_POST_GENERAL)):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        with torch.cuda.stream(stream):
+            ctx.PostProcess(flags=flags, stream=stream.cuda_stream)
+            for a, b in ev:
+                a.record(stream)
+                ctx.PostProcess(flags=flags, stream=stream.cuda_stream)
+                b.record(stream)
+        torch.cuda.synchronize()
+        out[name + "_ms"] = round(float(np.mean([a.elapsed_time(b) for a, b in ev])), 4)
+    gbs = POST_BYTES_PER_PIXEL * width * height / (out["fused_ms"] * 1e-3) / 1e9
+    out["fused_roofline"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_pixel": POST_BYTES_PER_PIXEL}
+    return out
+
+
 def transfer_rates(ctx, torch, dev, stream, width, height, kernel, frames=8):
     """G-buffer D2H cost (positions + normals, 32 B/pixel). Pageable synchronous
     download (sf_download, what the reference-style GetGBuffer pays unpinned), stream-ordered copy into
@@ -125,35 +148,58 @@ def transfer_rates(ctx, torch, dev, stream, width, height, kernel, frames=8):
     ctx.Synchronize()
     pinned_ms = (time.perf_counter() - t) * 1e3 / frames
     ctx.release_pinned()
-    # double-buffered render -> D2H pipeline
+    # double-buffered pipelines: render frame i+1 while frame i drains over PCIe on a copy stream.
+    # "gbuffer": positions + normals (what the reference's PBO upload reads, 32 B/pixel);
+    # "image": SSAO + blur + final on the device first (sf_post_process), RGBA8 out (4 B/pixel)
     copy = torch.cuda.Stream(device=dev)
-    slabs = [[torch.empty((height, width, 4), dtype=torch.float32, device=dev) for _ in range(2)] for _ in range(2)]
-    host = [[torch.empty((height, width, 4), dtype=torch.float32, pin_memory=True) for _ in range(2)] for _ in range(2)]
-    done = [torch.cuda.Event() for _ in range(2)]
-    drained = [torch.cuda.Event() for _ in range(2)]
-    torch.cuda.synchronize(dev)
-    t = time.perf_counter()
-    for i in range(frames + 1):
-        b = i & 1
-        if i < frames:
-            with torch.cuda.stream(stream):
-                if i >= 2:
-                    stream.wait_event(drained[b])
-                ctx.render_to(slabs[b][0].data_ptr(), slabs[b][1].data_ptr(), kernel=kernel, stream=stream.cuda_stream)
-                done[b].record(stream)
-        if i >= 1:
-            p = (i - 1) & 1
-            with torch.cuda.stream(copy):
-                copy.wait_event(done[p])
-                host[p][0].copy_(slabs[p][0], non_blocking=True)
-                host[p][1].copy_(slabs[p][1], non_blocking=True)
-                drained[p].record(copy)
-    torch.cuda.synchronize(dev)
-    pipe_ms = (time.perf_counter() - t) * 1e3 / frames
+
+    def pipeline(image):
+        slabs = [[torch.empty((height, width, 4), dtype=torch.float32, device=dev) for _ in range(2)] for _ in range(2)]
+        rgba = [torch.empty((height, width, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
+        if image:
+            host = [[torch.empty((height, width, 4), dtype=torch.uint8, pin_memory=True)] for _ in range(2)]
+        else:
+            host = [[torch.empty((height, width, 4), dtype=torch.float32, pin_memory=True) for _ in range(2)]
+                    for _ in range(2)]
+        done = [torch.cuda.Event() for _ in range(2)]
+        drained = [torch.cuda.Event() for _ in range(2)]
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for i in range(frames + 1):
+            b = i & 1
+            if i < frames:
+                with torch.cuda.stream(stream):
+                    if i >= 2:
+                        stream.wait_event(drained[b])
+                    ctx.render_to(slabs[b][0].data_ptr(), slabs[b][1].data_ptr(), kernel=kernel,
+                                  stream=stream.cuda_stream)
+                    if image:
+                        ctx.PostProcess(slabs[b][0].data_ptr(), slabs[b][1].data_ptr(), rgba[b].data_ptr(),
+                                        flags=sf.SF_POST_UNIT_NORMALS, stream=stream.cuda_stream)
+                    done[b].record(stream)
+            if i >= 1:
+                p = (i - 1) & 1
+                with torch.cuda.stream(copy):
+                    copy.wait_event(done[p])
+                    if image:
+                        host[p][0].copy_(rgba[p], non_blocking=True)
+                    else:
+                        host[p][0].copy_(slabs[p][0], non_blocking=True)
+                        host[p][1].copy_(slabs[p][1], non_blocking=True)
+                    drained[p].record(copy)
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t) * 1e3 / frames
+
+    pipeline(False)   # warm the pinned pools
+    pipe_ms = pipeline(False)
+    pipeline(True)
+    img_ms = pipeline(True)
     return {"bytes": nbytes, "pageable_ms": round(pageable_ms, 3), "pinned_ms": round(pinned_ms, 3),
             "pinned_GBps": round(nbytes / (pinned_ms * 1e-3) / 1e9, 2),
             "pipelined_frame_ms": round(pipe_ms, 3),
             "pcie_inclusive_Mrays": round(width * height / (pipe_ms * 1e-3) / 1e6, 2),
+            "image_pipelined_frame_ms": round(img_ms, 3),
+            "image_pcie_inclusive_Mrays": round(width * height / (img_ms * 1e-3) / 1e6, 2),
             "note": "PCIe-inclusive figures; `value` is the HBM-resident render rate"}
 
 
@@ -255,6 +301,11 @@ def main():
     total_rays = rays_per_step_rank * n if args.mode == "frames" else width * height
     value = total_rays / t_step / 1e6
 
+    # SSAO post-process of the rendered G-buffer, timed alone on the render stream
+    post = None
+    if rank == 0 and args.mode == "frames":
+        post = post_rates(ctx, torch, stream, width, height)
+
     # D2H into the host GBuffer (PCIe-inclusive, reported separately -- never `value`)
     d2h = None
     if rank == 0 and args.mode == "frames":
@@ -295,6 +346,7 @@ def main():
                        "parallelism": f"frames x{n}" if args.mode == "frames" else f"row-bands x{n} + RCCL gather"},
             "frame_ms": round(t_step * 1e3, 4),
             "kernel_ms": round(kern_ms_max, 4),
+            "post": post,
             "d2h": d2h,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),

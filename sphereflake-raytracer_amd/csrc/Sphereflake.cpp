@@ -3,14 +3,17 @@
 #include "Sphereflake.hpp"
 
 #include <chrono>
+#include <cstring>
 #include <ctime>
 
 namespace SphereflakeRaytracer {
 
-void Sphereflake::Check(int rc)
+static void Check(int rc)
 {
     if (rc != SF_OK) throw std::runtime_error(std::string("sphereflake: ") + sf_strerror(rc));
 }
+
+void Sphereflake::Check(int rc) { SphereflakeRaytracer::Check(rc); }
 
 Sphereflake::Sphereflake(size_t width, size_t height, int device) : m_Width(width), m_Height(height)
 {
@@ -113,5 +116,37 @@ float Sphereflake::GetClosestSphereDistance() const
 }
 
 void Sphereflake::ResetClosestSphereDistance() { Check(sf_reset_closest(m_Ctx)); }
+
+SSAO::SSAO(Sphereflake& flake, int downScale) : m_Flake(flake)
+{
+    if (downScale < 1) throw std::runtime_error("sphereflake: SSAO downScale must be >= 1");
+    Check(sf_post_defaults(flake.Context(), &m_Params));
+    m_Params.downscale = (uint32_t)downScale;
+}
+
+void SSAO::SetCameraPosition(const sf_vec3& p)
+{
+    m_Params.camera_position[0] = p.x;
+    m_Params.camera_position[1] = p.y;
+    m_Params.camera_position[2] = p.z;
+    m_CameraSet = true;
+}
+
+void SSAO::Render()
+{
+    if (!m_CameraSet) {
+        sf_post_params d;
+        Check(sf_post_defaults(m_Flake.Context(), &d));
+        std::memcpy(m_Params.camera_position, d.camera_position, sizeof d.camera_position);
+    }
+    Check(sf_post_process(m_Flake.Context(), &m_Params, nullptr, nullptr, nullptr, nullptr));
+}
+
+const std::vector<uint8_t>& SSAO::GetImage() const
+{
+    m_Image.resize(m_Flake.Width() * m_Flake.Height() * 4);
+    Check(sf_download_image(m_Flake.Context(), m_Image.data()));
+    return m_Image;
+}
 
 }  // namespace SphereflakeRaytracer

@@ -2,9 +2,11 @@
 // reference app drives SphereflakeRaytracer::Sphereflake (main.cpp: construct, SetView each frame,
 // GetGBuffer for the PBO upload, the stats getters for the overlay). Used by tests/test_gpu_class.py.
 //
-// usage: class_drive W H ox oy oz tlx tly tlz trx try trz blx bly blz out.bin [frames]
+// usage: class_drive W H ox oy oz tlx tly tlz trx try trz blx bly blz out.bin [frames [image.bin]]
 //   corners as C99 hex floats (bit-exact hand-over); writes positions then normals (W*H vec4 each)
-//   of the last frame to out.bin and prints "max_depth rays closest(hex)" on stdout.
+//   of the last frame to out.bin and prints "max_depth rays closest(hex)" on stdout. With image.bin,
+//   also runs the headless SSAO chain as main.cpp:312-330 does (radius from GetClosestSphereDistance,
+//   camera = origin) and writes the RGBA8 image.
 #include <cstdio>
 #include <cstdlib>
 #include <exception>
@@ -41,6 +43,17 @@ int main(int argc, char** argv)
         std::fwrite(g.normals.data(), sizeof(sf_vec4), g.normals.size(), out);
         std::fclose(out);
         std::printf("%d %lld %a\n", flake.GetMaxDepthReached(), rays, flake.GetClosestSphereDistance());
+        if (argc > 17) {
+            SSAO ssao(flake, 1);
+            ssao.SetSampleRadiusMultiplier(flake.GetClosestSphereDistance());
+            ssao.SetCameraPosition(sf_vec3(v[0], v[1], v[2]));
+            ssao.Render();
+            const std::vector<uint8_t>& img = ssao.GetImage();
+            FILE* f = std::fopen(argv[17], "wb");
+            if (!f) return 4;
+            std::fwrite(img.data(), 1, img.size(), f);
+            std::fclose(f);
+        }
         flake.ResetRaysPerSecond();
         flake.ResetMaxDepthReached();
         flake.ResetClosestSphereDistance();

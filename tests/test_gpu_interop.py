@@ -25,16 +25,19 @@ def device():
     assert os.path.exists(DRIVE), "class_drive not built (make -C sphereflake-raytracer_amd)"
 
 
-def drive(name, tmp_path, frames=1):
+def drive(name, tmp_path, frames=1, image=False):
     fx = load_frame(name)
     W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
     corners = sf.config_camera(W, H, K).corners()
     args = [DRIVE, str(W), str(H)] + [float(x).hex() for c in corners for x in c]
     out = tmp_path / f"{name}.bin"
-    r = subprocess.run(args + [str(out), str(frames)], capture_output=True, text=True, timeout=100)
+    extra = [str(tmp_path / f"{name}.rgba")] if image else []
+    r = subprocess.run(args + [str(out), str(frames)] + extra, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr
     g = np.fromfile(out, np.float32).reshape(2, H, W, 4)
     lines = r.stdout.split("\n")
+    if image:
+        return fx, g[0], g[1], lines[0].split(), np.fromfile(tmp_path / f"{name}.rgba", np.uint8).reshape(H, W, 4)
     return fx, g[0], g[1], lines[0].split(), lines[1].split()
 
 
@@ -70,3 +73,14 @@ def test_async_pinned_download_equals_sync():
         assert np.array_equal(g.normals.view(np.uint32), ref.normals.view(np.uint32))
         assert frame_digest(g.positions, g.normals) == fx["frame_digest"]
         s.release_pinned()
+
+
+def test_cpp_ssao_class_matches_oracle(tmp_path):
+    """Headless SSAO class (Sphereflake.hpp) driven like main.cpp:312-330, against oracle/post.py."""
+    from oracle import post
+    fx, pos, nrm, st, img = drive("t1", tmp_path, image=True)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    origin = sf.config_camera(W, H, K).corners()[0]
+    radius = np.float32(8) * np.float32(float.fromhex(st[2]))
+    exp = post.post_process(pos, nrm, origin, radius)[0]
+    assert np.array_equal(img, exp)
