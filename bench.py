@@ -211,12 +211,17 @@ def main():
     import torch
     import torch.distributed as dist
     dist_on = world > 1
+    # SF_BENCH_BACKEND=gloo + local ranks folded onto the visible devices: rehearses the multi-rank
+    # flow on a 1-GPU box (RCCL refuses two ranks on one GPU). The driver's runs use nccl (= RCCL).
+    backend = os.environ.get("SF_BENCH_BACKEND", "nccl")
+    gpu = local % max(1, torch.cuda.device_count()) if dist_on else 0
+    torch.cuda.set_device(gpu)
     if dist_on:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if dist_on else 0)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
     if not os.path.exists(sf.LIB_PATH):
         if rank == 0:
             sf.build()
@@ -267,8 +272,12 @@ def main():
             if args.mode == "rows" and dist_on:
                 send_p[:slab_rows].copy_(slab_p)
                 send_n[:slab_rows].copy_(slab_n)
-                shard.gather_frame(send_p, height, args.band_rows)   # RCCL gather + reassembly on rank 0
-                shard.gather_frame(send_n, height, args.band_rows)
+                if backend == "nccl":
+                    shard.gather_frame(send_p, height, args.band_rows)   # RCCL gather + reassembly on rank 0
+                    shard.gather_frame(send_n, height, args.band_rows)
+                else:   # gloo rehearsal: host tensors
+                    shard.gather_frame(send_p.cpu(), height, args.band_rows)
+                    shard.gather_frame(send_n.cpu(), height, args.band_rows)
 
     for i in range(args.warmup):
         run_step(i, False)

@@ -12,8 +12,9 @@ Restates, in IEEE binary32 with the shaders' operation order:
 with the GL state they run under (main.cpp:181-203, GLFramebufferObject.cpp:41-45, SSAO.cpp:166-174):
 G-buffer textures RGBA32F NEAREST/CLAMP; pass targets RGBA8 LINEAR/CLAMP (every pass output
 quantised to 8 bits); noise RGBA32F LINEAR/REPEAT. Texture filtering is modelled with the texel
-coordinate snapped to 8 fractional bits (NEAREST floor, GL bilinear blend) -- the same model the
-HIP kernels implement. Parity against GL driver output is unpinned (no GL here); parity of the noise
+coordinate snapped to 8 fractional bits (NEAREST floor, GL bilinear blend), and division by a uniform
+or a per-tap scalar as multiplication by the correctly rounded reciprocal -- the same model the HIP
+kernels implement. Parity against GL driver output is unpinned (no GL here); parity of the noise
 texture is pinned bit for bit against the reference's own std::mt19937 path (sf_ssao_noise).
 """
 from __future__ import annotations
@@ -133,7 +134,8 @@ def ssao(pos4, nrm4, radius, downscale=1, intensity=DEFAULTS["intensity"], scale
     noise = ssao_noise() if noise is None else noise
     fx = (np.arange(aw, dtype=np.float32) + F(0.5))[None, :].repeat(ah, 0)
     fy = (np.arange(ah, dtype=np.float32) + F(0.5))[:, None].repeat(aw, 1)
-    u, v = fx / F(aw), fy / F(ah)
+    rcx, rcy = F(1) / F(aw), F(1) / F(ah)
+    u, v = fx * rcx, fy * rcy
     tx, ty = nearest(u, W), nearest(v, H)
     p, n = pos4[ty, tx, :3], nrm4[ty, tx, :3]
     bg = _background(p)
@@ -142,14 +144,16 @@ def ssao(pos4, nrm4, radius, downscale=1, intensity=DEFAULTS["intensity"], scale
         nx, ny = sample_noise(noise, u * F(0.1), v * F(0.1))
         rx, ry = nx * F(2) - F(1), ny * F(2) - F(1)
         ln = np.sqrt(rx * rx + ry * ry)
-        rx, ry = rx / ln, ry / ln
+        il = F(1) / ln
+        rx, ry = rx * il, ry * il
 
         def occlude(ox, oy):
-            sx, sy = nearest((fx + ox) / F(aw), W), nearest((fy + oy) / F(ah), H)
+            sx, sy = nearest((fx + ox) * rcx, W), nearest((fy + oy) * rcy, H)
             s = pos4[sy, sx, :3]
             dx, dy, dz = s[..., 0] - p[..., 0], s[..., 1] - p[..., 1], s[..., 2] - p[..., 2]
             dist = np.sqrt(dx * dx + dy * dy + dz * dz)
-            t = n[..., 0] * (dx / dist) + n[..., 1] * (dy / dist) + n[..., 2] * (dz / dist)
+            idt = F(1) / dist
+            t = n[..., 0] * (dx * idt) + n[..., 1] * (dy * idt) + n[..., 2] * (dz * idt)
             m = t - F(bias)
             c = np.where(m > F(0), m, F(0)).astype(np.float32)
             return c * (F(1) / (F(1) + dist * dist * F(scale))) * F(intensity)
@@ -202,7 +206,7 @@ def final(pos4, ssao_tex, camera_position):
     H, W = pos4.shape[:2]
     fx = (np.arange(W, dtype=np.float32) + F(0.5))[None, :].repeat(H, 0)
     fy = (np.arange(H, dtype=np.float32) + F(0.5))[:, None].repeat(W, 1)
-    u, v = fx / F(W), fy / F(H)
+    u, v = fx * (F(1) / F(W)), fy * (F(1) / F(H))
     p = pos4[nearest(v, H), nearest(u, W), :3]
     s = sample_u8(ssao_tex, u, v)
     cam = np.asarray(camera_position, np.float32)

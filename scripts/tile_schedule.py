@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--K", type=float, default=0.25)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "tile_trace.npy"))
+    ap.add_argument("--counts", action="store_true", help="library is a COUNTS=1 build: print event counts")
     a = ap.parse_args()
     with sf.Sphereflake(a.width, a.height) as s:
         s.SetCamera(sf.config_camera(a.width, a.height, a.K))
@@ -29,7 +30,13 @@ def main():
             s.Render()
         tr = s.tile_trace()
         ph = s.phase_sums.astype(np.float64)
-    if ph.sum() > 0:
+    if a.counts:
+        names = ["nodes tested", "child iterations", "no-lane-hit iterations", "children entered", "leaf skips"]
+        per = a.reps
+        print("event counts per render:", ", ".join(f"{n} {ph[k] / per:.0f}" for k, n in enumerate(names)))
+        print(f"  iterations/node {ph[1] / max(ph[0], 1):.2f}, miss share {ph[2] / max(ph[1], 1):.3f}, "
+              f"entered/node {ph[3] / max(ph[0], 1):.2f}")
+    elif ph.sum() > 0:
         names = {1: "push", 6: "expand: node read + build", 2: "expand: child tests", 3: "head->self",
                  4: "self test", 5: "pop"}
         tot = ph[1:7].sum()

@@ -232,10 +232,26 @@ __device__ __forceinline__ void wave_atomic_add_u64(uint64_t* p, uint64_t v)
             for (int k_ = 1; k_ < 7; ++k_) wave_atomic_add_u64((uint64_t*)(p) + k_, ph_sum[k_]);  \
         }                                                                                      \
     } while (0)
+#elif defined(SF_COUNTS)
+// Diagnostic build only (make COUNTS=1): per-wave event counts instead of stamps, summed into
+// phase_sums[k]: 0 nodes whose children are tested, 1 child-loop iterations, 2 iterations no lane
+// hits (bounding), 3 children entered, 4 leaf skips.
+#define SF_STAMP_DECL uint64_t ph_sum[7] = {0, 0, 0, 0, 0, 0, 0}
+#define SF_STAMP(k)
+#define SF_COUNT(k, v) (ph_sum[k] += (v))
+#define SF_STAMP_FLUSH(p)                                                                      \
+    do {                                                                                       \
+        if (p) {                                                                               \
+            for (int k_ = 0; k_ < 5; ++k_) wave_atomic_add_u64((uint64_t*)(p) + k_, ph_sum[k_]);  \
+        }                                                                                      \
+    } while (0)
 #else
 #define SF_STAMP_DECL
 #define SF_STAMP(k)
 #define SF_STAMP_FLUSH(p) (void)(p)
+#endif
+#ifndef SF_COUNT
+#define SF_COUNT(k, v)
 #endif
 
 // Per-depth constants {(2r)^2, r^2, (4/3) r, T} through the constant address space, so a uniform depth
@@ -379,6 +395,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         if (lod_cull) {
             const float leaf = depth_leaf(K, d);
             if (__builtin_amdgcn_readfirstlane((int)(pc.w > leaf))) {
+                SF_COUNT(4, 1);
                 pend = 0u;
                 return 0u;
             }
@@ -419,16 +436,21 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             // (each ballot is the compare's own lane mask: no bool materialisation); per-lane bools
             // are formed only where a lane's own bit is needed (its E bit).
             const uint64_t actm = wave_ballot(act);
+            SF_COUNT(0, 1);
             while (M) {   // uniform loop over the children some lane can reach, in index order
                 const uint32_t i = __builtin_ctz(M);
                 M &= M - 1u;
+                SF_COUNT(1, 1);
                 const float cx = readlane_f(x, 27u + i), cy = readlane_f(y, 27u + i);
                 const float cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
                 const float tca = (cx * dx + cy * dy) + cz * dz;
                 const float d2 = cc - tca * tca;
                 const bool f0 = tca >= 0.0f, f1 = d2 <= R2b;
                 const uint64_t hbm = actm & wave_ballot(f0) & wave_ballot(f1);   // bounding (SIMD_AVX.h:247-258)
-                if (hbm == 0ull) continue;
+                if (hbm == 0ull) {
+                    SF_COUNT(2, 1);
+                    continue;
+                }
                 // LOD on t = fl(tca - sqrt_rn(R2b - d2)) (SIMD_AVX.h:260-267; t0 <= t1 picks t1 for
                 // thc >= 0). Fast bracket: the hardware sqrt is within 2 ulp of sqrt_rn and t is
                 // monotone in it, so t_lo = fl(tca - (s + 2ulp)) <= t <= t_hi = fl(tca - (s - 2ulp)):
@@ -453,6 +475,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 }
                 e = exi ? (e | (1u << i)) : e;
                 pm |= (exm != 0ull ? 1u : 0u) << i;
+                SF_COUNT(3, exm != 0ull ? 1 : 0);
             }
         } else {
             // Packet semantics (frame-less mode): early-outs over the 8 lanes of a reference packet.

@@ -12,8 +12,10 @@
 //   - noise: RGBA32F 64x64, LINEAR, REPEAT (SSAO.cpp:166-174)
 // Texture filtering is a model, not a driver emulation: the texel-space coordinate is snapped to
 // 8 fractional bits (round to nearest even), NEAREST takes floor, LINEAR the GL bilinear blend
-// with those 1/256 weights. oracle/post.py restates the same formulas; the GPU result equals it bit
-// for bit (tests/test_gpu_post.py).
+// with those 1/256 weights. Division by a uniform or by a per-tap scalar is evaluated as
+// multiplication by the correctly rounded reciprocal, as shader compilers emit vector / scalar.
+// oracle/post.py restates the same formulas; the GPU result equals it bit for bit
+// (tests/test_gpu_post.py).
 //
 // With the reference's thresholds (normalThreshold 2.47 > any dot of two unit normals) no blur tap is
 // ever accepted, so both blurs collapse to a per-pixel weight: sf_post_fused does SSAO + blurs + final
@@ -91,15 +93,17 @@ __device__ inline float2 sample_noise(const float* noise, float u, float v)
 
 __device__ inline bool is_background(float4 p) { return p.x * p.x + p.y * p.y + p.z * p.z == 0.0f; }   // length == 0
 
-// post_ssao.glsl:19-25 occlude()
-__device__ inline float occlude(const PostArgs& a, float fx, float fy, float ox, float oy, float4 p, float4 n)
+// post_ssao.glsl:19-25 occlude(); rx, ry = 1 / framebufferSize
+__device__ inline float occlude(const PostArgs& a, float fx, float fy, float ox, float oy, float rx, float ry, float4 p,
+                                float4 n)
 {
-    const int tx = nearest((fx + ox) / a.faw, a.fw, (int)a.W);
-    const int ty = nearest((fy + oy) / a.fah, a.fh, (int)a.H);
+    const int tx = nearest((fx + ox) * rx, a.fw, (int)a.W);
+    const int ty = nearest((fy + oy) * ry, a.fh, (int)a.H);
     const float4 s = ld4(a.pos, (uint32_t)ty * a.W + (uint32_t)tx);
     const float dx = s.x - p.x, dy = s.y - p.y, dz = s.z - p.z;
     const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
-    const float t = n.x * (dx / dist) + n.y * (dy / dist) + n.z * (dz / dist);
+    const float id = 1.0f / dist;
+    const float t = n.x * (dx * id) + n.y * (dy * id) + n.z * (dz * id);
     const float m = t - a.bias;
     const float c = m > 0.0f ? m : 0.0f;   // max(0.0, NaN) -> 0
     return c * (1.0f / (1.0f + dist * dist * a.scale)) * a.intensity;
@@ -109,7 +113,8 @@ __device__ inline float occlude(const PostArgs& a, float fx, float fy, float ox,
 __device__ inline uint8_t ssao_at(const PostArgs& a, uint32_t i, uint32_t j)
 {
     const float fx = (float)i + 0.5f, fy = (float)j + 0.5f;
-    const float u = fx / a.faw, v = fy / a.fah;
+    const float rx = 1.0f / a.faw, ry = 1.0f / a.fah;
+    const float u = fx * rx, v = fy * ry;
     const uint32_t px = (uint32_t)nearest(v, a.fh, (int)a.H) * a.W + (uint32_t)nearest(u, a.fw, (int)a.W);
     const float4 p = ld4(a.pos, px);
     if (is_background(p)) return 0;   // vec4(0, 0, 0, 1)
@@ -117,22 +122,22 @@ __device__ inline uint8_t ssao_at(const PostArgs& a, uint32_t i, uint32_t j)
     const float R = a.radius >= 0.0f ? a.radius : 8.0f * sf_key_float(a.stats[1]);
     const float rad = R / sqrtf(fabsf(p.z));
     const float2 nz = sample_noise(a.noise, u * 0.1f, v * 0.1f);
-    float rx = nz.x * 2.0f - 1.0f, ry = nz.y * 2.0f - 1.0f;
-    const float len = sqrtf(rx * rx + ry * ry);
-    rx = rx / len;
-    ry = ry / len;
+    const float qx = nz.x * 2.0f - 1.0f, qy = nz.y * 2.0f - 1.0f;
+    const float len = sqrtf(qx * qx + qy * qy);
+    const float il = 1.0f / len;
+    const float nx = qx * il, ny = qy * il;
     float ao = 0.0f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const float kx = k == 0 ? 1.0f : k == 1 ? -1.0f : 0.0f;   // kernel[4] (post_ssao.glsl:15)
         const float ky = k == 2 ? 1.0f : k == 3 ? -1.0f : 0.0f;
-        const float f = 2.0f * (rx * kx + ry * ky);                 // reflect(I, N) = I - 2 dot(N, I) N
-        const float c1x = (kx - f * rx) * rad, c1y = (ky - f * ry) * rad;
+        const float f = 2.0f * (nx * kx + ny * ky);                 // reflect(I, N) = I - 2 dot(N, I) N
+        const float c1x = (kx - f * nx) * rad, c1y = (ky - f * ny) * rad;
         const float c2x = c1x * 0.707f - c1y * 0.707f, c2y = c1x * 0.707f + c1y * 0.707f;
-        ao += occlude(a, fx, fy, c1x * 0.25f, c1y * 0.25f, p, n);
-        ao += occlude(a, fx, fy, c1x * 0.75f, c1y * 0.75f, p, n);
-        ao += occlude(a, fx, fy, c2x * 0.5f, c2y * 0.5f, p, n);
-        ao += occlude(a, fx, fy, c2x, c2y, p, n);
+        ao += occlude(a, fx, fy, c1x * 0.25f, c1y * 0.25f, rx, ry, p, n);
+        ao += occlude(a, fx, fy, c1x * 0.75f, c1y * 0.75f, rx, ry, p, n);
+        ao += occlude(a, fx, fy, c2x * 0.5f, c2y * 0.5f, rx, ry, p, n);
+        ao += occlude(a, fx, fy, c2x, c2y, rx, ry, p, n);
     }
     ao = ao / 16.0f;
     return quant(1.0f - ao);
@@ -222,7 +227,7 @@ extern "C" __global__ void __launch_bounds__(256) sf_post_final(PostArgs a)
 {
     uint32_t i, j;
     if (!pixel(a.W, a.H, i, j)) return;
-    const float u = ((float)i + 0.5f) / a.fw, v = ((float)j + 0.5f) / a.fh;
+    const float u = ((float)i + 0.5f) * (1.0f / a.fw), v = ((float)j + 0.5f) * (1.0f / a.fh);
     const uint32_t px = (uint32_t)nearest(v, a.fh, (int)a.H) * a.W + (uint32_t)nearest(u, a.fw, (int)a.W);
     const float4 p = ld4(a.pos, px);
     final_store(a, j * a.W + i, p, is_background(p) ? 0.0f : sample_u8(a.blur_v, a.W, a.H, a.fw, a.fh, u, v));

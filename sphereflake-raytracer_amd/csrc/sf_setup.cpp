@@ -307,18 +307,15 @@ void ssao_noise(float out[SF_NOISE_SIZE * SF_NOISE_SIZE * 4])
 
 // The final and blur passes sample their RGBA8 sources LINEAR at the fragment centre. In the
 // 8-bit-subtexel texture model (sf_post.hip) that is exactly the fragment's own texel iff the centre
-// coordinate snaps to an integer for every i < n in both shader forms: (i+0.5) * (1/n) * n - 0.5
-// (post_ssao_blur.glsl:26-29) and (i+0.5) / n * n - 0.5 (post_final.glsl:17). Then the blur passes
-// with no accepted tap reduce to a per-pixel weight, and the fused post kernel equals the multi-pass
-// one bit for bit.
+// coordinate (i+0.5) * (1/n) * n - 0.5 (post_ssao_blur.glsl:26-29, post_final.glsl:17) snaps to an
+// integer for every i < n. Then the blur passes with no accepted tap reduce to a per-pixel weight,
+// and the fused post kernel equals the multi-pass one bit for bit.
 bool post_centre_exact(uint32_t n)
 {
     const float fn = (float)n, ps = 1.0f / fn;
     for (uint32_t i = 0; i < n; ++i) {
         const float fc = (float)i + 0.5f;
-        const float a = std::rint((fc * ps * fn - 0.5f) * 256.0f);
-        const float b = std::rint((fc / fn * fn - 0.5f) * 256.0f);
-        if (a != 256.0f * (float)i || b != 256.0f * (float)i) return false;
+        if (std::rint((fc * ps * fn - 0.5f) * 256.0f) != 256.0f * (float)i) return false;
     }
     return true;
 }
