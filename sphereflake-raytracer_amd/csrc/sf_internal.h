@@ -13,19 +13,23 @@
 #define SF_DEPTH_TABLE 33      // depths 0..32 (SF_MAX_DEPTH_LIMIT)
 #define SF_TILE 8              // a wave64 traces one 8x8 pixel tile
 #define SF_WAVES_PER_BLOCK 4   // 256-thread workgroups (per-ray kernel)
+#ifndef SF_WAVES_PER_EU
+#define SF_WAVES_PER_EU 7      // occupancy target of the persistent trace kernels (waves per SIMD)
+#endif
 #ifndef SF_TRACE_WAVES
 #define SF_TRACE_WAVES 2       // independent waves per workgroup of the wave kernels
 #endif
 // Wave-coherent traversal LDS image, per wave (units: floats):
-//   [root: 16][(levels - 1) x (table 144 | E 32)]
+//   [root: 16][cone: 8][(levels - 1) x (table 144 | E 32)]
 // A transform is 16 floats: [cx cy cz cc | col0.xyz - | col1.xyz - | col2.xyz -] (cc = Dot(centre, centre)).
 #define SF_LDS_ROOT 16
+#define SF_LDS_CONE 8                     // the wave's ray cone {ax, ay, az, cosT, sinT, -, -, -}
 #define SF_LDS_CHILD 16
 #define SF_LDS_TABLE (9 * SF_LDS_CHILD)   // the 9 child transforms of the node open at a level
 #define SF_LDS_E 32                       // 64 lanes x u16: per-lane child-expand bits of that node
 #define SF_LDS_LEVEL (SF_LDS_TABLE + SF_LDS_E)
 // levels - 1 level images: the deepest provisioned level's table is never read (see traverse)
-#define SF_LDS_WAVE_FLOATS(levels) (SF_LDS_ROOT + ((levels) - 1) * SF_LDS_LEVEL)
+#define SF_LDS_WAVE_FLOATS(levels) (SF_LDS_ROOT + SF_LDS_CONE + ((levels) - 1) * SF_LDS_LEVEL)
 
 // Persistent-kernel tile queues: SF_QUEUES counters per render parity, one 128-byte line each, after
 // the two overflow counters (u32 words).
@@ -34,7 +38,8 @@
 #define SF_QUEUE_WORD(parity, k) (SF_QUEUE_STRIDE + ((parity) * SF_QUEUES + (k)) * SF_QUEUE_STRIDE)
 #define SF_COUNTER_WORDS (SF_QUEUE_STRIDE + 2u * SF_QUEUES * SF_QUEUE_STRIDE)
 
-#define SF_FLAG_NO_LOD_CULL 1u   // disable the per-child LOD reachability cull (A/B only; results identical)
+#define SF_FLAG_NO_LOD_CULL 1u    // disable the leaf-threshold skip (A/B only; results identical)
+#define SF_FLAG_NO_CONE_CULL 2u   // disable the per-child ray-cone cull (A/B only; results identical)
 
 struct DepthTables {
     float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)

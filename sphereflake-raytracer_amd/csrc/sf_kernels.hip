@@ -115,6 +115,15 @@ __device__ __forceinline__ void shade(float dx, float dy, float dz, const HitSta
     }
 }
 
+// max over the wave of a non-negative float (ordered as its bit pattern)
+__device__ __forceinline__ float wave_max_pos(float v)
+{
+    uint32_t b = __float_as_uint(v);
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, m, 64));
+    return __uint_as_float(__builtin_amdgcn_readfirstlane(b));
+}
+
 __device__ __forceinline__ float wave_min(float v)
 {
 #pragma unroll
@@ -172,10 +181,14 @@ __device__ __forceinline__ bool group_any(bool p)
 struct TraverseLds {
     float* base;
     __device__ __forceinline__ float* root() const { return base; }
-    __device__ __forceinline__ float* table(uint32_t lvl) const { return base + SF_LDS_ROOT + lvl * SF_LDS_LEVEL; }
+    __device__ __forceinline__ float* cone() const { return base + SF_LDS_ROOT; }
+    __device__ __forceinline__ float* table(uint32_t lvl) const
+    {
+        return base + SF_LDS_ROOT + SF_LDS_CONE + lvl * SF_LDS_LEVEL;
+    }
     __device__ __forceinline__ uint16_t* E(uint32_t lvl) const
     {
-        return reinterpret_cast<uint16_t*>(base + SF_LDS_ROOT + lvl * SF_LDS_LEVEL + SF_LDS_TABLE);
+        return reinterpret_cast<uint16_t*>(base + SF_LDS_ROOT + SF_LDS_CONE + lvl * SF_LDS_LEVEL + SF_LDS_TABLE);
     }
 };
 
@@ -305,6 +318,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
 {
     const uint32_t lane = threadIdx.x & 63u;
     const TraverseLds L{ Lbase };
+    const bool cone_cull = (K_flags & SF_FLAG_NO_CONE_CULL) == 0u;
     SF_STAMP_DECL;
 
     h.minT = FLT_MAX;
@@ -329,6 +343,28 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     if (!wave_ballot(ex0)) return;
     maxd = 0;
 
+    // ---- the wave's ray cone: axis = lane 36's direction (pixel (4, 4) of the tile), sinT bounds the
+    // sine of every lane's angle to it (|d x a| with |d|, |a| = 1 +- 2^-20, plus 2^-16 slack). A wide
+    // cone (scattered packets of the frame-less mode, or sinT >= 1/2) disables the child cone cull
+    // below through cosT = 0, sinT = 1.
+    // Kept in LDS (read with the node in expand): as uniform registers they would spill SGPRs.
+    {
+    const float ax = readlane_f(dx, 36u), ay = readlane_f(dy, 36u), az = readlane_f(dz, 36u);
+    float cosT = 0.0f, sinT = 1.0f;
+    if (cone_cull) {
+        const float cx_ = dy * az - dz * ay, cy_ = dz * ax - dx * az, cz_ = dx * ay - dy * ax;
+        const float s2 = (cx_ * cx_ + cy_ * cy_) + cz_ * cz_;
+        const bool fwd = (dx * ax + dy * ay) + dz * az > 0.0f;
+        const float s2m = fwd ? s2 : 1.0f;
+        const float sm = __builtin_amdgcn_sqrtf(wave_max_pos(s2m)) * (1.0f + 0x1p-16f) + 0x1p-16f;
+        if (sm < 0.5f) {
+            sinT = sm;
+            cosT = __builtin_amdgcn_sqrtf(1.0f - sm * sm) * (1.0f - 0x1p-16f);
+        }
+    }
+    if (lane < 5u) L.cone()[lane] = lane == 0u ? ax : lane == 1u ? ay : lane == 2u ? az : lane == 3u ? cosT : sinT;
+    }
+
     // This lane's column of the cooperative child build: column c = lane / 9, child i = lane % 9, so
     // lanes 27..35 hold the 9 child centres (read back by v_readlane, no LDS round trip) and one ballot
     // yields a per-child mask (bits 27..35).
@@ -348,6 +384,34 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     uint32_t cN = 0;                // uniform: its index in the parent's table
     uint32_t idxN = 0;              // uniform: its heap index mod 2^32 (root 0, child i of n: 9n+1+i)
 
+    // ---- the own sphere of a node (Sphereflake.h:174-224) with centre/|c|^2 `pc`, depth dd, heap index
+    // idx, tested when the node opens. The reference tests it after the children (post-order) and
+    // accepts strictly smaller t, so on an exact tie the earlier node in post-order wins. Pre-order
+    // differs from post-order only for ancestor/descendant pairs, hence: a tie is accepted iff the
+    // current best is an ancestor of this node (`anc`). Same result as the reference's order in every case.
+    auto self_test = [&](const float4 pc, uint32_t dd, bool act, uint32_t idx, float R2s) {
+        const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
+        const float d2 = pc.w - tca * tca;
+        const bool f0 = tca >= 0.0f, in = d2 <= R2s;
+        bool hs;
+        if constexpr (PACKET) hs = act && group_any<PACKET>(f0) && group_any<PACKET>(in);
+        else hs = act & f0 & in;
+        const uint64_t hsm = PACKET ? wave_ballot(hs) : (wave_ballot(act) & wave_ballot(f0) & wave_ballot(in));
+        if (hsm) {
+            const float ts = near_root(tca, d2, R2s);
+            // bitwise, not short-circuit: selects instead of divergent branches
+            const bool acc = hs & ((ts < h.minT) | ((ts == h.minT) & anc));
+            h.minT = acc ? ts : h.minT;
+            h.cx = acc ? pc.x : h.cx;
+            h.cy = acc ? pc.y : h.cy;
+            h.cz = acc ? pc.z : h.cz;
+            h.index = acc ? idx : h.index;
+            h.depth = acc ? (int32_t)dd : h.depth;
+            h.hit = h.hit | acc;
+            anc = anc | acc;
+        }
+    };
+
     // ---- expand the node at `node` (depth d, transform in LDS): build its 9 child transforms into
     // table(d), then test the children (depth d+1) for the lanes in `act`. Returns this lane's 9-bit
     // "child expands" vector; *pend = the wave's mask of children some lane expands.
@@ -360,39 +424,11 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         const float4 p2 = *reinterpret_cast<const float4*>(node + 12);
         const float4 dtn = depth_consts(K, d);        // this node: r^2, (4/3) r
         const float4 dtc = depth_consts(K, d + 1u);   // children: (2r)^2, T
-        // ---- the node's own sphere (Sphereflake.h:174-224), tested here, when the node opens, with
-        // the centre already in registers. The reference tests it after the children (post-order)
-        // and accepts strictly smaller t, so on an exact tie the earlier node in post-order wins.
-        // Pre-order differs from post-order only for ancestor/descendant pairs, hence: a tie is
-        // accepted iff the current best is an ancestor of this node (`anc`). Same result as the
-        // reference's order in every case.
-        {
-            const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
-            const float d2 = pc.w - tca * tca;
-            const float R2s = dtn.y;
-            const bool f0 = tca >= 0.0f, in = d2 <= R2s;
-            bool hs;
-            if constexpr (PACKET) hs = act && group_any<PACKET>(f0) && group_any<PACKET>(in);
-            else hs = act & f0 & in;
-            const uint64_t hsm = PACKET ? wave_ballot(hs) : (wave_ballot(act) & wave_ballot(f0) & wave_ballot(in));
-            if (hsm) {
-                const float ts = near_root(tca, d2, R2s);
-                const bool acc = hs && in && ((ts < h.minT) || ((ts == h.minT) && anc));
-                if (acc) {
-                    h.minT = ts;
-                    h.cx = pc.x;
-                    h.cy = pc.y;
-                    h.cz = pc.z;
-                    h.index = idxN;
-                    h.depth = (int32_t)d;
-                    h.hit = true;
-                }
-                anc = anc | acc;
-            }
-        }
+        self_test(pc, d, act, idxN, dtn.y);
         // No child of this node can pass the LOD test for any ray (sfhost::leaf_threshold): skip the
         // build and the child tests (per-ray semantics only, like the reachability cull below).
-        if (lod_cull) {
+        // (pushed nodes never qualify: leaf children are tested inline by the DFS loop; only the root)
+        if (lod_cull && d == 0u) {
             const float leaf = depth_leaf(K, d);
             if (__builtin_amdgcn_readfirstlane((int)(pc.w > leaf))) {
                 SF_COUNT(4, 1);
@@ -413,21 +449,24 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         if (d + 1u < levels) *reinterpret_cast<float4*>(L.table(d) + slot) = make_float4(x, y, z, w);
         const float R2b = dtc.x;
         const float T = dtc.w;
-        uint32_t M = 0x1ffu;
-        if (lod_cull) {
-            // LOD reachability of child bi (centre lanes 27..35): any lane's float t satisfies
-            // t >= sqrt(|c|^2 - R^2 - dl) - sqrt(R^2 + dl) (1 - O(2^-22)), dl = 2^-16 |c|^2 bounding
-            // the rounding of tca, d2 and the direction's length (SIMD_AVX.h:244-267). If that bound
-            // is >= T, i.e. |c|^2 - R^2 - dl > rhs^2, no lane can pass the LOD test
-            // (Sphereflake.h:146-153), so the child does nothing in the reference for any lane: skip
-            // it for the whole wave. The 2^-12 slack in rhs covers the rounding of this test itself
-            // (hardware sqrt, squares), so no correctly rounded operation is needed here.
-            const float dl = w * 0x1p-16f;
-            const float ra = (w - R2b) - dl;
-            const float rhs = (T + __builtin_amdgcn_sqrtf(R2b + dl)) * (1.0f + 0x1p-12f);
-            const uint64_t skip = wave_ballot(ra > 0.0f) & wave_ballot(ra > rhs * rhs);
-            M = (uint32_t)(~skip >> 27) & 0x1ffu;
-        }
+        // Cone cull of child bi (centre c in lanes 27..35): no ray of the wave's cone can hit its bounding
+        // sphere. With ca = c.a, q = c - ca a, every lane's angle phi to c is >= alpha - theta, so its
+        // line passes at distance |c| sin(phi) >= |q| cosT - ca sinT from c. A float hit
+        // (tca >= 0, cc - tca^2 <= R^2, SIMD_AVX.h:247-258) needs |c| sin(phi) <= sqrt(R^2 + dl),
+        // dl = 2^-18 |c|^2 covering the rounding of tca, d2, |c|^2 and |d| (~12 ulp + 2^-21); the last
+        // terms cover this test's own rounding (hardware sqrt). With beta < 45 deg and theta < 30 deg
+        // every lane's phi stays in [beta, 180 - beta], which also covers the 8-lane packet tests.
+        // Such a child changes nothing for any lane in the reference: skip it for the whole wave.
+        const float4 cn = *reinterpret_cast<const float4*>(L.cone());
+        const float ax = cn.x, ay = cn.y, az = cn.z, cosT = cn.w, sinT = L.cone()[4];
+        const float dl = w * 0x1p-18f;
+        const float ca = (x * ax + y * ay) + z * az;
+        const float qx = x - ca * ax, qy = y - ca * ay, qz = z - ca * az;
+        const float sq = __builtin_amdgcn_sqrtf((qx * qx + qy * qy) + qz * qz);
+        const float lhs = sq * cosT - ca * sinT;
+        const float rhs = __builtin_amdgcn_sqrtf(R2b + dl) * (1.0f + 0x1p-18f) + (ca + sq) * 0x1p-18f;
+        const uint64_t skip = wave_ballot(ca > 0.0f) & wave_ballot(w > 2.0f * (R2b + dl)) & wave_ballot(lhs > rhs);
+        uint32_t M = (uint32_t)(~skip >> 27) & 0x1ffu;
         M = __builtin_amdgcn_readfirstlane(M);
         SF_STAMP(6);
         uint32_t e = 0, pm = 0;
@@ -525,12 +564,25 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 overflowed = true;
                 continue;
             }
+            const bool a = ((eN >> c) & 1u) != 0u;
+            const float* node = L.table(d) + c * SF_LDS_CHILD;
+            if (lod_cull) {
+                // A child none of whose children can pass LOD for any ray (sfhost::leaf_threshold) only
+                // needs its own sphere: test it here, in its DFS turn, without a push or a level.
+                lds_fence();
+                const float4 pc = *reinterpret_cast<const float4*>(node);
+                if (__builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, d + 1u)))) {
+                    SF_COUNT(4, 1);
+                    maxd = (int32_t)d + 1 > maxd ? (int32_t)d + 1 : maxd;   // Sphereflake.h:157-160
+                    self_test(pc, d + 1u, a, 9u * idxN + 1u + c, depth_consts(K, d + 1u).y);
+                    anc = anc & (h.depth != (int32_t)d + 1);   // the child is finished
+                    continue;
+                }
+            }
             // save the open node's state, enter child c
             stk_pc = writelane_u(pend | (cN << 16), d, stk_pc);
             stk_ix = writelane_u(idxN, d, stk_ix);
             L.E(d)[lane] = (uint16_t)eN;
-            const bool a = ((eN >> c) & 1u) != 0u;
-            const float* node = L.table(d) + c * SF_LDS_CHILD;
             idxN = 9u * idxN + 1u + c;
             cN = c;
             d += 1u;
@@ -811,15 +863,15 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
     publish_stats(a, maxd, closest, 0u);
 }
 
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_trace_queue1(FrameArgs a)
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue1(FrameArgs a)
 {
     trace_queue_body<1>(a);
 }
-extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_trace_queue2(FrameArgs a)
+extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue2(FrameArgs a)
 {
     trace_queue_body<2>(a);
 }
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_trace_queue4(FrameArgs a)
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue4(FrameArgs a)
 {
     trace_queue_body<4>(a);
 }
