@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--K", type=float, default=K)
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the post-process and transfer sections (profiling runs of the timed loop only)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--check", action="store_true", help="verify the frame against the oracle rows")
     return ap.parse_args()
@@ -66,6 +68,23 @@ def frame_camera(width, height, k, frame):
 
 
 CPU_REPS = 40                        # ~1.2 s wall x 16 threads: ~20 s of CPU work
+
+
+def pmc_valu(kernel, cus=256):
+    """VALU issue of `kernel` from the committed PMC summary: wave-level VALU instructions per launch
+    against the VALU issue slots of the profiled dispatch (CUs x 4 SIMDs x cycles / 2: one wave64
+    VALU instruction issues over 2 cycles; cycles = GRBM_GUI_ACTIVE / 8 XCDs)."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            c = json.load(f)["kernels"][kernel]
+        cycles = c["GRBM_GUI_ACTIVE"] / 8.0
+        slots = cus * 4 * cycles / 2.0
+        return {"valu_insts": round(c["SQ_INSTS_VALU"]), "salu_insts": round(c["SQ_INSTS_SALU"]),
+                "issue_slots": round(slots), "valu_issue_frac": round(c["SQ_INSTS_VALU"] / slots, 4),
+                "clock_mhz": round(cycles / c["profiled_dispatch_us"], 1), "source": "profiles/pmc_traffic.json"}
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None
 
 
 def pmc_traffic(kernel):
@@ -89,10 +108,13 @@ def cpu_baseline(width, height, k, threads):
     ref = os.path.join(pyoracle.REF_DIR, "ref_bench")
     if os.path.exists(ref):
         r = pyoracle.ref_bench(width, height, k, threads, CPU_REPS)
+        r1 = pyoracle.ref_bench(width, height, k, 1, 3)   # also one thread
         return {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
                 "sample": f"{CPU_REPS} full {width}x{height} K={k} frames (reference 8-ray packet footprint, 8/9 "
                           f"pixel coverage), median; reference AVX path -O3 -mavx, {threads} threads",
-                "frame_ms": round(r["median_s"] * 1e3, 2)}
+                "frame_ms": round(r["median_s"] * 1e3, 2),
+                "single_thread": {"value": round(r1["mrays_per_s"], 3), "frame_ms": round(r1["median_s"] * 1e3, 1),
+                                  "sample": "3 full frames, 1 thread"}}
     setup = {"W": width, "H": height}
     cam = sf.config_camera(width, height, k)
     o, tl, tr, bl = cam.corners()
@@ -312,12 +334,12 @@ def main():
 
     # SSAO post-process of the rendered G-buffer, timed alone on the render stream
     post = None
-    if rank == 0 and args.mode == "frames":
+    if rank == 0 and args.mode == "frames" and not args.no_extras:
         post = post_rates(ctx, torch, stream, width, height)
 
     # D2H into the host GBuffer (PCIe-inclusive, reported separately -- never `value`)
     d2h = None
-    if rank == 0 and args.mode == "frames":
+    if rank == 0 and args.mode == "frames" and not args.no_extras:
         d2h = transfer_rates(ctx, torch, dev, stream, width, height, kernel)
 
     check = None
@@ -361,9 +383,11 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": round(traffic) if traffic else None,
                          "kernel": TRACE_KERNEL, "kernel_ms": round(trace_ms, 4),
-                         "note": "path is VALU-bound (SURVEY.md §8(d)); achieved = 32 B/ray x rays per launch / mean "
-                                 "duration of the trace kernel (HIP events around it on its launch stream); traffic = "
-                                 "PMC WRITE_SIZE + 2 x FETCH_SIZE per launch from " + str(traffic_src)},
+                         "note": "path is VALU/latency-bound (SURVEY.md §8(d), see `valu`); achieved = 32 B/ray x "
+                                 "rays per launch / mean duration of the trace kernel (HIP events around it on its "
+                                 "launch stream); traffic = PMC WRITE_SIZE + 2 x FETCH_SIZE per launch "
+                                 "(profiles/pmc_traffic.json)"},
+            "valu": pmc_valu(TRACE_KERNEL),
         }
         if check is not None:
             out["check_rows_bit_exact"] = check

@@ -35,5 +35,6 @@ for k, cs in acc.items():
         print(f"   {c:28s} {means[k][c]:16.1f}")
 if out_json:
     with open(out_json, "w") as f:
-        json.dump({"source": "rocprofv3 --pmc passes of scripts/prof_pmc.sh (" + ", ".join(args) + "); "
+        rel = sorted({os.path.relpath(d, os.getcwd()) for d in args})
+        json.dump({"source": "rocprofv3 --pmc passes of scripts/prof_pmc.sh (" + ", ".join(rel) + "); "
                              "FETCH_SIZE/WRITE_SIZE in KB per dispatch", "kernels": means}, f, indent=1)
