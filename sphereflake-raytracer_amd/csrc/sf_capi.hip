@@ -89,6 +89,7 @@ struct sf_ctx {
     int cus = 256;
     int occ_key = -1, occ_blocks = 0;            // cached occupancy (waves per block, levels) -> blocks per CU
     uint32_t max_blocks = 0;                     // diagnostics: env SF_MAX_BLOCKS caps the persistent grid
+    uint32_t prio_tiles = 2048;                  // tuning knob: env SF_PRIO_TILES (heaviest order positions at s_setprio 3)
     // frame-less progressive mode
     uint32_t* mt_state = nullptr;      // 624 words + next index (std::mt19937 layout)
     uint32_t* draws = nullptr;         // 2 per packet
@@ -252,6 +253,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if (const char* ev = std::getenv("SF_ORDER")) c->use_order = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_FLAGS")) c->flags = (uint32_t)std::strtoul(ev, nullptr, 0);
+    if (const char* ev = std::getenv("SF_PRIO_TILES")) c->prio_tiles = (uint32_t)std::strtoul(ev, nullptr, 0);
     if (const char* ev = std::getenv("SF_TRACE_WAVES")) {
         const int w = std::atoi(ev);
         c->waves_per_block = (w == 1 || w == 2 || w == 4) ? (uint32_t)w : SF_TRACE_WAVES;
@@ -474,6 +476,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 a.tile_cost = c->tile_cost;
                 a.chunk_cnt = c->chunk_cnt;
                 a.tile_order = (c->order_n == ntiles && c->order_stream == s) ? c->tile_order : nullptr;
+                a.prio_tiles = c->prio_tiles;
             }
             if (c->timing) SF_HIP(c, hipEventRecord(c->ev[c->ev_next][0], s));
             if (wpb == 1) hipLaunchKernelGGL(sf_trace_queue1, grid, block, lds, s, a);

@@ -94,6 +94,7 @@ struct FrameArgs {
     uint32_t* tile_cost;              // out (NULL = off): per tile, shader cycles of its traversal
     const uint32_t* tile_order;       // in (NULL = row-major): tile permutation, heaviest first
     uint32_t* chunk_cnt;              // out (with tile_cost): per 64-tile chunk, cost-bucket histogram
+    uint32_t prio_tiles;              // order positions traced at raised wave priority (s_setprio)
 };
 
 // Headless SSAO post-process (Shaders/post_ssao.glsl, post_ssao_blur.glsl,

@@ -856,7 +856,11 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
             t = at.tile_order[g];
 #endif
         }
+        // the heaviest tiles of the previous render bound the frame: give their waves issue priority
+        const bool prio = at.tile_order && g < at.prio_tiles;
+        if (prio) __builtin_amdgcn_s_setprio(3);
         const TileStats st = trace_tile<false>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity);
+        if (prio) __builtin_amdgcn_s_setprio(0);
         maxd = st.maxd > maxd ? st.maxd : maxd;
         closest = fminf(closest, st.closest);
     }
