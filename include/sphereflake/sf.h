@@ -139,6 +139,18 @@ int sf_download_async(sf_ctx* ctx, float* pos4, float* nrm4, float* min_t, uint3
 int sf_host_register(void* ptr, size_t bytes);
 int sf_host_unregister(void* ptr);
 
+/* --- reference variant ----------------------------------- */
+/* The reference compiles one of two SIMD paths (Sphereflake.cpp:29-33): AVX (SIMD_AVX.h: LOD constant
+   70, 8-lane packets, 8-pixel frame-less footprint) or, with __ARCH_NO_AVX (its Linux CMake build),
+   SSE (SIMD_SSE.h: LOD constant 60, 4-lane packets, 2x2 footprint, Sphereflake.cpp:115-138). A context
+   reproduces either bit for bit; default AVX. Synchronous; later renders use the chosen variant. */
+#define SF_VARIANT_AVX 0
+#define SF_VARIANT_SSE 1
+int sf_set_variant(sf_ctx* ctx, int variant);
+int sf_get_variant(const sf_ctx* ctx);   /* SF_VARIANT_* or SF_EINVAL */
+/* Exact threshold T: sqrtf(t / r) < lod_constant || t < 0  <=>  t < T (Sphereflake.h:129,146). Host only. */
+int sf_lod_threshold(float r, float lod_constant, float* T);
+
 /* --- SSAO post-process ---------------------------------- */
 /* The reference's GL passes over the G-buffer (SSAO.cpp:106-142: SSAO, blur x, blur y;
    main.cpp:312-330: final composite), run headless as HIP kernels. Output: RGBA8 image, W*H*4

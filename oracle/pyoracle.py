@@ -80,10 +80,14 @@ def _fp(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
 
 
-def render(setup: dict, rows=None, threads: int | None = None, lut: np.ndarray | None = None) -> dict:
+def render(setup: dict, rows=None, threads: int | None = None, lut: np.ndarray | None = None,
+           lod: float = 70.0) -> dict:
     """Per-ray oracle frame for the given rows (default: all). Returns numpy arrays
-    pos4/nrm4 [n, W, 4] f32, minT [n, W] f32, index [n, W] u32, depth [n, W] i8, stats."""
+    pos4/nrm4 [n, W, 4] f32, minT [n, W] f32, index [n, W] u32, depth [n, W] i8, stats.
+    lod: the LOD constant, 70 (AVX path, default) or 60 (SSE path, SIMD_SSE.h:21)."""
     L = lib()
+    L.sfo_set_lod_constant.argtypes = [ctypes.c_float]
+    L.sfo_set_lod_constant(ctypes.c_float(lod))
     W, H = int(setup["W"]), int(setup["H"])
     rows = np.arange(H) if rows is None else np.asarray(rows)
     n = len(rows)
@@ -133,12 +137,14 @@ def ref_available() -> bool:
     return os.path.exists(os.path.join(REF_DIR, "ref_harness"))
 
 
-def ref_render(W: int, H: int, K: float, row_step: int = 1, threads: int = 8, tmp: str = "/tmp") -> dict:
-    """Run the reference itself (oracle/_ref/ref_harness, built from /root/reference).
-    Returns pos/nrm (xyz) and minT for rows y % row_step == 0 plus its JSON stats."""
-    path = os.path.join(tmp, f"sf_ref_{W}x{H}_{K}_{row_step}_{os.getpid()}.bin")
-    out = subprocess.check_output([os.path.join(REF_DIR, "ref_harness"), "render", str(W), str(H),
-                                   repr(K), path, str(threads), str(row_step)])
+def ref_render(W: int, H: int, K: float, row_step: int = 1, threads: int = 8, tmp: str = "/tmp",
+               sse: bool = False) -> dict:
+    """Run the reference itself (oracle/_ref/ref_harness, built from /root/reference; ref_harness_sse:
+    the same sources built with __ARCH_NO_AVX). Returns pos/nrm (xyz) and minT for rows
+    y % row_step == 0 plus its JSON stats."""
+    path = os.path.join(tmp, f"sf_ref_{W}x{H}_{K}_{row_step}_{int(sse)}_{os.getpid()}.bin")
+    out = subprocess.check_output([os.path.join(REF_DIR, "ref_harness_sse" if sse else "ref_harness"), "render",
+                                   str(W), str(H), repr(K), path, str(threads), str(row_step)])
     stats = json.loads(out)
     n = (H + row_step - 1) // row_step
     a = np.fromfile(path, dtype=np.float32).reshape(n, W, 7)

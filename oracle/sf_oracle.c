@@ -101,6 +101,11 @@ typedef struct {
     int depth;
 } hit_t;
 
+/* LOD constant of the predicate sqrtf(t / r) < C: 70 in the AVX path (SIMD_AVX.h:25, Sphereflake.h:146),
+   60 in the SSE path (SIMD_SSE.h:21, Sphereflake.h:129). Set before rendering (sfo_set_lod_constant). */
+static float g_lod_constant = 70.0f;
+void sfo_set_lod_constant(float c) { g_lod_constant = c; }
+
 /* Sphereflake::IntersectSphereflake, Sphereflake.h:86-226 (per ray). */
 static void intersect(trav_t* tv, const float D[3], const float* parent, hit_t* h,
                       float parentRadius, int depth, uint64_t node)
@@ -112,7 +117,7 @@ static void intersect(trav_t* tv, const float D[3], const float* parent, hit_t* 
     float t;
     tv->nodes++;
     if (!ray_sphere(D, C, R2b, &t)) return;                       /* :119, :140-144 */
-    if (!(sqrtf(t / r) < 70.0f || t < 0.0f)) return;             /* :146-153 */
+    if (!(sqrtf(t / r) < g_lod_constant || t < 0.0f)) return;    /* :146-153 (SSE :129-136) */
     if (depth > tv->max_depth) tv->max_depth = depth;             /* :157-160 */
     tv->interior++;
     float scale = (4.0f / 3.0f) * r;                              /* :162 */

@@ -1,3 +1,8 @@
 set -e
-T=${1:-v30}
-scripts/sweep.sh ${T}sw "SF_PRIO_TILES=0" "SF_PRIO_TILES=128" "SF_PRIO_TILES=512" "SF_PRIO_TILES=2048" "SF_PRIO_TILES=8192" "SF_PRIO_TILES=0"
+T=${1:-v31}
+mkdir -p gpurun_out/$T
+timeout -k 10 90 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$T/smoke.log 2>&1 || { tail -5 gpurun_out/$T/smoke.log; exit 1; }
+tail -1 gpurun_out/$T/smoke.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/$T/pytest.log 2>&1 || { tail -30 gpurun_out/$T/pytest.log; exit 1; }
+tail -2 gpurun_out/$T/pytest.log
+scripts/sweep.sh ${T}sw "SF_FLAGS=0"

@@ -35,6 +35,9 @@ extern "C" __global__ void sf_post_fused(PostArgs a);
 extern "C" __global__ void sf_mt_draws(uint32_t* state, uint32_t* out, uint32_t n);
 extern "C" __global__ void sf_progressive_trace(FrameArgs a, const uint32_t* draws, uint64_t counter0, uint32_t packets,
                                                 uint64_t ticket0, PacketLane* lanes, unsigned long long* owner);
+extern "C" __global__ void sf_progressive_trace_sse(FrameArgs a, const uint32_t* draws, uint64_t counter0,
+                                                    uint32_t packets, uint64_t ticket0, PacketLane* lanes,
+                                                    unsigned long long* owner);
 extern "C" __global__ void sf_progressive_scatter(FrameArgs a, uint32_t packets, uint64_t ticket0,
                                                   const PacketLane* lanes, const unsigned long long* owner);
 
@@ -89,6 +92,7 @@ struct sf_ctx {
     int cus = 256;
     int occ_key = -1, occ_blocks = 0;            // cached occupancy (waves per block, levels) -> blocks per CU
     uint32_t max_blocks = 0;                     // diagnostics: env SF_MAX_BLOCKS caps the persistent grid
+    int variant = SF_VARIANT_AVX;                // reference path reproduced (sf_set_variant)
     uint32_t prio_tiles = 2048;                  // tuning knob: env SF_PRIO_TILES (heaviest order positions at s_setprio 3)
     // frame-less progressive mode
     uint32_t* mt_state = nullptr;      // 624 words + next index (std::mt19937 layout)
@@ -177,7 +181,7 @@ static void free_ctx(sf_ctx* c)
 static int upload_consts(sf_ctx* c)
 {
     std::memcpy(c->host_consts.child, c->child, sizeof c->child);
-    sfhost::depth_tables(&c->host_consts.dt);
+    sfhost::depth_tables(&c->host_consts.dt, c->variant == SF_VARIANT_SSE ? 60.0f : 70.0f);
     for (int d = 0; d < SF_DEPTH_TABLE; ++d) {
         float* e = c->host_consts.depth8[d];
         e[0] = c->host_consts.dt.r2_bound[d];
@@ -544,7 +548,10 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
 {
     if (!c) return SF_EINVAL;
     if (!c->has_view) return SF_ENOVIEW;
-    if (c->W < 3 || c->H < 3) return SF_EINVAL;   // the reference samples x0 in [1, W-2]
+    const bool sse = c->variant == SF_VARIANT_SSE;
+    const uint32_t pl = sse ? 4u : 8u;             // packet lanes (SIMD_SSE.h / SIMD_AVX.h)
+    // the AVX worker samples x0 in [1, W-2], the SSE worker x0 in [0, W-2] (Sphereflake.cpp:117-118, 140-141)
+    if (sse ? (c->W < 2 || c->H < 2) : (c->W < 3 || c->H < 3)) return SF_EINVAL;
     if (packets == 0) return SF_OK;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     DevGuard g(c->device);
@@ -584,19 +591,25 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     a.nrm = c->nrm;
     a.min_t = c->min_t;
     a.emit_aux = 1;
+    a.packet_lanes = pl;
     hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(1024), 0, s, c->mt_state, c->draws, 2 * packets);
     SF_HIP(c, hipGetLastError());
-    const uint32_t waves = (packets + 7) / 8;
+    const uint32_t ppw = 64u / pl;                   // packets per wave
+    const uint32_t waves = (packets + ppw - 1) / ppw;
     const size_t lds = (size_t)SF_LDS_WAVE_FLOATS(16) * 4;
-    hipLaunchKernelGGL(sf_progressive_trace, dim3(waves), dim3(64), lds, s, a, (const uint32_t*)c->draws, counter0,
-                       packets, c->ticket, c->lanes, c->owner);
+    if (sse)
+        hipLaunchKernelGGL(sf_progressive_trace_sse, dim3(waves), dim3(64), lds, s, a, (const uint32_t*)c->draws,
+                           counter0, packets, c->ticket, c->lanes, c->owner);
+    else
+        hipLaunchKernelGGL(sf_progressive_trace, dim3(waves), dim3(64), lds, s, a, (const uint32_t*)c->draws,
+                           counter0, packets, c->ticket, c->lanes, c->owner);
     SF_HIP(c, hipGetLastError());
-    hipLaunchKernelGGL(sf_progressive_scatter, dim3((packets * 8 + 255) / 256), dim3(256), 0, s, a, packets, c->ticket,
+    hipLaunchKernelGGL(sf_progressive_scatter, dim3((packets * pl + 255) / 256), dim3(256), 0, s, a, packets, c->ticket,
                        (const PacketLane*)c->lanes, (const unsigned long long*)c->owner);
     SF_HIP(c, hipGetLastError());
     c->ticket += packets;
     c->prog_next = counter0 + packets;
-    c->rays += 8 * (int64_t)packets;                 // m_RaysPerSecond += 8 (Sphereflake.cpp:184)
+    c->rays += (int64_t)pl * packets;                // m_RaysPerSecond += 8 / 4 (Sphereflake.cpp:184-186)
     return SF_OK;
 }
 
@@ -758,6 +771,20 @@ int sf_download_image(sf_ctx* c, uint8_t* rgba)
     return SF_OK;
 }
 
+int sf_set_variant(sf_ctx* c, int variant)
+{
+    if (!c || (variant != SF_VARIANT_AVX && variant != SF_VARIANT_SSE)) return SF_EINVAL;
+    if (variant == c->variant) return SF_OK;
+    DevGuard g(c->device);
+    SF_HIP(c, hipStreamSynchronize(c->stream));
+    c->variant = variant;
+    c->order_n = 0;       // tile costs of the other variant's frames: start over
+    *c->h_depth = -1;     // level hint likewise
+    return upload_consts(c);
+}
+
+int sf_get_variant(const sf_ctx* c) { return c ? c->variant : SF_EINVAL; }
+
 int sf_set_tile_trace(sf_ctx* c, int enable)
 {
     if (!c) return SF_EINVAL;
@@ -880,6 +907,13 @@ int sf_root_transform(const float origin[3], float root[16])
 {
     if (!origin || !root) return SF_EINVAL;
     sfhost::root_transform(origin, root);
+    return SF_OK;
+}
+
+int sf_lod_threshold(float r, float lod_constant, float* T)
+{
+    if (!T || !(r > 0.0f) || !(lod_constant > 0.0f)) return SF_EINVAL;
+    *T = sfhost::lod_threshold(r, lod_constant);
     return SF_OK;
 }
 

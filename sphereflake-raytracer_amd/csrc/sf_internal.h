@@ -94,6 +94,7 @@ struct FrameArgs {
     uint32_t* tile_cost;              // out (NULL = off): per tile, shader cycles of its traversal
     const uint32_t* tile_order;       // in (NULL = row-major): tile permutation, heaviest first
     uint32_t* chunk_cnt;              // out (with tile_cost): per 64-tile chunk, cost-bucket histogram
+    uint32_t packet_lanes;            // frame-less mode: 8 (AVX variant) or 4 (SSE variant, 2x2 footprint)
     uint32_t prio_tiles;              // order positions traced at raised wave priority (s_setprio)
 };
 
@@ -126,8 +127,8 @@ void root_transform(const float origin[3], float root[16]);
 void camera_corners(uint32_t W, uint32_t H, const float pos[3], float pitch, float yaw, float roll,
                     float fov, float o[3], float tl[3], float tr[3], float bl[3]);
 float radius(uint32_t depth);
-float lod_threshold(float r);
-void depth_tables(DepthTables* t);
+float lod_threshold(float r, float lod_constant = 70.0f);
+void depth_tables(DepthTables* t, float lod_constant = 70.0f);
 float leaf_threshold(const DepthTables* t, uint32_t depth);
 void sobol_matrices(uint32_t out[2][52]);
 void mt19937_seed(uint32_t seed, uint32_t state[625]);

@@ -141,14 +141,15 @@ __device__ __attribute__((noinline)) float near_root_exact(float tca, float d2, 
     return near_root(tca, d2, R2);
 }
 
-// "Any lane of my group": a group is the lane itself (per-ray semantics) or the 8 lanes of a
-// reference AVX packet (packet semantics: movemask early-outs, SIMD_AVX.h:247,255, Sphereflake.h:140,149,207).
-template <bool PACKET>
+// "Any lane of my group": a group is the lane itself (PW = 0, per-ray semantics) or the PW lanes of a
+// reference packet (packet semantics: movemask early-outs, SIMD_AVX.h:247,255, Sphereflake.h:140,149,207;
+// PW = 8 for the AVX path, 4 for the SSE path, SIMD_SSE.h).
+template <int PW>
 __device__ __forceinline__ bool group_any(bool p)
 {
-    if constexpr (PACKET) {
+    if constexpr (PW != 0) {
         const uint64_t b = wave_ballot(p);
-        return ((b >> (threadIdx.x & 56u)) & 0xffull) != 0ull;
+        return ((b >> (threadIdx.x & (64u - PW))) & ((1ull << PW) - 1ull)) != 0ull;
     } else {
         return p;
     }
@@ -310,12 +311,13 @@ __device__ __forceinline__ void stage_root(float* __restrict__ Lbase, const floa
     }
 }
 
-template <bool PACKET>
+template <int PW>   // packet width of the semantics: 0 per ray, 8 (AVX) or 4 (SSE) frame-less packets
 __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ Lbase,
                                          uint32_t levels, float dx, float dy, float dz, bool valid, HitState& h,
                                          int32_t& maxd, bool& overflowed, uint32_t K_flags,
                                          uint64_t* phase_sums = nullptr)
 {
+    constexpr bool PACKET = PW != 0;
     const uint32_t lane = threadIdx.x & 63u;
     const TraverseLds L{ Lbase };
     const bool cone_cull = (K_flags & SF_FLAG_NO_CONE_CULL) == 0u;
@@ -337,8 +339,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         const float4 dt0 = depth_consts(K, 0u);
         const float tca = (rcx * dx + rcy * dy) + rcz * dz;
         const float d2 = rcc - tca * tca;
-        const bool hb = valid && group_any<PACKET>(tca >= 0.0f) && group_any<PACKET>(d2 <= dt0.x);
-        ex0 = hb && group_any<PACKET>(near_root(tca, d2, dt0.x) < dt0.w);
+        const bool hb = valid && group_any<PW>(tca >= 0.0f) && group_any<PW>(d2 <= dt0.x);
+        ex0 = hb && group_any<PW>(near_root(tca, d2, dt0.x) < dt0.w);
     }
     if (!wave_ballot(ex0)) return;
     maxd = 0;
@@ -394,7 +396,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         const float d2 = pc.w - tca * tca;
         const bool f0 = tca >= 0.0f, in = d2 <= R2s;
         bool hs;
-        if constexpr (PACKET) hs = act && group_any<PACKET>(f0) && group_any<PACKET>(in);
+        if constexpr (PACKET) hs = act && group_any<PW>(f0) && group_any<PW>(in);
         else hs = act & f0 & in;
         const uint64_t hsm = PACKET ? wave_ballot(hs) : (wave_ballot(act) & wave_ballot(f0) & wave_ballot(in));
         if (hsm) {
@@ -525,7 +527,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 const float cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
                 const float tca = (cx * dx + cy * dy) + cz * dz;
                 const float d2 = cc - tca * tca;
-                const bool hb = act & group_any<PACKET>(tca >= 0.0f) & group_any<PACKET>(d2 <= R2b);
+                const bool hb = act & group_any<PW>(tca >= 0.0f) & group_any<PW>(d2 <= R2b);
                 if (wave_ballot(hb)) {
                     const float xs = R2b - d2;
                     const float sq = __builtin_amdgcn_sqrtf(xs);
@@ -536,7 +538,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                     float t_dec = t_hi < T ? t_hi : t_lo;    // on the same side of T as t when decided
                     const bool undecided = hb & ((!(t_hi < T) & !(t_lo >= T)) | (xs < 0x1p-96f));
                     if (wave_ballot(undecided)) t_dec = undecided ? near_root_exact(tca, d2, R2b) : t_dec;
-                    const bool exi = hb & group_any<PACKET>(t_dec < T);
+                    const bool exi = hb & group_any<PW>(t_dec < T);
                     const uint64_t mi = wave_ballot(exi);
                     e |= exi ? (1u << i) : 0u;
                     pm |= (mi != 0ull ? 1u : 0u) << i;
@@ -717,7 +719,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     HitState h;
     int32_t maxd = -1;
     bool overflowed = false;
-    traverse<false>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed, a.flags,
+    traverse<0>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed, a.flags,
                     FIXUP ? nullptr : a.phase_sums);
     if (!FIXUP && a.tile_trace) {
         // diagnostics only: never read by the kernel, never feeds an output value. Every lane stores
@@ -1155,27 +1157,45 @@ __device__ __forceinline__ float sobol_sample(uint64_t index, const uint32_t* __
 // the footprint of Sphereflake.cpp:143-147 around (x0, y0) drawn at Sobol index counter0 + j with
 // scrambles draws[2j], draws[2j+1] (Sphereflake.cpp:139-141). Results are staged per lane; the
 // owner word of each pixel keeps the highest ticket, so the scatter reproduces sequential order.
-extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace(FrameArgs a, const uint32_t* draws,
-                                                                       uint64_t counter0, uint32_t packets,
-                                                                       uint64_t ticket0, PacketLane* lanes,
-                                                                       unsigned long long* owner)
+// One wave = 64 / PW packets of PW lanes (Sphereflake.cpp:115-160): the AVX footprint is 8 pixels
+// around (x0, y0) = 1 + floor(S (W - 2)), 1 + floor(S (H - 2)); the SSE footprint the 2x2 block at
+// (x0, y0) = floor(S (W - 1)), floor(S (H - 1)).
+template <int PW>
+__device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint32_t* draws, uint64_t counter0,
+                                                  uint32_t packets, uint64_t ticket0, PacketLane* lanes,
+                                                  unsigned long long* owner)
 {
     extern __shared__ float lds[];
+    constexpr uint32_t PPW = 64u / PW;   // packets per wave
     const DeviceConsts* __restrict__ K = a.consts;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t packet = blockIdx.x * 8u + (lane >> 3);
-    if (blockIdx.x * 8u >= packets) return;   // wave-uniform
+    const uint32_t packet = blockIdx.x * PPW + lane / PW;
+    if (blockIdx.x * PPW >= packets) return;   // wave-uniform
     const bool valid = packet < packets;
-    const uint32_t q = lane & 7u;
+    const uint32_t q = lane % PW;
     float x0 = 0.f, y0 = 0.f;
     if (valid) {
         const uint64_t c = counter0 + packet;
-        x0 = 1.0f + floorf(sobol_sample(c, K->sobol[0], draws[2u * packet]) * (float)(a.W - 2u));
-        y0 = 1.0f + floorf(sobol_sample(c, K->sobol[1], draws[2u * packet + 1u]) * (float)(a.H - 2u));
+        const float s0 = sobol_sample(c, K->sobol[0], draws[2u * packet]);
+        const float s1 = sobol_sample(c, K->sobol[1], draws[2u * packet + 1u]);
+        if constexpr (PW == 8) {
+            x0 = 1.0f + floorf(s0 * (float)(a.W - 2u));
+            y0 = 1.0f + floorf(s1 * (float)(a.H - 2u));
+        } else {
+            x0 = floorf(s0 * (float)(a.W - 1u));
+            y0 = floorf(s1 * (float)(a.H - 1u));
+        }
     }
-    // footprint: xa = {x0, x0+1, x0+1, x0, x0, x0+1, x0-1, x0-1}, ya = {y0, y0+1, y0, y0+1, y0-1, y0-1, y0, y0-1}
-    const float ox = (q == 1u || q == 2u || q == 5u) ? 1.0f : (q >= 6u ? -1.0f : 0.0f);
-    const float oy = (q == 1u || q == 3u) ? 1.0f : ((q == 4u || q == 5u || q == 7u) ? -1.0f : 0.0f);
+    float ox, oy;
+    if constexpr (PW == 8) {
+        // xa = {x0, x0+1, x0+1, x0, x0, x0+1, x0-1, x0-1}, ya = {y0, y0+1, y0, y0+1, y0-1, y0-1, y0, y0-1}
+        ox = (q == 1u || q == 2u || q == 5u) ? 1.0f : (q >= 6u ? -1.0f : 0.0f);
+        oy = (q == 1u || q == 3u) ? 1.0f : ((q == 4u || q == 5u || q == 7u) ? -1.0f : 0.0f);
+    } else {
+        // xa = {x0, x0+1, x0, x0+1}, ya = {y0, y0, y0+1, y0+1}
+        ox = (q & 1u) ? 1.0f : 0.0f;
+        oy = (q & 2u) ? 1.0f : 0.0f;
+    }
     const float xf = x0 + ox, yf = y0 + oy;
     float dx, dy, dz;
     ray_dir(a, xf, yf, dx, dy, dz, K->lut);
@@ -1184,7 +1204,7 @@ extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace(FrameArgs 
     int32_t maxd = -1;
     bool overflowed = false;
     stage_root(lds, a.root);
-    traverse<true>(K, a.root, lds, SF_PROGRESSIVE_LEVELS, dx, dy, dz, valid, h, maxd, overflowed, a.flags);
+    traverse<PW>(K, a.root, lds, SF_PROGRESSIVE_LEVELS, dx, dy, dz, valid, h, maxd, overflowed, a.flags);
 
     PacketLane out;
     shade(dx, dy, dz, h, K->lut, out.px, out.py, out.pz, out.nx, out.ny, out.nz);
@@ -1193,7 +1213,7 @@ extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace(FrameArgs 
     const uint64_t pix = (uint64_t)xf + (uint64_t)yf * a.W;
     const bool inb = valid && pix < (uint64_t)a.W * a.H;
     out.pixel = inb ? (uint32_t)pix : 0xffffffffu;
-    if (valid) lanes[(size_t)packet * 8u + q] = out;
+    if (valid) lanes[(size_t)packet * PW + q] = out;
     if (inb) atomicMax(owner + pix, (unsigned long long)(ticket0 + packet));
 
     const float closest = wave_min(inb ? h.minT : FLT_MAX);
@@ -1205,16 +1225,32 @@ extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace(FrameArgs 
     }
 }
 
+extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace(FrameArgs a, const uint32_t* draws,
+                                                                       uint64_t counter0, uint32_t packets,
+                                                                       uint64_t ticket0, PacketLane* lanes,
+                                                                       unsigned long long* owner)
+{
+    progressive_trace<8>(a, draws, counter0, packets, ticket0, lanes, owner);
+}
+extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace_sse(FrameArgs a, const uint32_t* draws,
+                                                                           uint64_t counter0, uint32_t packets,
+                                                                           uint64_t ticket0, PacketLane* lanes,
+                                                                           unsigned long long* owner)
+{
+    progressive_trace<4>(a, draws, counter0, packets, ticket0, lanes, owner);
+}
+
 // Last writer wins by ticket (= the reference worker's sequential packet order).
 extern "C" __global__ __launch_bounds__(256) void sf_progressive_scatter(FrameArgs a, uint32_t packets, uint64_t ticket0,
                                                                          const PacketLane* lanes,
                                                                          const unsigned long long* owner)
 {
+    const uint32_t pl = a.packet_lanes;   // lanes per packet (8 AVX, 4 SSE)
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= packets * 8u) return;
+    if (i >= packets * pl) return;
     const PacketLane l = lanes[i];
     if (l.pixel == 0xffffffffu) return;
-    if (owner[l.pixel] != (unsigned long long)(ticket0 + i / 8u)) return;
+    if (owner[l.pixel] != (unsigned long long)(ticket0 + i / pl)) return;
     reinterpret_cast<float4*>(a.pos)[l.pixel] = make_float4(l.px, l.py, l.pz, 1.0f);
     reinterpret_cast<float4*>(a.nrm)[l.pixel] = make_float4(l.nx, l.ny, l.nz, 1.0f);
     if (a.emit_aux && a.min_t) a.min_t[l.pixel] = l.min_t;

@@ -219,13 +219,13 @@ float radius(uint32_t depth)
 
 static inline float bits2f(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 
-// Exact LOD threshold. The reference predicate  sqrtf(t / r) < 70 || t < 0  (Sphereflake.h:146) is a
-// composition of correctly rounded monotone operations, so for t >= 0 it is true exactly on
-// [0, T) for some float T; for t < 0 it is true. Hence  pred(t) <=> t < T. Binary search over the
-// ordered bit patterns of non-negative floats finds T.
-float lod_threshold(float r)
+// Exact LOD threshold. The reference predicate  sqrtf(t / r) < C || t < 0  (Sphereflake.h:146, C = 70;
+// SSE variant Sphereflake.h:129, C = 60) is a composition of correctly rounded monotone operations, so
+// for t >= 0 it is true exactly on [0, T) for some float T; for t < 0 it is true. Hence
+// pred(t) <=> t < T. Binary search over the ordered bit patterns of non-negative floats finds T.
+float lod_threshold(float r, float lod_constant)
 {
-    auto pred = [r](float t) { return std::sqrt(t / r) < 70.0f || t < 0.0f; };
+    auto pred = [r, lod_constant](float t) { return std::sqrt(t / r) < lod_constant || t < 0.0f; };
     uint32_t lo = 0, hi = 0x7f800000u;   // pred(lo) true (t = 0), pred(+inf) false
     while (hi - lo > 1) {
         uint32_t mid = lo + (hi - lo) / 2;
@@ -234,7 +234,7 @@ float lod_threshold(float r)
     return bits2f(hi);
 }
 
-void depth_tables(DepthTables* t)
+void depth_tables(DepthTables* t, float lod_constant)
 {
     for (uint32_t d = 0; d < SF_DEPTH_TABLE; ++d) {
         float r = radius(d);
@@ -242,7 +242,7 @@ void depth_tables(DepthTables* t)
         t->r2_bound[d] = dr * dr;                 // Sphereflake.h:108-110
         t->r2_self[d] = r * r;                    // :180
         t->scale[d] = (4.0f / 3.0f) * r;          // :162
-        t->lod[d] = lod_threshold(r);             // :146
+        t->lod[d] = lod_threshold(r, lod_constant);   // :146 (SSE :129)
     }
 }
 

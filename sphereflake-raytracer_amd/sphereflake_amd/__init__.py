@@ -66,6 +66,8 @@ class sf_post_params(ctypes.Structure):
                 ("stream", ctypes.c_void_p)]
 
 
+SF_VARIANT_AVX = 0
+SF_VARIANT_SSE = 1
 SF_POST_GENERAL = 1
 SF_POST_UNIT_NORMALS = 2
 
@@ -86,6 +88,9 @@ SIGNATURES = {
     "sf_download": (ctypes.c_int, [_CTX, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "sf_download_async": (ctypes.c_int, [_CTX, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
+    "sf_set_variant": (ctypes.c_int, [_CTX, ctypes.c_int]),
+    "sf_get_variant": (ctypes.c_int, [_CTX]),
+    "sf_lod_threshold": (ctypes.c_int, [ctypes.c_float, ctypes.c_float, _F]),
     "sf_post_defaults": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_post_params)]),
     "sf_post_process": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_post_params), ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p]),
@@ -198,6 +203,14 @@ def depth_constants(depth: int):
     r, t = ctypes.c_float(), ctypes.c_float()
     _check(lib().sf_depth_constants(depth, ctypes.byref(r), ctypes.byref(t)), "sf_depth_constants")
     return r.value, t.value
+
+
+def lod_threshold(r: float, lod_constant: float = 70.0) -> float:
+    """Exact T with sqrtf(t / r) < lod_constant || t < 0  <=>  t < T (Sphereflake.h:129,146)."""
+    t = ctypes.c_float()
+    _check(lib().sf_lod_threshold(ctypes.c_float(r), ctypes.c_float(lod_constant), ctypes.byref(t)),
+           "sf_lod_threshold")
+    return t.value
 
 
 def rsqrtps(x: float) -> float:
@@ -362,6 +375,17 @@ class Sphereflake:
     def GetGBuffer(self) -> GBuffer:
         pos, nrm, _, _ = self.download()
         return GBuffer(pos, nrm)
+
+    # reference variant ---------------------------------
+    def SetVariant(self, variant):
+        """'avx' / SF_VARIANT_AVX (default: LOD 70, 8-lane packets) or 'sse' / SF_VARIANT_SSE (LOD 60,
+        4-lane packets, 2x2 frame-less footprint): the reference built without / with __ARCH_NO_AVX."""
+        v = {"avx": SF_VARIANT_AVX, "sse": SF_VARIANT_SSE}.get(variant, variant)
+        with self._mutex:
+            _check(lib().sf_set_variant(self._ctx, int(v)), "SetVariant", self._ctx)
+
+    def GetVariant(self) -> int:
+        return lib().sf_get_variant(self._ctx)
 
     # transfer/interop (SURVEY.md §8(f3)) ------------------------------------
     def pinned_gbuffer(self) -> GBuffer:

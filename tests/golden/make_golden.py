@@ -91,11 +91,11 @@ def gen_setup(name, W, H, K):
     return pyoracle.load_setup(name)
 
 
-def gen_frame(name, W, H, K, step, nsamp):
+def gen_frame(name, W, H, K, step, nsamp, sse=False):
     setup = gen_setup(name, W, H, K)
-    ref = pyoracle.ref_render(W, H, K, row_step=step, threads=8)
+    ref = pyoracle.ref_render(W, H, K, row_step=step, threads=8, sse=sse)
     rows = np.arange(0, H, step)
-    orc = pyoracle.render(setup, rows=rows, threads=8)
+    orc = pyoracle.render(setup, rows=rows, threads=8, lod=60.0 if sse else 70.0)
     # --- gate: restatement == reference, bit for bit
     for key, rk in (("pos4", "pos"), ("nrm4", "nrm")):
         a = orc[key][..., :3].view(np.uint32)
@@ -111,6 +111,7 @@ def gen_frame(name, W, H, K, step, nsamp):
     g, a = row_digests(pos4, nrm4, orc["minT"], orc["index"])
     fx = {
         "name": name, "W": W, "H": H, "K": float(np.float32(K)).hex(), "row_step": step,
+        "variant": "sse" if sse else "avx",
         "stats": {
             "max_depth": ref["stats"]["max_depth"], "closest": ref["stats"]["closest"],
             "hits": ref["stats"]["hits"], "rays": int(len(rows) * W),
@@ -152,21 +153,36 @@ PROGRESSIVE = {
 }
 
 
-def gen_progressive(name, W, H, K, seed, packets):
+def gen_progressive(name, W, H, K, seed, packets, sse=False):
     path = f"/tmp/sf_prog_{name}.bin"
-    st = run_json([os.path.join(REF, "ref_harness"), "progressive", str(W), str(H), repr(K), str(seed),
-                   str(packets), path])
+    st = run_json([os.path.join(REF, "ref_harness_sse" if sse else "ref_harness"), "progressive", str(W), str(H),
+                   repr(K), str(seed), str(packets), path])
     a = np.fromfile(path, dtype=np.float32)
     os.unlink(path)
     pos4 = a[: 4 * W * H].reshape(H, W, 4)
     nrm4 = a[4 * W * H:].reshape(H, W, 4)
     g = [hashlib.sha256(pos4[y].tobytes() + nrm4[y].tobytes()).hexdigest()[:16] for y in range(H)]
     fx = {"name": name, "W": W, "H": H, "K": float(np.float32(K)).hex(), "seed": seed, "packets": packets,
+          "variant": "sse" if sse else "avx",
           "stats": st, "frame_digest": frame_digest(pos4, nrm4), "row_digest_gbuf": g,
           "written": int((pos4[..., 3] == 1.0).sum())}
     with open(os.path.join(HERE, f"progressive_{name}.json"), "w") as f:
         json.dump(fx, f, separators=(",", ":"))
     print(name, st, fx["written"])
+
+
+# The reference's SSE variant (__ARCH_NO_AVX: LOD constant 60, 4-lane packets,
+# 2x2 frame-less footprint): same cameras as above.
+SSE_CONFIGS = {
+    "s1": (64, 36, 1.0, 1, 0),
+    "s2": (80, 45, 0.22, 1, 0),
+    "s3": (640, 360, 1.0, 1, 4096),
+    "s4": (1920, 1080, 0.25, 1, 4096),
+}
+SSE_PROGRESSIVE = {
+    "ps1": (64, 36, 0.25, 1, 3000),
+    "ps2": (640, 360, 1.0, 12345, 100000),
+}
 
 
 def gen_sobol_mt():
@@ -195,6 +211,14 @@ def main():
         if args.only and name not in args.only:
             continue
         gen_progressive(name, *cfg)
+    for name, (W, H, K, step, nsamp) in SSE_CONFIGS.items():
+        if args.only and name not in args.only:
+            continue
+        gen_frame(name, W, H, K, step, nsamp, sse=True)
+    for name, cfg in SSE_PROGRESSIVE.items():
+        if args.only and name not in args.only:
+            continue
+        gen_progressive(name, *cfg, sse=True)
 
 
 if __name__ == "__main__":

@@ -259,3 +259,61 @@ def test_camera_inside_bounding_ball_uses_fixup_levels():
     for x, y in zip(a, b):
         assert np.array_equal(np.ascontiguousarray(x).view(np.uint8), np.ascontiguousarray(y).view(np.uint8))
     assert st.overflow_tiles == 0
+
+
+# ---- the reference's SSE variant: LOD 60, 4-lane packets, 2x2 footprint
+
+@pytest.mark.parametrize("name", ["s1", "s2"])
+def test_sse_variant_tiny_frames_bit_exact(name):
+    exp = load_npz(name)
+    fx = load_frame(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetVariant("sse")
+        assert s.GetVariant() == sf.SF_VARIANT_SSE
+        s.SetCamera(sf.config_camera(W, H, K))
+        s.Render(emit_aux=True)
+        pos, nrm, mint, idx = s.download(aux=True)
+        st = s.stats()
+    for k, got in (("pos4", pos), ("nrm4", nrm), ("minT", mint), ("index", idx)):
+        assert np.array_equal(np.ascontiguousarray(got).view(np.uint8), np.ascontiguousarray(exp[k]).view(np.uint8)), k
+    check_stats(fx, st, mint)
+
+
+@pytest.mark.parametrize("name", ["s3", "s4"])
+def test_sse_variant_config_frames_bit_exact(name):
+    """Full frames, rendered twice (the second with the heavy-first tile order) after switching an AVX
+    context to the SSE variant: the switch must reset every per-variant table and hint."""
+    fx = load_frame(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        s.Render()
+        s.SetVariant("sse")
+        for k in range(2):
+            s.Render(emit_aux=True)
+            pos, nrm, mint, idx = s.download(aux=True)
+            assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == [], f"render {k}"
+            assert bad_rows(fx["row_digest_aux"], aux_digests(mint, idx)) == [], f"render {k}"
+        st = s.stats()
+    assert st.max_depth == fx["stats"]["max_depth"]
+
+
+@pytest.mark.parametrize("name", ["ps1", "ps2"])
+def test_sse_variant_progressive_matches_reference_worker(name):
+    """Frame-less mode of the SSE build: 4-ray packets on the 2x2 footprint (Sphereflake.cpp:115-138)."""
+    fx = load_progressive(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetVariant(sf.SF_VARIANT_SSE)
+        s.SetCamera(sf.config_camera(W, H, K))
+        half = fx["packets"] // 3
+        s.Progressive(fx["seed"], half, counter0=0)
+        s.Progressive(fx["seed"], fx["packets"] - half)
+        pos, nrm, _, _ = s.download()
+        st = s.stats()
+    bad = bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm))
+    assert bad == [], f"{len(bad)} rows differ, first {bad[:5]}"
+    assert st.max_depth == fx["stats"]["max_depth"]
+    assert np.float32(st.closest) == np.float32(float.fromhex(fx["stats"]["closest"]))
+    assert st.rays == fx["stats"]["rays"]

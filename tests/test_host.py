@@ -168,3 +168,21 @@ def test_save_ppm_layout(tmp_path):
     assert b[:len(head)] == head
     px = np.frombuffer(b[len(head):], np.uint8).reshape(2, 3, 3)
     assert tuple(px[0, 0]) == (255, 128, 0) and tuple(px[1, 2]) == (255, 0, 64)
+
+
+@pytest.mark.parametrize("c", [70.0, 60.0])
+def test_lod_threshold_exact_both_variants(c):
+    """sqrtf(t/r) < C || t < 0  <=>  t < T for the AVX (70) and SSE (60, SIMD_SSE.h:21) constants."""
+    rng = np.random.default_rng(11)
+    for d in range(0, 16):
+        r = np.float32(sf.depth_constants(d)[0])
+        T = np.float32(sf.lod_threshold(float(r), c))
+        tb = np.array([T], np.float32).view(np.int32)[0]
+        near = (np.arange(tb - 500, tb + 500, dtype=np.int32)).view(np.float32)
+        rand = (rng.random(5000).astype(np.float32) * np.float32(3) * T).astype(np.float32)
+        for t in (near, rand, -rand):
+            with np.errstate(invalid="ignore"):
+                ref = (np.sqrt(t / r) < np.float32(c)) | (t < 0)
+            assert np.array_equal(ref, t < T), (c, d)
+    r1, T1 = sf.depth_constants(1)
+    assert sf.lod_threshold(r1, 70.0) == T1

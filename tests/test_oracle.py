@@ -108,3 +108,28 @@ def test_oracle_matches_reference_binary(W, H, K, lut):
     assert np.array_equal(r["nrm4"][..., :3].view(np.uint32), ref["nrm"].view(np.uint32))
     assert np.array_equal(r["minT"].view(np.uint32), ref["minT"].view(np.uint32))
     assert r["stats"]["max_depth"] == ref["stats"]["max_depth"]
+
+
+# ---- the reference's SSE variant (__ARCH_NO_AVX, LOD constant 60)
+
+@pytest.mark.parametrize("name", ["s1", "s2"])
+def test_sse_variant_tiny_frames_bit_exact(name, lut):
+    fx = load_npz(name)
+    r = pyoracle.render(pyoracle.load_setup(name), lut=lut, threads=4, lod=60.0)
+    for k in ("pos4", "nrm4", "minT", "index", "depth"):
+        assert np.array_equal(np.ascontiguousarray(r[k]).view(np.uint8), np.ascontiguousarray(fx[k]).view(np.uint8)), k
+
+
+@pytest.mark.parametrize("name,nrows", [("s3", 40), ("s4", 12)])
+def test_sse_variant_rows(name, nrows, lut):
+    fx = load_frame(name)
+    assert fx["variant"] == "sse"
+    rows = np.linspace(0, fx["H"] - 1, nrows).astype(int)
+    r = pyoracle.render(pyoracle.load_setup(name), rows=rows, lut=lut, lod=60.0)
+    exp = [fx["row_digest_gbuf"][k] for k in rows]
+    assert bad_rows(exp, row_digests(r["pos4"], r["nrm4"])) == []
+
+
+def test_sse_and_avx_variants_differ():
+    """The LOD constant changes the image: the same camera renders differently under 60 and 70."""
+    assert load_frame("s4")["frame_digest"] != load_frame("c3")["frame_digest"]
