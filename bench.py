@@ -67,6 +67,7 @@ def frame_camera(width, height, k, frame):
     return cam
 
 
+KTIMING_PERIOD = 5                   # trace-kernel HIP events on every 5th timed render
 CPU_REPS = 40                        # ~1.2 s wall x 16 threads: ~20 s of CPU work
 
 
@@ -275,7 +276,9 @@ def main():
     if args.mode == "frames":
         o, tl, tr, bl = views[0]
         ctx.SetView(o, tl, tr, bl)
-    ctx.kernel_timing(True)   # HIP events around the dominant (trace) kernel of every render
+    # HIP events around the dominant (trace) kernel of every KTIMING_PERIOD-th render: an event pair
+    # costs ~7 us of stream time per frame, so it is sampled (SF_BENCH_KTIMING=0: off, for A/B)
+    ktiming = os.environ.get("SF_BENCH_KTIMING", "1") != "0"
 
     ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -303,6 +306,7 @@ def main():
 
     for i in range(args.warmup):
         run_step(i, False)
+    ctx.kernel_timing(ktiming, period=KTIMING_PERIOD)   # samples timed renders 0, 5, 10, ...
     torch.cuda.synchronize(dev)
     if dist_on:
         dist.barrier()
@@ -319,7 +323,7 @@ def main():
     if st.overflow_tiles:
         raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
     kern_ms = float(np.mean([ev_s[i].elapsed_time(ev_e[i]) for i in range(args.steps)]))   # whole render
-    tk = ctx.kernel_timing(n=min(args.steps, 64))        # the trace kernel alone, last timed renders
+    tk = ctx.kernel_timing(n=min(-(-args.steps // KTIMING_PERIOD), 64)) if ktiming else []   # the trace kernel alone, last timed renders
     trace_ms = float(np.mean(tk)) if len(tk) else kern_ms
 
     t_step = dt / args.steps

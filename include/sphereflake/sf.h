@@ -242,8 +242,10 @@ int sf_get_tile_trace(sf_ctx* ctx, uint64_t* out, size_t n);   /* n >= 3 * tiles
 
 /* --- measurement ---------------------------------------------------------- */
 
-/* When enabled, every full-frame render records HIP events on its launch stream around its main
-   trace kernel (the dominant kernel; the roofline in bench.py is priced on it). */
+/* enable = k > 0: every k-th full-frame render (counting from the call) records HIP events on its
+   launch stream around its main trace kernel (the dominant kernel; the roofline in bench.py is priced
+   on it). An event pair costs a few us of stream time, so sampling keeps the measurement out of the
+   frame rate. enable = 0 turns it off. */
 int sf_set_kernel_timing(sf_ctx* ctx, int enable);
 /* Durations (ms) of the main trace kernel of the last min(n, 64) timed renders, oldest first;
    returns how many were written (>= 0) or a negative SF_E*. Synchronises. */

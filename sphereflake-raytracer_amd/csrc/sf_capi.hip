@@ -124,6 +124,7 @@ struct sf_ctx {
     hipEvent_t ev[kTimed][2] = {};
     bool timing = false;
     uint32_t ev_next = 0, ev_count = 0;
+    uint32_t ev_period = 1, ev_phase = 0;   // time every ev_period-th render
     // SSAO post-process (sf_post_process): lazily allocated
     float* noise = nullptr;            // 64x64 float4
     uint8_t* ao = nullptr;             // SSAO target, sized for post_ao_px pixels
@@ -482,12 +483,14 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 a.tile_order = (c->order_n == ntiles && c->order_stream == s) ? c->tile_order : nullptr;
                 a.prio_tiles = c->prio_tiles;
             }
-            if (c->timing) SF_HIP(c, hipEventRecord(c->ev[c->ev_next][0], s));
+            const bool timed = c->timing && c->ev_phase == 0;
+            if (c->timing) c->ev_phase = (c->ev_phase + 1u) % c->ev_period;
+            if (timed) SF_HIP(c, hipEventRecord(c->ev[c->ev_next][0], s));
             if (wpb == 1) hipLaunchKernelGGL(sf_trace_queue1, grid, block, lds, s, a);
             else if (wpb == 2) hipLaunchKernelGGL(sf_trace_queue2, grid, block, 2 * lds, s, a);
             else hipLaunchKernelGGL(sf_trace_queue4, grid, block, 4 * lds, s, a);
             SF_HIP(c, hipGetLastError());
-            if (c->timing) {
+            if (timed) {
                 SF_HIP(c, hipEventRecord(c->ev[c->ev_next][1], s));
                 c->ev_next = (c->ev_next + 1u) % sf_ctx::kTimed;
                 c->ev_count = c->ev_count < (uint32_t)sf_ctx::kTimed ? c->ev_count + 1u : c->ev_count;
@@ -834,8 +837,10 @@ int sf_set_kernel_timing(sf_ctx* c, int enable)
         for (int i = 0; i < sf_ctx::kTimed; ++i)
             for (int j = 0; j < 2; ++j) SF_HIP(c, hipEventCreate(&c->ev[i][j]));
     }
+    if (enable < 0) return SF_EINVAL;
     c->timing = enable != 0;
-    c->ev_next = c->ev_count = 0;
+    c->ev_period = enable > 0 ? (uint32_t)enable : 1u;
+    c->ev_next = c->ev_count = c->ev_phase = 0;
     return SF_OK;
 }
 

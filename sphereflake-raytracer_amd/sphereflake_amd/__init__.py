@@ -472,11 +472,12 @@ class Sphereflake:
         self.phase_sums = out[3 * n:]          # segment cycle sums of stamp builds (zeros otherwise)
         return out[:3 * n].reshape(n, 3)
 
-    def kernel_timing(self, enable: bool | None = None, n: int = 64):
-        """Measurement: enable HIP events around each render's main trace kernel, or (enable=None)
-        return the durations (ms) of the last n timed renders, oldest first."""
+    def kernel_timing(self, enable: bool | None = None, n: int = 64, period: int = 1):
+        """Measurement: enable HIP events around the main trace kernel of every `period`-th render, or
+        (enable=None) return the durations (ms) of the last n timed renders, oldest first."""
         if enable is not None:
-            _check(lib().sf_set_kernel_timing(self._ctx, int(bool(enable))), "sf_set_kernel_timing", self._ctx)
+            k = max(1, int(period)) if enable else 0
+            _check(lib().sf_set_kernel_timing(self._ctx, k), "sf_set_kernel_timing", self._ctx)
             return None
         out = np.zeros(n, np.float32)
         k = lib().sf_kernel_times(self._ctx, out.ctypes.data_as(_F), n)

@@ -240,8 +240,13 @@ def test_repeat_renders_heavy_first_order_bit_exact():
             assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == [], f"render {k}"
             assert bad_rows(fx["row_digest_aux"], aux_digests(mint, idx)) == [], f"render {k}"
         ms = s.kernel_timing()
+        s.kernel_timing(True, period=2)     # sampled: renders 0 and 2 of the next three
+        for k in range(3):
+            s.Render()
+        ms2 = s.kernel_timing()
         st = s.stats()
     assert len(ms) == 3 and np.all(ms > 0)
+    assert len(ms2) == 2 and np.all(ms2 > 0)
     assert st.max_depth == fx["stats"]["max_depth"] and st.overflow_tiles == 0
 
 
