@@ -81,8 +81,14 @@ def pmc_valu(kernel, cus=256):
             c = json.load(f)["kernels"][kernel]
         cycles = c["GRBM_GUI_ACTIVE"] / 8.0
         slots = cus * 4 * cycles / 2.0
+        # wavefront occupancy: SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md), summed over the
+        # chip -> mean resident waves; against the gfx950 peak of 8 waves per SIMD
+        waves = 4.0 * c["SQ_WAVE_CYCLES"] / cycles
+        peak_waves = cus * 4 * 8
         return {"valu_insts": round(c["SQ_INSTS_VALU"]), "salu_insts": round(c["SQ_INSTS_SALU"]),
                 "issue_slots": round(slots), "valu_issue_frac": round(c["SQ_INSTS_VALU"] / slots, 4),
+                "occupancy": {"mean_waves": round(waves, 1), "peak_waves": peak_waves,
+                              "frac": round(waves / peak_waves, 4)},
                 "clock_mhz": round(cycles / c["profiled_dispatch_us"], 1), "source": "profiles/pmc_traffic.json"}
     except (OSError, KeyError, ValueError, ZeroDivisionError):
         return None

@@ -239,6 +239,11 @@ float sf_rsqrtps(float x);
    never changes results. */
 int sf_set_tile_trace(sf_ctx* ctx, int enable);
 int sf_get_tile_trace(sf_ctx* ctx, uint64_t* out, size_t n);   /* n >= 3 * tiles; synchronises */
+/* Heavy-first tile schedule: the permutation the next persistent render takes its 8x8 tiles in
+   (computed from the last render's per-tile costs, heaviest log2-bucket first, stable within a bucket)
+   and those costs (shader cycles). Either pointer may be NULL; n >= tiles. Returns the tile count, 0
+   when no order exists yet, or a negative SF_E*. Synchronises. */
+int sf_get_tile_order(sf_ctx* ctx, uint32_t* order, uint32_t* cost, size_t n);
 
 /* --- measurement ---------------------------------------------------------- */
 

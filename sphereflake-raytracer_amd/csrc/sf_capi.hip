@@ -819,6 +819,19 @@ int sf_get_tile_trace(sf_ctx* c, uint64_t* out, size_t n)
     return SF_OK;
 }
 
+int sf_get_tile_order(sf_ctx* c, uint32_t* order, uint32_t* cost, size_t n)
+{
+    if (!c) return SF_EINVAL;
+    DevGuard g(c->device);
+    const size_t ntiles = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8);
+    if (n < ntiles || (!order && !cost)) return SF_EINVAL;
+    SF_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->order_n != ntiles) return 0;
+    if (order) SF_HIP(c, hipMemcpy(order, c->tile_order, ntiles * 4, hipMemcpyDeviceToHost));
+    if (cost) SF_HIP(c, hipMemcpy(cost, c->tile_cost, ntiles * 4, hipMemcpyDeviceToHost));
+    return (int)ntiles;
+}
+
 int sf_device_buffers(sf_ctx* c, float** pos4, float** nrm4, float** min_t, uint32_t** hidx)
 {
     if (!c) return SF_EINVAL;

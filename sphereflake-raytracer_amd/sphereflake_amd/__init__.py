@@ -113,6 +113,8 @@ SIGNATURES = {
     "sf_rsqrtps": (ctypes.c_float, [ctypes.c_float]),
     "sf_set_tile_trace": (ctypes.c_int, [_CTX, ctypes.c_int]),
     "sf_get_tile_trace": (ctypes.c_int, [_CTX, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]),
+    "sf_get_tile_order": (ctypes.c_int, [_CTX, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                         ctypes.c_size_t]),
     "sf_set_kernel_timing": (ctypes.c_int, [_CTX, ctypes.c_int]),
     "sf_kernel_times": (ctypes.c_int, [_CTX, _F, ctypes.c_uint32]),
     "sf_strerror": (ctypes.c_char_p, [ctypes.c_int]),
@@ -471,6 +473,19 @@ class Sphereflake:
                "sf_get_tile_trace", self._ctx)
         self.phase_sums = out[3 * n:]          # segment cycle sums of stamp builds (zeros otherwise)
         return out[:3 * n].reshape(n, 3)
+
+    def tile_order(self):
+        """Heavy-first schedule: (order, cost) uint32 arrays over the 8x8 tiles -- the permutation the
+        next persistent render takes tiles in, and the last render's per-tile shader cycles it was
+        computed from -- or None before any ordered render."""
+        n = ((self.width + 7) // 8) * ((self.height + 7) // 8)
+        order = np.zeros(n, np.uint32)
+        cost = np.zeros(n, np.uint32)
+        P = ctypes.POINTER(ctypes.c_uint32)
+        k = lib().sf_get_tile_order(self._ctx, order.ctypes.data_as(P), cost.ctypes.data_as(P), n)
+        if k < 0:
+            _check(k, "sf_get_tile_order", self._ctx)
+        return (order, cost) if k else None
 
     def kernel_timing(self, enable: bool | None = None, n: int = 64, period: int = 1):
         """Measurement: enable HIP events around the main trace kernel of every `period`-th render, or

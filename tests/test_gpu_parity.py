@@ -322,3 +322,29 @@ def test_sse_variant_progressive_matches_reference_worker(name):
     assert st.max_depth == fx["stats"]["max_depth"]
     assert np.float32(st.closest) == np.float32(float.fromhex(fx["stats"]["closest"]))
     assert st.rays == fx["stats"]["rays"]
+
+
+def cost_bucket(c):
+    """Host restatement of the kernels' cost_bucket (sf_kernels.hip): 2 log buckets per octave from 2^8."""
+    k = (np.asarray(c | 1, np.uint32).astype(np.float32).view(np.uint32) >> 22).astype(np.int64)
+    b = k - (135 << 1)
+    return np.where((b >= 0) & (b < 32), b, np.where(k < (135 << 1), 0, 31))
+
+
+@pytest.mark.parametrize("W,H", [(1920, 1080), (3840, 2160), (100, 60)])
+def test_tile_order_is_stable_heavy_first_permutation(W, H):
+    """The next render's tile order (sf_order_scan + sf_order_scatter) is a permutation of the tiles,
+    non-increasing in cost bucket and in tile order within a bucket: exactly the stable sort of the
+    last render's tile costs by bucket, heaviest first."""
+    n = ((W + 7) // 8) * ((H + 7) // 8)
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, 0.25))
+        assert s.tile_order() is None
+        s.Render()
+        order, cost = s.tile_order()
+    assert np.array_equal(np.sort(order), np.arange(n, dtype=np.uint32))
+    bk = cost_bucket(cost)[order]
+    assert np.all(np.diff(bk) <= 0)
+    assert np.all(np.diff(order.astype(np.int64))[np.diff(bk) == 0] > 0)
+    exp = np.lexsort((np.arange(n), -cost_bucket(cost)))
+    assert np.array_equal(order, exp.astype(np.uint32))
