@@ -44,8 +44,8 @@ TRACE_KERNEL = "sf_trace_queue2"    # the dominant kernel (persistent wave-coher
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--mode", choices=["frames", "rows"], default="frames")
     ap.add_argument("--kernel", choices=["wave", "ray"], default="wave")
     ap.add_argument("--width", type=int, default=W)

@@ -239,10 +239,12 @@ float sf_rsqrtps(float x);
    never changes results. */
 int sf_set_tile_trace(sf_ctx* ctx, int enable);
 int sf_get_tile_trace(sf_ctx* ctx, uint64_t* out, size_t n);   /* n >= 3 * tiles; synchronises */
-/* Heavy-first tile schedule: the permutation the next persistent render takes its 8x8 tiles in
-   (computed from the last render's per-tile costs, heaviest log2-bucket first, stable within a bucket)
-   and those costs (shader cycles). Either pointer may be NULL; n >= tiles. Returns the tile count, 0
-   when no order exists yet, or a negative SF_E*. Synchronises. */
+/* Heavy-first tile schedule: the work units the next persistent render takes in order (computed from
+   the last render's per-tile costs, heaviest cost bucket first, stable within a bucket; a unit is
+   tile | half << 30, half 0 = the whole 8x8 tile, 1/2 = its pixel rows 0-3/4-7 -- the tiles of the
+   heaviest bucket are traced as two half units) and those costs (shader cycles, one per tile).
+   Either pointer may be NULL; n >= 2 * tiles (order) or tiles (cost only). Returns the unit count,
+   0 when no order exists yet, or a negative SF_E*. Synchronises. */
 int sf_get_tile_order(sf_ctx* ctx, uint32_t* order, uint32_t* cost, size_t n);
 
 /* --- measurement ---------------------------------------------------------- */

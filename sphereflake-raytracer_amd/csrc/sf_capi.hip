@@ -22,9 +22,10 @@ extern "C" __global__ void sf_trace_wave4(FrameArgs a, uint32_t* overflow_list, 
 extern "C" __global__ void sf_trace_queue1(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2(FrameArgs a);
 extern "C" __global__ void sf_trace_queue4(FrameArgs a);
-extern "C" __global__ void sf_order_scan(const uint32_t* chunk_cnt, uint32_t nc, uint32_t* chunk_off);
+extern "C" __global__ void sf_order_scan(const uint32_t* chunk_cnt, uint32_t nc, uint32_t n_tiles,
+                                         uint32_t split_buckets, uint32_t* chunk_off, uint32_t* order_meta);
 extern "C" __global__ void sf_order_scatter(const uint32_t* cost, uint32_t n, uint32_t* chunk_cnt,
-                                            const uint32_t* chunk_off, uint32_t* order);
+                                            const uint32_t* chunk_off, const uint32_t* order_meta, uint32_t* order);
 extern "C" __global__ void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list, uint32_t* counters,
                                          uint32_t parity);
 extern "C" __global__ void sf_trace_ray(FrameArgs a);
@@ -116,6 +117,8 @@ struct sf_ctx {
     uint32_t* tile_order = nullptr;
     uint32_t* chunk_cnt = nullptr;     // per 64-tile chunk x SF_ORDER_BUCKETS (zeroed by sf_order_scatter)
     uint32_t* chunk_off = nullptr;
+    uint32_t* order_meta = nullptr;    // [0] work units in tile_order, [1] first split bucket
+    uint32_t split_buckets = SF_SPLIT_BUCKETS_DEFAULT;   // env SF_SPLIT_BUCKETS (0: never split)
     uint32_t order_n = 0;              // tile count the current tile_order is a permutation of (0: none)
     hipStream_t order_stream = nullptr;   // the stream it was computed on (used only on the same stream)
     bool use_order = true;             // env SF_ORDER=0: row-major order always
@@ -167,6 +170,7 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->tile_order);
     (void)hipFree(c->chunk_cnt);
     (void)hipFree(c->chunk_off);
+    (void)hipFree(c->order_meta);
     (void)hipFree(c->noise);
     (void)hipFree(c->ao);
     (void)hipFree(c->blur_h);
@@ -256,6 +260,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     c->cus = prop.multiProcessorCount;
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_ORDER")) c->use_order = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_SPLIT_BUCKETS")) c->split_buckets = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_FLAGS")) c->flags = (uint32_t)std::strtoul(ev, nullptr, 0);
     if (const char* ev = std::getenv("SF_PRIO_TILES")) c->prio_tiles = (uint32_t)std::strtoul(ev, nullptr, 0);
@@ -285,7 +290,8 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if ((e = hipMalloc(&c->ovf_counters, SF_COUNTER_WORDS * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->ovf_list, ntiles * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->tile_cost, ntiles * 4)) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&c->tile_order, ntiles * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->tile_order, 2 * ntiles * 4)) != hipSuccess) return fail(e);   // <= 2 units per tile
+    if ((e = hipMalloc(&c->order_meta, 2 * 4)) != hipSuccess) return fail(e);
     const size_t nchunks = (ntiles + 63) / 64;
     if ((e = hipMalloc(&c->chunk_cnt, nchunks * SF_ORDER_BUCKETS * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->chunk_off, nchunks * SF_ORDER_BUCKETS * 4)) != hipSuccess) return fail(e);
@@ -481,6 +487,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 a.tile_cost = c->tile_cost;
                 a.chunk_cnt = c->chunk_cnt;
                 a.tile_order = (c->order_n == ntiles && c->order_stream == s) ? c->tile_order : nullptr;
+                a.order_meta = c->order_meta;
                 a.prio_tiles = c->prio_tiles;
             }
             const bool timed = c->timing && c->ev_phase == 0;
@@ -497,10 +504,12 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             }
             if (c->use_order) {   // the next render's tile order, from this render's tile costs
                 const uint32_t nc = (ntiles + 63u) / 64u;
-                hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->chunk_cnt, nc, c->chunk_off);
+                hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->chunk_cnt, nc, ntiles,
+                                   c->split_buckets, c->chunk_off, c->order_meta);
                 SF_HIP(c, hipGetLastError());
                 hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost, ntiles,
-                                   c->chunk_cnt, (const uint32_t*)c->chunk_off, c->tile_order);
+                                   c->chunk_cnt, (const uint32_t*)c->chunk_off, (const uint32_t*)c->order_meta,
+                                   c->tile_order);
                 SF_HIP(c, hipGetLastError());
                 c->order_n = ntiles;
                 c->order_stream = s;
@@ -827,9 +836,12 @@ int sf_get_tile_order(sf_ctx* c, uint32_t* order, uint32_t* cost, size_t n)
     if (n < ntiles || (!order && !cost)) return SF_EINVAL;
     SF_HIP(c, hipStreamSynchronize(c->stream));
     if (c->order_n != ntiles) return 0;
-    if (order) SF_HIP(c, hipMemcpy(order, c->tile_order, ntiles * 4, hipMemcpyDeviceToHost));
+    uint32_t meta[2];
+    SF_HIP(c, hipMemcpy(meta, c->order_meta, sizeof(meta), hipMemcpyDeviceToHost));
+    if (order && n < meta[0]) return SF_EINVAL;
+    if (order) SF_HIP(c, hipMemcpy(order, c->tile_order, (size_t)meta[0] * 4, hipMemcpyDeviceToHost));
     if (cost) SF_HIP(c, hipMemcpy(cost, c->tile_cost, ntiles * 4, hipMemcpyDeviceToHost));
-    return (int)ntiles;
+    return (int)meta[0];
 }
 
 int sf_device_buffers(sf_ctx* c, float** pos4, float** nrm4, float** min_t, uint32_t** hidx)

@@ -40,6 +40,10 @@
 
 #define SF_FLAG_NO_LOD_CULL 1u    // disable the leaf-threshold skip (A/B only; results identical)
 #define SF_FLAG_NO_CONE_CULL 2u   // disable the per-child ray-cone cull (A/B only; results identical)
+// diagnostics (schedule studies): trace only one half unit of every 8x8 tile -- pixel rows 0-3, or
+// with SF_FLAG_DIAG_HALF_SEL rows 4-7. Other pixels are not written. Never set by the product path.
+#define SF_FLAG_DIAG_HALF 4u
+#define SF_FLAG_DIAG_HALF_SEL 8u
 
 struct DepthTables {
     float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)
@@ -92,7 +96,8 @@ struct FrameArgs {
     uint32_t* overflow_list;          // tiles to re-trace with SF_MAX_DEPTH_LIMIT levels
     uint32_t parity;                  // which half of `counters` this render uses
     uint32_t* tile_cost;              // out (NULL = off): per tile, shader cycles of its traversal
-    const uint32_t* tile_order;       // in (NULL = row-major): tile permutation, heaviest first
+    const uint32_t* tile_order;       // in (NULL = row-major): work units (SF_UNIT_*), heaviest first
+    const uint32_t* order_meta;       // with tile_order: [0] units in it, [1] first split bucket
     uint32_t* chunk_cnt;              // out (with tile_cost): per 64-tile chunk, cost-bucket histogram
     uint32_t packet_lanes;            // frame-less mode: 8 (AVX variant) or 4 (SSE variant, 2x2 footprint)
     uint32_t prio_tiles;              // order positions traced at raised wave priority (s_setprio)
@@ -120,6 +125,14 @@ struct PostArgs {
 };
 
 #define SF_ORDER_BUCKETS 32u           // log-spaced cost buckets of sf_tile_order (2 per octave from 2^8 cycles)
+// A work unit of the tile order: tile index | half << SF_UNIT_HALF_SHIFT. Half 0 = the whole 8x8 tile;
+// 1, 2 = its pixel rows 0-3 / 4-7 (the heaviest tiles are traced as two half units by two waves:
+// a tile's serial DFS otherwise bounds the frame).
+#define SF_UNIT_HALF_SHIFT 30u
+#define SF_UNIT_TILE_MASK ((1u << SF_UNIT_HALF_SHIFT) - 1u)
+// Tiles in the top this-many occupied cost buckets are split (env SF_SPLIT_BUCKETS). Off by default:
+// measured slower at 1920x1080 K=0.25 (1 bucket +1.5 %, 2 buckets +3.5 % frame time).
+#define SF_SPLIT_BUCKETS_DEFAULT 0u
 
 namespace sfhost {
 void child_transforms(float child[9][16]);

@@ -315,7 +315,7 @@ template <int PW>   // packet width of the semantics: 0 per ray, 8 (AVX) or 4 (S
 __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ Lbase,
                                          uint32_t levels, float dx, float dy, float dz, bool valid, HitState& h,
                                          int32_t& maxd, bool& overflowed, uint32_t K_flags,
-                                         uint64_t* phase_sums = nullptr)
+                                         uint64_t* phase_sums = nullptr, uint32_t axl = 36u)
 {
     constexpr bool PACKET = PW != 0;
     const uint32_t lane = threadIdx.x & 63u;
@@ -345,13 +345,14 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     if (!wave_ballot(ex0)) return;
     maxd = 0;
 
-    // ---- the wave's ray cone: axis = lane 36's direction (pixel (4, 4) of the tile), sinT bounds the
+    // ---- the wave's ray cone: axis = lane axl's direction (pixel (4, 4) of the tile), sinT bounds the
     // sine of every lane's angle to it (|d x a| with |d|, |a| = 1 +- 2^-20, plus 2^-16 slack). A wide
     // cone (scattered packets of the frame-less mode, or sinT >= 1/2) disables the child cone cull
     // below through cosT = 0, sinT = 1.
     // Kept in LDS (read with the node in expand): as uniform registers they would spill SGPRs.
     {
-    const float ax = readlane_f(dx, 36u), ay = readlane_f(dy, 36u), az = readlane_f(dz, 36u);
+    // (half units: axl = the centre pixel of the traced half, (4, 2) or (4, 6))
+    const float ax = readlane_f(dx, axl), ay = readlane_f(dy, axl), az = readlane_f(dz, axl);
     float cosT = 0.0f, sinT = 1.0f;
     if (cone_cull) {
         const float cx_ = dy * az - dz * ay, cy_ = dz * ax - dx * az, cz_ = dx * ay - dy * ax;
@@ -620,7 +621,7 @@ struct Tile {
 };
 
 // Tile of a wave: owned tile row k (band sharding) -> frame tile row.
-__device__ __forceinline__ Tile tile_of(const FrameArgs& a, uint32_t tile, uint32_t lane)
+__device__ __forceinline__ Tile tile_of(const FrameArgs& a, uint32_t tile, uint32_t lane, uint32_t half = 0u)
 {
     const uint32_t tx = tile % a.tiles_x, k = tile / a.tiles_x;
     const uint32_t band = a.band_index + (k / a.tiles_per_band) * a.band_count;
@@ -632,7 +633,8 @@ __device__ __forceinline__ Tile tile_of(const FrameArgs& a, uint32_t tile, uint3
     Tile t;
     t.x = tx * SF_TILE + (l & 7u);
     t.y = ty * SF_TILE + (l >> 3);
-    t.valid = t.x < a.W && t.y < a.H;
+    // half unit: only the lanes of pixel rows 0-3 (half 1) or 4-7 (half 2) take part
+    t.valid = t.x < a.W && t.y < a.H && (half == 0u || (l >> 5) + 1u == half);
     t.orow = a.compact ? (k * SF_TILE + (l >> 3)) : t.y;
     return t;
 }
@@ -706,11 +708,13 @@ __device__ __forceinline__ uint32_t cost_bucket(uint32_t c)
 
 template <bool FIXUP>
 __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __restrict__ L, uint32_t tile,
-                                                uint32_t levels, uint32_t* overflow_list, uint32_t* overflow_count)
+                                                uint32_t levels, uint32_t* overflow_list, uint32_t* overflow_count,
+                                                uint32_t half = 0u)
 {
     const DeviceConsts* __restrict__ K = a.consts;
     const uint32_t lane = threadIdx.x & 63u;
-    const Tile t = tile_of(a, tile, lane);
+    if (a.flags & SF_FLAG_DIAG_HALF) half = (a.flags & SF_FLAG_DIAG_HALF_SEL) ? 2u : 1u;
+    const Tile t = tile_of(a, tile, lane, half);
     const uint64_t t_start = a.tile_trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint64_t c_start = (!FIXUP && a.tile_cost) ? __builtin_amdgcn_s_memtime() : 0ull;
     float dx, dy, dz;
@@ -720,7 +724,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     int32_t maxd = -1;
     bool overflowed = false;
     traverse<0>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed, a.flags,
-                    FIXUP ? nullptr : a.phase_sums);
+                    FIXUP ? nullptr : a.phase_sums, half == 0u ? 36u : half == 1u ? 20u : 52u);
     if (!FIXUP && a.tile_trace) {
         // diagnostics only: never read by the kernel, never feeds an output value. Every lane stores
         // the same (uniform) words: no lane-0-only region.
@@ -734,9 +738,10 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
         a.tile_trace[3u * tile + 2u] = ((uint64_t)xcc << 32) | hw;
     }
 
-    if (!FIXUP && a.tile_cost) {
-        // scheduling hint for the next render (sf_order_scan / sf_order_scatter); uniform values
-        const uint64_t cyc = __builtin_amdgcn_s_memtime() - c_start;
+    if (!FIXUP && a.tile_cost && half <= 1u) {
+        // scheduling hint for the next render (sf_order_scan / sf_order_scatter); uniform values.
+        // A split tile is counted once, by its first half, at twice that half's cost.
+        const uint64_t cyc = (__builtin_amdgcn_s_memtime() - c_start) << (half ? 1u : 0u);
         const uint32_t cost = cyc > 0xffffffffull ? 0xffffffffu : (uint32_t)cyc;
         a.tile_cost[tile] = cost;
         const uint32_t slot = __builtin_amdgcn_readfirstlane((tile >> 6) * SF_ORDER_BUCKETS + cost_bucket(cost));
@@ -821,6 +826,17 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
     if (blockIdx.x == 0 && threadIdx.x == 0) a.counters[a.parity ^ 1u] = 0u;   // and overflow count
     float* const L = lds + wv * SF_LDS_WAVE_FLOATS(a.max_depth);
     const uint32_t ntiles = a.tiles_x * a.tile_rows;
+    // work units: tiles in row-major order, or the previous render's heavy-first order in which the
+    // heaviest tiles come as two half units (order_meta[0] entries)
+    uint32_t nunits = ntiles;
+    if (a.tile_order) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        typedef const __attribute__((address_space(4))) uint32_t* ConstU32;
+        nunits = ((ConstU32)(const void*)a.order_meta)[0];
+#else
+        nunits = a.order_meta[0];
+#endif
+    }
     stage_root(L, a.root);
     uint32_t xcc;
     __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -843,25 +859,27 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
         at = a;
 #endif
         const uint32_t q = wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u);   // uniform
-        const uint32_t g = q * SF_QUEUES + k;   // position in the render's tile order
-        if (g >= ntiles) {        // queue k is empty: the next one; done when all are
+        const uint32_t g = q * SF_QUEUES + k;   // position in the render's unit order
+        if (g >= nunits) {        // queue k is empty: the next one; done when all are
             if (++dry == SF_QUEUES) break;
             k = (k + 1u) & (SF_QUEUES - 1u);
             continue;
         }
-        uint32_t t = g;
+        uint32_t t = g, half = 0u;
         if (at.tile_order) {      // heaviest tiles of the previous render first (scalar load)
 #if defined(__HIP_DEVICE_COMPILE__)
             typedef const __attribute__((address_space(4))) uint32_t* ConstU32;
-            t = ((ConstU32)(const void*)at.tile_order)[g];
+            const uint32_t u = ((ConstU32)(const void*)at.tile_order)[g];
 #else
-            t = at.tile_order[g];
+            const uint32_t u = at.tile_order[g];
 #endif
+            t = u & SF_UNIT_TILE_MASK;
+            half = u >> SF_UNIT_HALF_SHIFT;
         }
         // the heaviest tiles of the previous render bound the frame: give their waves issue priority
         const bool prio = at.tile_order && g < at.prio_tiles;
         if (prio) __builtin_amdgcn_s_setprio(3);
-        const TileStats st = trace_tile<false>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity);
+        const TileStats st = trace_tile<false>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity, half);
         if (prio) __builtin_amdgcn_s_setprio(0);
         maxd = st.maxd > maxd ? st.maxd : maxd;
         closest = fminf(closest, st.closest);
@@ -892,7 +910,9 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #define SF_SCAN_BATCH 16   // chunk counts a scan thread loads at once (independent loads, one wait)
 
 extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t* __restrict__ chunk_cnt, uint32_t nc,
-                                                                   uint32_t* __restrict__ chunk_off)
+                                                                   uint32_t n_tiles, uint32_t split_buckets,
+                                                                   uint32_t* __restrict__ chunk_off,
+                                                                   uint32_t* __restrict__ order_meta)
 {
     // thread = (bucket b = tid % 32, slice k = tid / 32): chunks [k * per, (k + 1) * per) of bucket b
     __shared__ uint32_t part[32][SF_ORDER_BUCKETS + 1];
@@ -919,16 +939,31 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t*
         tot[tid] = acc;
     }
     __syncthreads();
-    if (tid == 0) {   // bucket totals -> exclusive offsets, heaviest bucket first
+    __shared__ uint32_t split_from;
+    if (tid == 0) {
+        // Split the tiles of the top `split_buckets` occupied buckets (at most an eighth of the tiles)
+        // into two half units each. Then bucket totals (in units) -> exclusive offsets, heaviest first.
+        int bmax = (int)SF_ORDER_BUCKETS - 1;
+        while (bmax > 0 && tot[bmax] == 0u) --bmax;
+        int bs = bmax - (int)split_buckets + 1;
+        if (bs < 1) bs = 1;
+        if (split_buckets == 0u) bs = (int)SF_ORDER_BUCKETS;
+        uint32_t nsplit = 0u;
+        for (int bb = bs; bb < (int)SF_ORDER_BUCKETS; ++bb) nsplit += tot[bb];
+        while (bs < (int)SF_ORDER_BUCKETS && 8u * nsplit > n_tiles) nsplit -= tot[bs++];
+        split_from = (uint32_t)bs;
         uint32_t acc = 0u;
         for (int bb = (int)SF_ORDER_BUCKETS - 1; bb >= 0; --bb) {
-            const uint32_t x = tot[bb];
+            const uint32_t x = tot[bb] * (bb >= bs ? 2u : 1u);
             tot[bb] = acc;
             acc += x;
         }
+        order_meta[0] = acc;            // units of the next render
+        order_meta[1] = (uint32_t)bs;   // first split bucket
     }
     __syncthreads();
-    uint32_t off = tot[b] + part[k][b];
+    const uint32_t mult = b >= split_from ? 2u : 1u;
+    uint32_t off = tot[b] + part[k][b] * mult;
     for (uint32_t cb = c0; cb < c1; cb += SF_SCAN_BATCH) {
         uint32_t v[SF_SCAN_BATCH];
 #pragma unroll
@@ -936,7 +971,7 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t*
 #pragma unroll
         for (int j = 0; j < SF_SCAN_BATCH; ++j) {
             if (cb + j < c1) chunk_off[(cb + j) * SF_ORDER_BUCKETS + b] = off;
-            off += v[j];
+            off += v[j] * mult;
         }
     }
 }
@@ -944,9 +979,11 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t*
 extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t* __restrict__ cost, uint32_t n,
                                                                     uint32_t* __restrict__ chunk_cnt,
                                                                     const uint32_t* __restrict__ chunk_off,
+                                                                    const uint32_t* __restrict__ order_meta,
                                                                     uint32_t* __restrict__ order)
 {
     const uint32_t c = blockIdx.x, lane = threadIdx.x, i = c * 64u + lane;
+    const uint32_t split_from = order_meta[1];
     const uint32_t bk = i < n ? cost_bucket(cost[i]) : SF_ORDER_BUCKETS;   // sentinel: no tile
     const uint32_t offs = chunk_off[c * SF_ORDER_BUCKETS + (lane & (SF_ORDER_BUCKETS - 1u))];   // lane b: bucket b
     uint64_t pending = __builtin_amdgcn_ballot_w64(bk < SF_ORDER_BUCKETS);
@@ -954,8 +991,15 @@ extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t
         const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)bk, (int)__builtin_ctzll(pending));
         const uint64_t m = __builtin_amdgcn_ballot_w64(bk == b);
         const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)offs, (int)b);
-        if (bk == b)
-            order[off + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = i;
+        if (bk == b) {
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (b >= split_from) {   // two half units, adjacent
+                order[off + 2u * rank] = i | (1u << SF_UNIT_HALF_SHIFT);
+                order[off + 2u * rank + 1u] = i | (2u << SF_UNIT_HALF_SHIFT);
+            } else {
+                order[off + rank] = i;
+            }
+        }
         pending &= ~m;
     }
     if (lane < SF_ORDER_BUCKETS) chunk_cnt[c * SF_ORDER_BUCKETS + lane] = 0u;   // for the next render

@@ -475,17 +475,17 @@ class Sphereflake:
         return out[:3 * n].reshape(n, 3)
 
     def tile_order(self):
-        """Heavy-first schedule: (order, cost) uint32 arrays over the 8x8 tiles -- the permutation the
-        next persistent render takes tiles in, and the last render's per-tile shader cycles it was
+        """Heavy-first schedule: (units, cost) uint32 arrays -- the work units (tile | half << 30) the
+        next persistent render takes in order, and the last render's per-tile shader cycles they were
         computed from -- or None before any ordered render."""
         n = ((self.width + 7) // 8) * ((self.height + 7) // 8)
-        order = np.zeros(n, np.uint32)
+        order = np.zeros(2 * n, np.uint32)
         cost = np.zeros(n, np.uint32)
         P = ctypes.POINTER(ctypes.c_uint32)
-        k = lib().sf_get_tile_order(self._ctx, order.ctypes.data_as(P), cost.ctypes.data_as(P), n)
+        k = lib().sf_get_tile_order(self._ctx, order.ctypes.data_as(P), cost.ctypes.data_as(P), 2 * n)
         if k < 0:
             _check(k, "sf_get_tile_order", self._ctx)
-        return (order, cost) if k else None
+        return (order[:k], cost) if k else None
 
     def kernel_timing(self, enable: bool | None = None, n: int = 64, period: int = 1):
         """Measurement: enable HIP events around the main trace kernel of every `period`-th render, or

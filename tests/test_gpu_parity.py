@@ -331,20 +331,74 @@ def cost_bucket(c):
     return np.where((b >= 0) & (b < 32), b, np.where(k < (135 << 1), 0, 31))
 
 
-@pytest.mark.parametrize("W,H", [(1920, 1080), (3840, 2160), (100, 60)])
-def test_tile_order_is_stable_heavy_first_permutation(W, H):
-    """The next render's tile order (sf_order_scan + sf_order_scatter) is a permutation of the tiles,
-    non-increasing in cost bucket and in tile order within a bucket: exactly the stable sort of the
-    last render's tile costs by bucket, heaviest first."""
+def expected_units(cost, split_buckets):
+    """Host restatement of sf_order_scan + sf_order_scatter: tiles stably sorted by cost bucket, heaviest
+    first; the tiles of the top `split_buckets` occupied buckets (bucket >= 1, at most an eighth of the
+    tiles) become two adjacent half units (tile | 1 << 30, tile | 2 << 30)."""
+    n = len(cost)
+    bk = cost_bucket(cost)
+    cnt = np.bincount(bk, minlength=32)
+    nz = np.nonzero(cnt[1:])[0]
+    bmax = int(nz[-1]) + 1 if len(nz) else 0
+    bs = 32 if split_buckets == 0 else max(1, bmax - split_buckets + 1)
+    nsplit = int(cnt[bs:].sum())
+    while bs < 32 and 8 * nsplit > n:
+        nsplit -= int(cnt[bs])
+        bs += 1
+    units = []
+    for t in np.lexsort((np.arange(n), -bk)):
+        if bk[t] >= bs:
+            units += [t | (1 << 30), t | (2 << 30)]
+        else:
+            units.append(t)
+    return np.array(units, np.uint32), nsplit
+
+
+@pytest.mark.parametrize("W,H,split", [(1920, 1080, None), (1920, 1080, 1), (1920, 1080, 3), (3840, 2160, 1),
+                                       (100, 60, 1)])
+def test_tile_order_is_stable_heavy_first_schedule(W, H, split, monkeypatch):
+    """The next render's work units (sf_order_scan + sf_order_scatter) are exactly the stable sort of
+    the last render's tile costs by bucket, heaviest first, with the heaviest tiles as half units: every
+    tile covered once (whole, or both halves)."""
+    if split is not None:
+        monkeypatch.setenv("SF_SPLIT_BUCKETS", str(split))
     n = ((W + 7) // 8) * ((H + 7) // 8)
     with sf.Sphereflake(W, H) as s:
         s.SetCamera(sf.config_camera(W, H, 0.25))
         assert s.tile_order() is None
         s.Render()
-        order, cost = s.tile_order()
-    assert np.array_equal(np.sort(order), np.arange(n, dtype=np.uint32))
-    bk = cost_bucket(cost)[order]
-    assert np.all(np.diff(bk) <= 0)
-    assert np.all(np.diff(order.astype(np.int64))[np.diff(bk) == 0] > 0)
-    exp = np.lexsort((np.arange(n), -cost_bucket(cost)))
-    assert np.array_equal(order, exp.astype(np.uint32))
+        units, cost = s.tile_order()
+    exp, nsplit = expected_units(cost, 0 if split is None else split)
+    assert np.array_equal(units, exp)
+    assert len(units) == n + nsplit
+    tiles, half = units & ((1 << 30) - 1), units >> 30
+    assert np.array_equal(np.sort(tiles[half <= 1]), np.arange(n, dtype=np.uint32))
+    assert np.array_equal(np.sort(tiles[half == 1]), np.sort(tiles[half == 2]))
+    if split is None:
+        assert nsplit == 0   # default: no split
+    elif W == 1920:
+        assert nsplit > 0
+
+
+def test_split_render_bit_exact_and_stable():
+    """With half units in the schedule (renders 2+), c3 stays bit-exact, splitting the heaviest bucket
+    and with every tile split-eligible (SF_SPLIT_BUCKETS=32: the cap of one eighth of the tiles applies)."""
+    fx = load_frame("c3")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    import os
+    for split in ("1", "32"):
+        os.environ["SF_SPLIT_BUCKETS"] = split
+        try:
+            with sf.Sphereflake(W, H) as s:
+                s.SetCamera(sf.config_camera(W, H, K))
+                for k in range(3):
+                    s.Render(emit_aux=True)
+                    pos, nrm, mint, idx = s.download(aux=True)
+                    assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == [], f"split {split} render {k}"
+                    assert bad_rows(fx["row_digest_aux"], aux_digests(mint, idx)) == [], f"split {split} render {k}"
+                units, _ = s.tile_order()
+                st = s.stats()
+            assert (units >> 30).max() == 2
+            assert st.max_depth == fx["stats"]["max_depth"] and st.overflow_tiles == 0
+        finally:
+            del os.environ["SF_SPLIT_BUCKETS"]
