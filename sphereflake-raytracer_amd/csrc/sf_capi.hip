@@ -23,7 +23,8 @@ extern "C" __global__ void sf_trace_queue1(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2(FrameArgs a);
 extern "C" __global__ void sf_trace_queue4(FrameArgs a);
 extern "C" __global__ void sf_order_scan(const uint32_t* chunk_cnt, uint32_t nc, uint32_t n_tiles,
-                                         uint32_t split_buckets, uint32_t* chunk_off, uint32_t* order_meta);
+                                         uint32_t split_buckets, uint32_t spare, uint32_t* chunk_off,
+                                         uint32_t* order_meta);
 extern "C" __global__ void sf_order_scatter(const uint32_t* cost, uint32_t n, uint32_t* chunk_cnt,
                                             const uint32_t* chunk_off, const uint32_t* order_meta, uint32_t* order);
 extern "C" __global__ void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list, uint32_t* counters,
@@ -118,7 +119,7 @@ struct sf_ctx {
     uint32_t* chunk_cnt = nullptr;     // per 64-tile chunk x SF_ORDER_BUCKETS (zeroed by sf_order_scatter)
     uint32_t* chunk_off = nullptr;
     uint32_t* order_meta = nullptr;    // [0] work units in tile_order, [1] first split bucket
-    uint32_t split_buckets = SF_SPLIT_BUCKETS_DEFAULT;   // env SF_SPLIT_BUCKETS (0: never split)
+    uint32_t split_buckets = SF_SPLIT_AUTO;   // env SF_SPLIT_BUCKETS = k: top k buckets (0: never split)
     uint32_t order_n = 0;              // tile count the current tile_order is a permutation of (0: none)
     hipStream_t order_stream = nullptr;   // the stream it was computed on (used only on the same stream)
     bool use_order = true;             // env SF_ORDER=0: row-major order always
@@ -479,7 +480,9 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 c->occ_key = key;
             }
             uint32_t nblk = (uint32_t)c->occ_blocks * (uint32_t)c->cus;
-            const uint32_t need = (ntiles + wpb - 1) / wpb;
+            // work units: tiles, or up to 2 per tile when the schedule may split tiles into halves
+            const uint32_t units_max = (c->use_order && c->split_buckets != 0u) ? 2u * ntiles : ntiles;
+            const uint32_t need = (units_max + wpb - 1) / wpb;
             if (nblk > need) nblk = need;
             if (c->max_blocks && nblk > c->max_blocks) nblk = c->max_blocks;
             const dim3 grid(nblk);
@@ -504,8 +507,10 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             }
             if (c->use_order) {   // the next render's tile order, from this render's tile costs
                 const uint32_t nc = (ntiles + 63u) / 64u;
+                const uint32_t waves = nblk * wpb;   // resident waves of the persistent grid
+                const uint32_t spare = waves > ntiles ? waves - ntiles : 0u;
                 hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->chunk_cnt, nc, ntiles,
-                                   c->split_buckets, c->chunk_off, c->order_meta);
+                                   c->split_buckets, spare, c->chunk_off, c->order_meta);
                 SF_HIP(c, hipGetLastError());
                 hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost, ntiles,
                                    c->chunk_cnt, (const uint32_t*)c->chunk_off, (const uint32_t*)c->order_meta,

@@ -130,9 +130,12 @@ struct PostArgs {
 // a tile's serial DFS otherwise bounds the frame).
 #define SF_UNIT_HALF_SHIFT 30u
 #define SF_UNIT_TILE_MASK ((1u << SF_UNIT_HALF_SHIFT) - 1u)
-// Tiles in the top this-many occupied cost buckets are split (env SF_SPLIT_BUCKETS). Off by default:
-// measured slower at 1920x1080 K=0.25 (1 bucket +1.5 %, 2 buckets +3.5 % frame time).
-#define SF_SPLIT_BUCKETS_DEFAULT 0u
+// Which tiles are split: env SF_SPLIT_BUCKETS = k splits the top k occupied cost buckets (at most an
+// eighth of the tiles). The default (SF_SPLIT_AUTO) splits only into idle wave slots: whole buckets,
+// heaviest first, while tiles + split tiles <= the persistent grid's waves. With more tiles than waves
+// (1920x1080: 32400 tiles, 7168 waves) nothing is split -- measured: splitting there costs +1.5-3.5 %;
+// at 640x360 (3600 tiles) it takes the frame from 0.198 to 0.144 ms.
+#define SF_SPLIT_AUTO 0xffffffffu
 
 namespace sfhost {
 void child_transforms(float child[9][16]);

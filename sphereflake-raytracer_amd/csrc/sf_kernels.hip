@@ -910,7 +910,7 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #define SF_SCAN_BATCH 16   // chunk counts a scan thread loads at once (independent loads, one wait)
 
 extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t* __restrict__ chunk_cnt, uint32_t nc,
-                                                                   uint32_t n_tiles, uint32_t split_buckets,
+                                                                   uint32_t n_tiles, uint32_t split_buckets, uint32_t spare,
                                                                    uint32_t* __restrict__ chunk_off,
                                                                    uint32_t* __restrict__ order_meta)
 {
@@ -941,16 +941,25 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t*
     __syncthreads();
     __shared__ uint32_t split_from;
     if (tid == 0) {
-        // Split the tiles of the top `split_buckets` occupied buckets (at most an eighth of the tiles)
-        // into two half units each. Then bucket totals (in units) -> exclusive offsets, heaviest first.
-        int bmax = (int)SF_ORDER_BUCKETS - 1;
-        while (bmax > 0 && tot[bmax] == 0u) --bmax;
-        int bs = bmax - (int)split_buckets + 1;
-        if (bs < 1) bs = 1;
-        if (split_buckets == 0u) bs = (int)SF_ORDER_BUCKETS;
+        // Split tiles into two half units each, heaviest buckets first (bucket 0 never): automatically
+        // as many whole buckets as fit into `spare` idle wave slots, or the top `split_buckets` occupied
+        // buckets (at most an eighth of the tiles). Then bucket totals (in units) -> exclusive offsets,
+        // heaviest first.
+        int bs = (int)SF_ORDER_BUCKETS;
         uint32_t nsplit = 0u;
-        for (int bb = bs; bb < (int)SF_ORDER_BUCKETS; ++bb) nsplit += tot[bb];
-        while (bs < (int)SF_ORDER_BUCKETS && 8u * nsplit > n_tiles) nsplit -= tot[bs++];
+        if (split_buckets == SF_SPLIT_AUTO) {
+            for (int bb = (int)SF_ORDER_BUCKETS - 1; bb >= 1 && nsplit + tot[bb] <= spare; --bb) {
+                nsplit += tot[bb];
+                bs = bb;
+            }
+        } else if (split_buckets != 0u) {
+            int bmax = (int)SF_ORDER_BUCKETS - 1;
+            while (bmax > 0 && tot[bmax] == 0u) --bmax;
+            bs = bmax - (int)split_buckets + 1;
+            if (bs < 1) bs = 1;
+            for (int bb = bs; bb < (int)SF_ORDER_BUCKETS; ++bb) nsplit += tot[bb];
+            while (bs < (int)SF_ORDER_BUCKETS && 8u * nsplit > n_tiles) nsplit -= tot[bs++];
+        }
         split_from = (uint32_t)bs;
         uint32_t acc = 0u;
         for (int bb = (int)SF_ORDER_BUCKETS - 1; bb >= 0; --bb) {

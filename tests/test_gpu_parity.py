@@ -331,20 +331,29 @@ def cost_bucket(c):
     return np.where((b >= 0) & (b < 32), b, np.where(k < (135 << 1), 0, 31))
 
 
-def expected_units(cost, split_buckets):
+def expected_units(cost, split_buckets, spare=0):
     """Host restatement of sf_order_scan + sf_order_scatter: tiles stably sorted by cost bucket, heaviest
-    first; the tiles of the top `split_buckets` occupied buckets (bucket >= 1, at most an eighth of the
-    tiles) become two adjacent half units (tile | 1 << 30, tile | 2 << 30)."""
+    first; split tiles become two adjacent half units (tile | 1 << 30, tile | 2 << 30). split_buckets
+    None (auto): whole buckets from the heaviest while the split count fits `spare` idle waves; k: the
+    top k occupied buckets, at most an eighth of the tiles. Bucket 0 is never split."""
     n = len(cost)
     bk = cost_bucket(cost)
     cnt = np.bincount(bk, minlength=32)
-    nz = np.nonzero(cnt[1:])[0]
-    bmax = int(nz[-1]) + 1 if len(nz) else 0
-    bs = 32 if split_buckets == 0 else max(1, bmax - split_buckets + 1)
-    nsplit = int(cnt[bs:].sum())
-    while bs < 32 and 8 * nsplit > n:
-        nsplit -= int(cnt[bs])
-        bs += 1
+    bs, nsplit = 32, 0
+    if split_buckets is None:
+        for b in range(31, 0, -1):
+            if nsplit + cnt[b] > spare:
+                break
+            nsplit += int(cnt[b])
+            bs = b
+    elif split_buckets:
+        nz = np.nonzero(cnt[1:])[0]
+        bmax = int(nz[-1]) + 1 if len(nz) else 0
+        bs = max(1, bmax - split_buckets + 1)
+        nsplit = int(cnt[bs:].sum())
+        while bs < 32 and 8 * nsplit > n:
+            nsplit -= int(cnt[bs])
+            bs += 1
     units = []
     for t in np.lexsort((np.arange(n), -bk)):
         if bk[t] >= bs:
@@ -355,7 +364,7 @@ def expected_units(cost, split_buckets):
 
 
 @pytest.mark.parametrize("W,H,split", [(1920, 1080, None), (1920, 1080, 1), (1920, 1080, 3), (3840, 2160, 1),
-                                       (100, 60, 1)])
+                                       (100, 60, 1), (100, 60, None), (640, 360, None)])
 def test_tile_order_is_stable_heavy_first_schedule(W, H, split, monkeypatch):
     """The next render's work units (sf_order_scan + sf_order_scatter) are exactly the stable sort of
     the last render's tile costs by bucket, heaviest first, with the heaviest tiles as half units: every
@@ -368,15 +377,21 @@ def test_tile_order_is_stable_heavy_first_schedule(W, H, split, monkeypatch):
         assert s.tile_order() is None
         s.Render()
         units, cost = s.tile_order()
-    exp, nsplit = expected_units(cost, 0 if split is None else split)
+    if split is None:   # auto: recover the idle-wave count from the split made (<= spare < next bucket)
+        n_split = len(units) - n
+        exp, nsplit = expected_units(cost, None, n_split)
+    else:
+        exp, nsplit = expected_units(cost, split)
     assert np.array_equal(units, exp)
     assert len(units) == n + nsplit
     tiles, half = units & ((1 << 30) - 1), units >> 30
     assert np.array_equal(np.sort(tiles[half <= 1]), np.arange(n, dtype=np.uint32))
     assert np.array_equal(np.sort(tiles[half == 1]), np.sort(tiles[half == 2]))
-    if split is None:
-        assert nsplit == 0   # default: no split
-    elif W == 1920:
+    if split is None and W * H >= 1920 * 1080:
+        assert nsplit == 0   # auto: more tiles than resident waves, nothing split
+    elif split is None and W * H <= 100 * 60:
+        assert nsplit == np.count_nonzero(cost_bucket(cost) >= 1)   # few tiles: every splittable one
+    else:
         assert nsplit > 0
 
 
