@@ -1,0 +1,55 @@
+"""GPU parity on seeded random views (beyond the fixed BASELINE cameras): random camera position
+(scale K log-uniform over [0.12, 2.5], inside and outside the flake's bounding ball), pitch, yaw,
+roll, FOV and frame sizes that are not multiples of the 8x8 tile, both reference variants (AVX LOD 70,
+SSE LOD 60). Each view is rendered three times -- row-major, then heavy-first, then with the heavy-
+first schedule's half units where the frame leaves idle waves -- and every render must equal the oracle
+restatement (oracle/sf_oracle.c, pinned to the reference build by tests/golden) bit for bit in
+position, normal, t and heap hit index. Camera setup (a1-a3) comes from the library, as in the
+product path; its bit-exactness against the reference dump is tests/test_host.py's job."""
+import numpy as np
+import pytest
+
+import sphereflake_amd as sf
+from oracle import pyoracle
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [(72, 40), (61, 37), (96, 54), (33, 70), (128, 72)]
+
+
+def random_view(rng, k):
+    W, H = SIZES[k % len(SIZES)]
+    cam = sf.Camera(W, H)
+    K = float(np.exp(rng.uniform(np.log(0.12), np.log(2.5))))
+    cam.SetPosition(np.asarray(sf.DEFAULT_CAMERA_POSITION, np.float32) * np.float32(K)
+                    + rng.normal(0.0, 0.15 * K, 3).astype(np.float32))
+    cam.SetPitch(np.float32(sf.DEFAULT_PITCH + rng.uniform(-0.4, 0.4)))
+    cam.SetYaw(np.float32(sf.DEFAULT_YAW + rng.uniform(-0.6, 0.6)))
+    cam.SetRoll(np.float32(rng.uniform(-0.3, 0.3)))
+    cam.SetFOV(float(rng.choice([45.0, 60.0, 90.0])))
+    return W, H, K, cam
+
+
+@pytest.mark.parametrize("variant", ["avx", "sse"])
+@pytest.mark.parametrize("seed", range(16))
+def test_random_view_bit_exact(seed, variant):
+    rng = np.random.default_rng(1000 + seed)
+    W, H, K, cam = random_view(rng, seed)
+    o, tl, tr, bl = cam.corners()
+    setup = {"W": W, "H": H, "origin": o, "tl": tl, "tr": tr, "bl": bl,
+             "root": sf.root_transform(o), "children": sf.child_transforms()}
+    ref = pyoracle.render(setup, lod=70.0 if variant == "avx" else 60.0)
+    with sf.Sphereflake(W, H) as s:
+        s.SetVariant(variant)
+        s.SetView(o, tl, tr, bl)
+        for k in range(3):
+            s.Render(emit_aux=True)
+            pos, nrm, mint, idx = s.download(aux=True)
+            what = f"seed {seed} {variant} {W}x{H} K={K:.3f} render {k}"
+            assert np.array_equal(idx, ref["index"]), what
+            assert np.array_equal(pos.view(np.uint32), ref["pos4"].view(np.uint32)), what
+            assert np.array_equal(nrm.view(np.uint32), ref["nrm4"].view(np.uint32)), what
+            assert np.array_equal(mint.view(np.uint32), ref["minT"].view(np.uint32)), what
+        st = s.stats()
+    assert st.max_depth == ref["stats"]["max_depth"]
+    assert np.float32(st.closest) == np.float32(ref["stats"]["closest"])
