@@ -36,10 +36,17 @@ extern "C" __global__ void sf_post_final(PostArgs a);
 extern "C" __global__ void sf_post_fused(PostArgs a);
 extern "C" __global__ void sf_mt_draws(uint32_t* state, uint32_t* out, uint32_t n);
 extern "C" __global__ void sf_progressive_trace(FrameArgs a, const uint32_t* draws, uint64_t counter0, uint32_t packets,
-                                                uint64_t ticket0, PacketLane* lanes, unsigned long long* owner);
+                                                uint64_t ticket0, PacketLane* lanes, unsigned long long* owner,
+                                                const uint32_t* perm);
+extern "C" __global__ void sf_packet_bin(FrameArgs a, const uint32_t* draws, uint64_t counter0, uint32_t packets,
+                                         uint32_t pw, uint32_t bin_shift, uint32_t bins_x, uint32_t* bin_cnt);
+extern "C" __global__ void sf_packet_scan(uint32_t* bin_cnt, uint32_t nbins);
+extern "C" __global__ void sf_packet_place(FrameArgs a, const uint32_t* draws, uint64_t counter0, uint32_t packets,
+                                           uint32_t pw, uint32_t bin_shift, uint32_t bins_x, uint32_t* bin_cur,
+                                           uint32_t* perm);
 extern "C" __global__ void sf_progressive_trace_sse(FrameArgs a, const uint32_t* draws, uint64_t counter0,
                                                     uint32_t packets, uint64_t ticket0, PacketLane* lanes,
-                                                    unsigned long long* owner);
+                                                    unsigned long long* owner, const uint32_t* perm);
 extern "C" __global__ void sf_progressive_scatter(FrameArgs a, uint32_t packets, uint64_t ticket0,
                                                   const PacketLane* lanes, const unsigned long long* owner);
 
@@ -101,6 +108,9 @@ struct sf_ctx {
     uint32_t* draws = nullptr;         // 2 per packet
     PacketLane* lanes = nullptr;       // 8 per packet
     uint32_t prog_cap = 0;             // packets the scratch buffers hold
+    uint32_t* perm = nullptr;          // binned trace order of a batch (prog_cap)
+    uint32_t* bin_cnt = nullptr;       // SF_PROG_MAX_BINS packet-bin counters / cursors
+    bool prog_bin = true;              // env SF_PROG_BIN=0: trace packets in draw order
     unsigned long long* owner = nullptr;   // per pixel: highest ticket written
     bool prog_seeded = false;
     uint32_t prog_seed = 0;
@@ -164,6 +174,8 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->mt_state);
     (void)hipFree(c->draws);
     (void)hipFree(c->lanes);
+    (void)hipFree(c->perm);
+    (void)hipFree(c->bin_cnt);
     (void)hipFree(c->owner);
     if (c->h_depth) (void)hipHostFree(c->h_depth);
     (void)hipFree(c->tile_trace);
@@ -261,6 +273,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     c->cus = prop.multiProcessorCount;
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_ORDER")) c->use_order = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_PROG_BIN")) c->prog_bin = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_SPLIT_BUCKETS")) c->split_buckets = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_FLAGS")) c->flags = (uint32_t)std::strtoul(ev, nullptr, 0);
@@ -581,11 +594,14 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
         (void)hipStreamSynchronize(s);
         (void)hipFree(c->draws);
         (void)hipFree(c->lanes);
+        (void)hipFree(c->perm);
         c->draws = nullptr;
         c->lanes = nullptr;
+        c->perm = nullptr;
         c->prog_cap = 0;
         SF_HIP(c, hipMalloc(&c->draws, (size_t)packets * 2 * 4));
         SF_HIP(c, hipMalloc(&c->lanes, (size_t)packets * 8 * sizeof(PacketLane)));
+        SF_HIP(c, hipMalloc(&c->perm, (size_t)packets * 4));
         c->prog_cap = packets;
     }
     if (!c->prog_seeded || seed != c->prog_seed || counter0 != c->prog_next) {
@@ -611,15 +627,39 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     a.packet_lanes = pl;
     hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(1024), 0, s, c->mt_state, c->draws, 2 * packets);
     SF_HIP(c, hipGetLastError());
+    // Trace order: packets binned by a square of 2^shift pixels (about 8 per bin, a wave's worth of
+    // AVX packets), so a wave's packets share their traversal. Small batches: draw order.
+    const uint32_t* perm = nullptr;
+    if (c->prog_bin && packets >= SF_PROG_BIN_MIN) {
+        if (!c->bin_cnt) SF_HIP(c, hipMalloc(&c->bin_cnt, SF_PROG_MAX_BINS * 4));
+        uint32_t shift = 2u, bx = 0, by = 0;
+        for (;; ++shift) {
+            bx = (c->W + (1u << shift) - 1u) >> shift;
+            by = (c->H + (1u << shift) - 1u) >> shift;
+            const uint64_t nb = (uint64_t)bx * by;
+            if (nb <= SF_PROG_MAX_BINS && 8ull * nb <= packets) break;
+            if (shift == 30u) break;
+        }
+        const uint32_t nbins = bx * by;
+        const uint32_t pb = (packets + 255u) / 256u;
+        SF_HIP(c, hipMemsetAsync(c->bin_cnt, 0, (size_t)nbins * 4, s));
+        hipLaunchKernelGGL(sf_packet_bin, dim3(pb), dim3(256), 0, s, a, (const uint32_t*)c->draws, counter0, packets,
+                           pl, shift, bx, c->bin_cnt);
+        hipLaunchKernelGGL(sf_packet_scan, dim3(1), dim3(1024), 0, s, c->bin_cnt, nbins);
+        hipLaunchKernelGGL(sf_packet_place, dim3(pb), dim3(256), 0, s, a, (const uint32_t*)c->draws, counter0, packets,
+                           pl, shift, bx, c->bin_cnt, c->perm);
+        SF_HIP(c, hipGetLastError());
+        perm = c->perm;
+    }
     const uint32_t ppw = 64u / pl;                   // packets per wave
     const uint32_t waves = (packets + ppw - 1) / ppw;
     const size_t lds = (size_t)SF_LDS_WAVE_FLOATS(16) * 4;
     if (sse)
         hipLaunchKernelGGL(sf_progressive_trace_sse, dim3(waves), dim3(64), lds, s, a, (const uint32_t*)c->draws,
-                           counter0, packets, c->ticket, c->lanes, c->owner);
+                           counter0, packets, c->ticket, c->lanes, c->owner, perm);
     else
         hipLaunchKernelGGL(sf_progressive_trace, dim3(waves), dim3(64), lds, s, a, (const uint32_t*)c->draws,
-                           counter0, packets, c->ticket, c->lanes, c->owner);
+                           counter0, packets, c->ticket, c->lanes, c->owner, perm);
     SF_HIP(c, hipGetLastError());
     hipLaunchKernelGGL(sf_progressive_scatter, dim3((packets * pl + 255) / 256), dim3(256), 0, s, a, packets, c->ticket,
                        (const PacketLane*)c->lanes, (const unsigned long long*)c->owner);

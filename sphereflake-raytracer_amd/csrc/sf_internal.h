@@ -124,6 +124,9 @@ struct PostArgs {
     uint8_t* rgba;                    // final image, W x H x RGBA8, row j = G-buffer row j
 };
 
+#define SF_PROG_MAX_BINS 65536u        // frame-less mode: packet bins (counting sort in one workgroup)
+#define SF_PROG_BIN_MIN 65536u         // frame-less batches below this many packets trace in draw order
+                                       // (binning pays once the batch is several waves per slot)
 #define SF_ORDER_BUCKETS 32u           // log-spaced cost buckets of sf_tile_order (2 per octave from 2^8 cycles)
 // A work unit of the tile order: tile index | half << SF_UNIT_HALF_SHIFT. Half 0 = the whole 8x8 tile;
 // 1, 2 = its pixel rows 0-3 / 4-7 (the heaviest tiles are traced as two half units by two waves:

@@ -1214,31 +1214,103 @@ __device__ __forceinline__ float sobol_sample(uint64_t index, const uint32_t* __
 // around (x0, y0) = 1 + floor(S (W - 2)), 1 + floor(S (H - 2)); the SSE footprint the 2x2 block at
 // (x0, y0) = floor(S (W - 1)), floor(S (H - 1)).
 template <int PW>
+__device__ __forceinline__ void packet_origin(const FrameArgs& a, const DeviceConsts* __restrict__ K,
+                                              const uint32_t* draws, uint64_t counter0, uint32_t packet,
+                                              float& x0, float& y0)
+{
+    const uint64_t c = counter0 + packet;
+    const float s0 = sobol_sample(c, K->sobol[0], draws[2u * packet]);
+    const float s1 = sobol_sample(c, K->sobol[1], draws[2u * packet + 1u]);
+    if constexpr (PW == 8) {
+        x0 = 1.0f + floorf(s0 * (float)(a.W - 2u));
+        y0 = 1.0f + floorf(s1 * (float)(a.H - 2u));
+    } else {
+        x0 = floorf(s0 * (float)(a.W - 1u));
+        y0 = floorf(s1 * (float)(a.H - 1u));
+    }
+}
+
+// Spatial binning of a batch's packets (the trace order only: results, tickets and the scatter are
+// per packet). The reference's packets land uniformly at random, so a wave of 64 / PW consecutive
+// packets shares almost no traversal; binned by a square of 2^bin_shift pixels around (x0, y0) they
+// share most of it. Counting sort: sf_packet_bin (histogram), sf_packet_scan (exclusive offsets,
+// one workgroup), sf_packet_place (slot by atomic cursor; order inside a bin is arbitrary).
+template <int PW>
+__device__ __forceinline__ uint32_t packet_bin(const FrameArgs& a, const DeviceConsts* __restrict__ K,
+                                               const uint32_t* draws, uint64_t counter0, uint32_t packet,
+                                               uint32_t bin_shift, uint32_t bins_x)
+{
+    float x0, y0;
+    packet_origin<PW>(a, K, draws, counter0, packet, x0, y0);
+    return ((uint32_t)y0 >> bin_shift) * bins_x + ((uint32_t)x0 >> bin_shift);
+}
+
+extern "C" __global__ __launch_bounds__(256) void sf_packet_bin(FrameArgs a, const uint32_t* draws, uint64_t counter0,
+                                                                 uint32_t packets, uint32_t pw, uint32_t bin_shift,
+                                                                 uint32_t bins_x, uint32_t* bin_cnt)
+{
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= packets) return;
+    const uint32_t b = pw == 8u ? packet_bin<8>(a, a.consts, draws, counter0, p, bin_shift, bins_x)
+                                : packet_bin<4>(a, a.consts, draws, counter0, p, bin_shift, bins_x);
+    atomicAdd(bin_cnt + b, 1u);
+}
+
+extern "C" __global__ __launch_bounds__(1024) void sf_packet_scan(uint32_t* bin_cnt, uint32_t nbins)
+{
+    // thread t: bins [t * per, (t + 1) * per) -> exclusive offsets in place (the place cursors)
+    // (nbins <= SF_PROG_MAX_BINS = 64 x 1024: a thread's counts are loaded at once and kept)
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x, per = (nbins + 1023u) / 1024u, b0 = t * per, b1 = min(nbins, b0 + per);
+    uint32_t v[SF_PROG_MAX_BINS / 1024u];
+#pragma unroll
+    for (uint32_t j = 0; j < SF_PROG_MAX_BINS / 1024u; ++j) v[j] = b0 + j < b1 ? bin_cnt[b0 + j] : 0u;
+    uint32_t s_ = 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < SF_PROG_MAX_BINS / 1024u; ++j) s_ += v[j];
+    part[t] = s_;
+    __syncthreads();
+    for (uint32_t o = 1u; o < 1024u; o <<= 1) {   // inclusive Hillis-Steele scan of the partials
+        const uint32_t v = t >= o ? part[t - o] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t off = part[t] - s_;
+#pragma unroll
+    for (uint32_t j = 0; j < SF_PROG_MAX_BINS / 1024u; ++j) {
+        if (b0 + j < b1) bin_cnt[b0 + j] = off;
+        off += v[j];
+    }
+}
+
+extern "C" __global__ __launch_bounds__(256) void sf_packet_place(FrameArgs a, const uint32_t* draws, uint64_t counter0,
+                                                                   uint32_t packets, uint32_t pw, uint32_t bin_shift,
+                                                                   uint32_t bins_x, uint32_t* bin_cur, uint32_t* perm)
+{
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= packets) return;
+    const uint32_t b = pw == 8u ? packet_bin<8>(a, a.consts, draws, counter0, p, bin_shift, bins_x)
+                                : packet_bin<4>(a, a.consts, draws, counter0, p, bin_shift, bins_x);
+    perm[atomicAdd(bin_cur + b, 1u)] = p;
+}
+
+template <int PW>
 __device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint32_t* draws, uint64_t counter0,
                                                   uint32_t packets, uint64_t ticket0, PacketLane* lanes,
-                                                  unsigned long long* owner)
+                                                  unsigned long long* owner, const uint32_t* perm)
 {
     extern __shared__ float lds[];
     constexpr uint32_t PPW = 64u / PW;   // packets per wave
     const DeviceConsts* __restrict__ K = a.consts;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t packet = blockIdx.x * PPW + lane / PW;
+    const uint32_t slot = blockIdx.x * PPW + lane / PW;   // position in the (binned) trace order
     if (blockIdx.x * PPW >= packets) return;   // wave-uniform
-    const bool valid = packet < packets;
+    const bool valid = slot < packets;
+    const uint32_t packet = valid ? (perm ? perm[slot] : slot) : slot;
     const uint32_t q = lane % PW;
     float x0 = 0.f, y0 = 0.f;
-    if (valid) {
-        const uint64_t c = counter0 + packet;
-        const float s0 = sobol_sample(c, K->sobol[0], draws[2u * packet]);
-        const float s1 = sobol_sample(c, K->sobol[1], draws[2u * packet + 1u]);
-        if constexpr (PW == 8) {
-            x0 = 1.0f + floorf(s0 * (float)(a.W - 2u));
-            y0 = 1.0f + floorf(s1 * (float)(a.H - 2u));
-        } else {
-            x0 = floorf(s0 * (float)(a.W - 1u));
-            y0 = floorf(s1 * (float)(a.H - 1u));
-        }
-    }
+    if (valid) packet_origin<PW>(a, K, draws, counter0, packet, x0, y0);
     float ox, oy;
     if constexpr (PW == 8) {
         // xa = {x0, x0+1, x0+1, x0, x0, x0+1, x0-1, x0-1}, ya = {y0, y0+1, y0, y0+1, y0-1, y0-1, y0, y0-1}
@@ -1271,9 +1343,12 @@ __device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint
 
     const float closest = wave_min(inb ? h.minT : FLT_MAX);
     const bool anyov = wave_ballot(overflowed) != 0ull;
-    if (lane == 0u) {
-        if (maxd >= 0) atomicMax(&a.stats[0], maxd);
-        atomicMin(&a.stats[1], sf_float_key(closest));
+    if (lane == 0u) {   // read before the atomic: issued only when it changes the word (one address)
+        const int32_t key = sf_float_key(closest);
+        const int32_t cur_d = __hip_atomic_load(&a.stats[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int32_t cur_k = __hip_atomic_load(&a.stats[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (maxd > cur_d) atomicMax(&a.stats[0], maxd);
+        if (key < cur_k) atomicMin(&a.stats[1], key);
         if (anyov) atomicAdd(&a.stats[2], 1);
     }
 }
@@ -1281,16 +1356,16 @@ __device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint
 extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace(FrameArgs a, const uint32_t* draws,
                                                                        uint64_t counter0, uint32_t packets,
                                                                        uint64_t ticket0, PacketLane* lanes,
-                                                                       unsigned long long* owner)
+                                                                       unsigned long long* owner, const uint32_t* perm)
 {
-    progressive_trace<8>(a, draws, counter0, packets, ticket0, lanes, owner);
+    progressive_trace<8>(a, draws, counter0, packets, ticket0, lanes, owner, perm);
 }
 extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace_sse(FrameArgs a, const uint32_t* draws,
                                                                            uint64_t counter0, uint32_t packets,
                                                                            uint64_t ticket0, PacketLane* lanes,
-                                                                           unsigned long long* owner)
+                                                                           unsigned long long* owner, const uint32_t* perm)
 {
-    progressive_trace<4>(a, draws, counter0, packets, ticket0, lanes, owner);
+    progressive_trace<4>(a, draws, counter0, packets, ticket0, lanes, owner, perm);
 }
 
 // Last writer wins by ticket (= the reference worker's sequential packet order).
