@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <utility>
 
 #include "sf_internal.h"
 #include "sphereflake/sf.h"
@@ -111,6 +112,18 @@ struct sf_ctx {
     uint32_t* perm = nullptr;          // binned trace order of a batch (prog_cap)
     uint32_t* bin_cnt = nullptr;       // SF_PROG_MAX_BINS packet-bin counters / cursors
     bool prog_bin = true;              // env SF_PROG_BIN=0: trace packets in draw order
+    // Draw prefetch: after a large batch, the next batch's mt19937 draws (same stream, same size) are
+    // generated on pf_stream while this batch traces -- the generator is one sequential workgroup.
+    // A call that does not continue the stream restores the state saved before the prefetch.
+    uint32_t* draws_pf = nullptr;      // the prefetched draws (prog_cap x 2)
+    uint32_t* mt_saved = nullptr;      // MT state before the pending prefetch
+    hipStream_t pf_stream = nullptr;
+    hipEvent_t pf_done = nullptr;      // prefetch written (pf_stream)
+    hipEvent_t mt_ready = nullptr;     // this batch's draws generated on the render stream
+    hipEvent_t traced = nullptr;       // the last batch's trace done reading its draws
+    bool traced_valid = false;
+    uint32_t pf_packets = 0;           // draws pending for a batch of this many packets (0: none)
+    bool prog_prefetch = true;         // env SF_PROG_PREFETCH=0: off
     unsigned long long* owner = nullptr;   // per pixel: highest ticket written
     bool prog_seeded = false;
     uint32_t prog_seed = 0;
@@ -176,6 +189,13 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->lanes);
     (void)hipFree(c->perm);
     (void)hipFree(c->bin_cnt);
+    if (c->pf_stream) (void)hipStreamSynchronize(c->pf_stream);
+    (void)hipFree(c->draws_pf);
+    (void)hipFree(c->mt_saved);
+    if (c->pf_done) (void)hipEventDestroy(c->pf_done);
+    if (c->mt_ready) (void)hipEventDestroy(c->mt_ready);
+    if (c->traced) (void)hipEventDestroy(c->traced);
+    if (c->pf_stream) (void)hipStreamDestroy(c->pf_stream);
     (void)hipFree(c->owner);
     if (c->h_depth) (void)hipHostFree(c->h_depth);
     (void)hipFree(c->tile_trace);
@@ -274,6 +294,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_ORDER")) c->use_order = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_BIN")) c->prog_bin = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_PROG_PREFETCH")) c->prog_prefetch = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_SPLIT_BUCKETS")) c->split_buckets = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_FLAGS")) c->flags = (uint32_t)std::strtoul(ev, nullptr, 0);
@@ -590,15 +611,29 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
         SF_HIP(c, hipMalloc(&c->owner, (size_t)c->W * c->H * 8));
         SF_HIP(c, hipMemsetAsync(c->owner, 0, (size_t)c->W * c->H * 8, s));
     }
+    // a pending prefetch either is this batch's draws, or is undone (MT state restored)
+    bool prefetched = false;
+    if (c->pf_packets) {
+        SF_HIP(c, hipStreamWaitEvent(s, c->pf_done, 0));
+        if (c->pf_packets == packets && c->prog_seeded && seed == c->prog_seed && counter0 == c->prog_next) {
+            std::swap(c->draws, c->draws_pf);
+            prefetched = true;
+        } else {
+            SF_HIP(c, hipMemcpyAsync(c->mt_state, c->mt_saved, 625 * 4, hipMemcpyDeviceToDevice, s));
+        }
+        c->pf_packets = 0;
+    }
     if (packets > c->prog_cap) {
         (void)hipStreamSynchronize(s);
         (void)hipFree(c->draws);
+        (void)hipFree(c->draws_pf);
         (void)hipFree(c->lanes);
         (void)hipFree(c->perm);
-        c->draws = nullptr;
+        c->draws = c->draws_pf = nullptr;
         c->lanes = nullptr;
         c->perm = nullptr;
         c->prog_cap = 0;
+        c->traced_valid = false;
         SF_HIP(c, hipMalloc(&c->draws, (size_t)packets * 2 * 4));
         SF_HIP(c, hipMalloc(&c->lanes, (size_t)packets * 8 * sizeof(PacketLane)));
         SF_HIP(c, hipMalloc(&c->perm, (size_t)packets * 4));
@@ -625,8 +660,30 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     a.min_t = c->min_t;
     a.emit_aux = 1;
     a.packet_lanes = pl;
-    hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(1024), 0, s, c->mt_state, c->draws, 2 * packets);
-    SF_HIP(c, hipGetLastError());
+    if (!prefetched) {
+        hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(1024), 0, s, c->mt_state, c->draws, 2 * packets);
+        SF_HIP(c, hipGetLastError());
+    }
+    // Prefetch the next batch's draws (a continuing stream of the same batch size) on pf_stream, into
+    // the buffer the previous batch traced from, overlapped with this batch's trace.
+    if (c->prog_prefetch && packets >= SF_PROG_PREFETCH_MIN) {
+        if (!c->pf_stream) {
+            SF_HIP(c, hipStreamCreateWithFlags(&c->pf_stream, hipStreamNonBlocking));
+            SF_HIP(c, hipEventCreateWithFlags(&c->pf_done, hipEventDisableTiming));
+            SF_HIP(c, hipEventCreateWithFlags(&c->mt_ready, hipEventDisableTiming));
+            SF_HIP(c, hipEventCreateWithFlags(&c->traced, hipEventDisableTiming));
+            SF_HIP(c, hipMalloc(&c->mt_saved, 625 * 4));
+        }
+        if (!c->draws_pf) SF_HIP(c, hipMalloc(&c->draws_pf, (size_t)c->prog_cap * 2 * 4));
+        SF_HIP(c, hipEventRecord(c->mt_ready, s));                 // MT state advanced past this batch
+        SF_HIP(c, hipStreamWaitEvent(c->pf_stream, c->mt_ready, 0));
+        if (c->traced_valid) SF_HIP(c, hipStreamWaitEvent(c->pf_stream, c->traced, 0));   // draws_pf free
+        SF_HIP(c, hipMemcpyAsync(c->mt_saved, c->mt_state, 625 * 4, hipMemcpyDeviceToDevice, c->pf_stream));
+        hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(1024), 0, c->pf_stream, c->mt_state, c->draws_pf, 2 * packets);
+        SF_HIP(c, hipGetLastError());
+        SF_HIP(c, hipEventRecord(c->pf_done, c->pf_stream));
+        c->pf_packets = packets;
+    }
     // Trace order: packets binned by a square of 2^shift pixels (about 8 per bin, a wave's worth of
     // AVX packets), so a wave's packets share their traversal. Small batches: draw order.
     const uint32_t* perm = nullptr;
@@ -661,6 +718,10 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
         hipLaunchKernelGGL(sf_progressive_trace, dim3(waves), dim3(64), lds, s, a, (const uint32_t*)c->draws,
                            counter0, packets, c->ticket, c->lanes, c->owner, perm);
     SF_HIP(c, hipGetLastError());
+    if (c->pf_stream) {   // the next prefetch may overwrite this batch's draws after this point
+        SF_HIP(c, hipEventRecord(c->traced, s));
+        c->traced_valid = true;
+    }
     hipLaunchKernelGGL(sf_progressive_scatter, dim3((packets * pl + 255) / 256), dim3(256), 0, s, a, packets, c->ticket,
                        (const PacketLane*)c->lanes, (const unsigned long long*)c->owner);
     SF_HIP(c, hipGetLastError());

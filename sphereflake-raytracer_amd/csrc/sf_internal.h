@@ -125,6 +125,7 @@ struct PostArgs {
 };
 
 #define SF_PROG_MAX_BINS 65536u        // frame-less mode: packet bins (counting sort in one workgroup)
+#define SF_PROG_PREFETCH_MIN 65536u    // frame-less batches from this many packets prefetch the next draws
 #define SF_PROG_BIN_MIN 65536u         // frame-less batches below this many packets trace in draw order
                                        // (binning pays once the batch is several waves per slot)
 #define SF_ORDER_BUCKETS 32u           // log-spaced cost buckets of sf_tile_order (2 per octave from 2^8 cycles)

@@ -225,6 +225,44 @@ def test_progressive_reseed_skip_ahead():
     assert np.array_equal(nrm[w].view(np.uint32), enrm[w].view(np.uint32))
 
 
+@pytest.mark.parametrize("calls", [
+    [(0, 100000), (0, 100000)],                          # the second batch is the prefetched draws
+    [(0, 100000), (0, 50000), (0, 50000)],               # size changes: prefetch undone, state restored
+    [(0, 70000), (1, 10), (0, 130000)],                  # another stream in between: restore + reseed/skip
+    [(0, 70000), (0, 70000), (0, 60000)],                # two prefetch hits, then a smaller batch
+])
+def test_progressive_draw_prefetch_paths(calls, monkeypatch):
+    """Large batches prefetch the next batch's mt19937 draws on a side stream; whatever the next call
+    is, the frame equals the same calls with the prefetch off (SF_PROG_PREFETCH=0), and a p3-only
+    sequence equals the reference worker's p3 stream (200000 packets of mt19937(777))."""
+    fx = load_progressive("p3")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+
+    def run():
+        with sf.Sphereflake(W, H) as s:
+            s.SetCamera(sf.config_camera(W, H, K))
+            done = 0
+            for other, n in calls:
+                if other:
+                    s.Progressive(fx["seed"] + 1, n, counter0=3)
+                else:
+                    s.Progressive(fx["seed"], n, counter0=done)
+                    done += n
+            assert done == fx["packets"]
+            pos, nrm, _, _ = s.download()
+            return pos, nrm, s.stats()
+
+    pos, nrm, st = run()
+    monkeypatch.setenv("SF_PROG_PREFETCH", "0")
+    epos, enrm, est = run()
+    assert np.array_equal(pos.view(np.uint32), epos.view(np.uint32))
+    assert np.array_equal(nrm.view(np.uint32), enrm.view(np.uint32))
+    assert (st.max_depth, st.closest, st.rays) == (est.max_depth, est.closest, est.rays)
+    if not any(other for other, _ in calls):
+        assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == []
+        assert st.max_depth == fx["stats"]["max_depth"]
+
+
 def test_repeat_renders_heavy_first_order_bit_exact():
     """From the second render on, the persistent kernel takes its tiles heaviest-first (costs of the
     previous render, sf_tile_order). The image must not depend on the order: renders 2 and 3 of c3
