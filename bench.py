@@ -157,6 +157,26 @@ def post_rates(ctx, torch, stream, width, height, reps=20):
     return out
 
 
+def progressive_rates(width, height, k, batch=1 << 18, reps=5):
+    """the frame-less mode (the reference's Initialize() worker stream: mt19937 draws,
+    Sobol pixel picks, 8-ray AVX / 4-ray SSE packets with packet early-outs, last-writer scatter) on a
+    fresh context with the same camera, in batches of `batch` packets continuing one stream."""
+    out = {"batch_packets": batch}
+    with sf.Sphereflake(width, height) as s:
+        s.SetCamera(sf.config_camera(width, height, k))
+        for variant, lanes in (("avx", 8), ("sse", 4)):
+            s.SetVariant(variant)
+            s.Progressive(12345, batch, 0)
+            s.Synchronize()
+            t = time.perf_counter()
+            for _ in range(reps):
+                s.Progressive(12345, batch)
+            s.Synchronize()
+            dt = (time.perf_counter() - t) / reps
+            out[variant] = {"ms_per_batch": round(dt * 1e3, 4), "Mrays_per_s": round(batch * lanes / dt / 1e6, 1)}
+    return out
+
+
 def transfer_rates(ctx, torch, dev, stream, width, height, kernel, frames=8):
     """G-buffer D2H cost (positions + normals, 32 B/pixel). Pageable synchronous
     download (sf_download, what the reference-style GetGBuffer pays unpinned), stream-ordered copy into
@@ -355,6 +375,9 @@ def main():
     d2h = None
     if rank == 0 and args.mode == "frames" and not args.no_extras:
         d2h = transfer_rates(ctx, torch, dev, stream, width, height, kernel)
+    prog = None
+    if rank == 0 and args.mode == "frames" and not args.no_extras:
+        prog = progressive_rates(width, height, args.K)
 
     check = None
     if args.check and rank == 0 and args.mode == "frames":
@@ -393,6 +416,7 @@ def main():
             "kernel_ms": round(kern_ms_max, 4),
             "post": post,
             "d2h": d2h,
+            "frameless": prog,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": round(traffic) if traffic else None,
