@@ -533,7 +533,7 @@ class Sphereflake:
             _check(lib().sf_progressive(self._ctx, seed & 0xffffffff, c0, packets, None), "sf_progressive", self._ctx)
         self._counter = c0 + packets
 
-    def Initialize(self, seed: int | None = None, batch: int = 1 << 16):
+    def Initialize(self, seed: int | None = None, batch: int = 1 << 18):
         """Start the frame-less progressive loop on a host thread (reference Initialize())."""
         import time
         if self._worker is not None:
