@@ -38,7 +38,16 @@ extern "C" __global__ void sf_post_fused(PostArgs a);
 extern "C" __global__ void sf_mt_draws(uint32_t* state, uint32_t* out, uint32_t n);
 extern "C" __global__ void sf_progressive_trace(FrameArgs a, const uint32_t* draws, uint64_t counter0, uint32_t packets,
                                                 uint64_t ticket0, PacketLane* lanes, unsigned long long* owner,
-                                                const uint32_t* perm);
+                                                const uint32_t* perm, uint32_t levels, uint32_t* ovf_list,
+                                                uint32_t* ovf_cnt);
+extern "C" __global__ void sf_progressive_fixup(FrameArgs a, const uint32_t* draws, uint64_t counter0, uint32_t packets,
+                                                uint64_t ticket0, PacketLane* lanes, unsigned long long* owner,
+                                                const uint32_t* perm, const uint32_t* ovf_list, uint32_t* counters,
+                                                uint32_t parity);
+extern "C" __global__ void sf_progressive_fixup_sse(FrameArgs a, const uint32_t* draws, uint64_t counter0,
+                                                    uint32_t packets, uint64_t ticket0, PacketLane* lanes,
+                                                    unsigned long long* owner, const uint32_t* perm,
+                                                    const uint32_t* ovf_list, uint32_t* counters, uint32_t parity);
 extern "C" __global__ void sf_packet_bin(FrameArgs a, const uint32_t* draws, uint64_t counter0, uint32_t packets,
                                          uint32_t pw, uint32_t bin_shift, uint32_t bins_x, uint32_t* bin_cnt);
 extern "C" __global__ void sf_packet_scan(uint32_t* bin_cnt, uint32_t nbins);
@@ -47,7 +56,8 @@ extern "C" __global__ void sf_packet_place(FrameArgs a, const uint32_t* draws, u
                                            uint32_t* perm);
 extern "C" __global__ void sf_progressive_trace_sse(FrameArgs a, const uint32_t* draws, uint64_t counter0,
                                                     uint32_t packets, uint64_t ticket0, PacketLane* lanes,
-                                                    unsigned long long* owner, const uint32_t* perm);
+                                                    unsigned long long* owner, const uint32_t* perm, uint32_t levels,
+                                                    uint32_t* ovf_list, uint32_t* ovf_cnt);
 extern "C" __global__ void sf_progressive_scatter(FrameArgs a, uint32_t packets, uint64_t ticket0,
                                                   const PacketLane* lanes, const unsigned long long* owner);
 
@@ -124,6 +134,14 @@ struct sf_ctx {
     bool traced_valid = false;
     uint32_t pf_packets = 0;           // draws pending for a batch of this many packets (0: none)
     bool prog_prefetch = true;         // env SF_PROG_PREFETCH=0: off
+    // Adaptive traversal levels: LDS for the deepest level seen so far + 1 (as full frames) instead of
+    // SF_PROGRESSIVE_LEVELS (twice the occupancy); a wave that needs more is re-traced by
+    // sf_progressive_fixup. env SF_PROG_ADAPT=0: always SF_PROGRESSIVE_LEVELS.
+    bool prog_adapt = true;
+    int32_t* h_prog_depth = nullptr;   // pinned copy of the max-depth stat after each batch
+    uint32_t* prog_ovf = nullptr;      // overflowed wave indices (prog_cap waves)
+    uint32_t* prog_ovf_cnt = nullptr;  // [2] list counts, alternating per batch
+    uint32_t prog_par = 0;
     unsigned long long* owner = nullptr;   // per pixel: highest ticket written
     bool prog_seeded = false;
     uint32_t prog_seed = 0;
@@ -190,6 +208,9 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->perm);
     (void)hipFree(c->bin_cnt);
     if (c->pf_stream) (void)hipStreamSynchronize(c->pf_stream);
+    if (c->h_prog_depth) (void)hipHostFree(c->h_prog_depth);
+    (void)hipFree(c->prog_ovf);
+    (void)hipFree(c->prog_ovf_cnt);
     (void)hipFree(c->draws_pf);
     (void)hipFree(c->mt_saved);
     if (c->pf_done) (void)hipEventDestroy(c->pf_done);
@@ -295,6 +316,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if (const char* ev = std::getenv("SF_ORDER")) c->use_order = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_BIN")) c->prog_bin = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_PREFETCH")) c->prog_prefetch = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_PROG_ADAPT")) c->prog_adapt = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_SPLIT_BUCKETS")) c->split_buckets = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_FLAGS")) c->flags = (uint32_t)std::strtoul(ev, nullptr, 0);
@@ -629,14 +651,17 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
         (void)hipFree(c->draws_pf);
         (void)hipFree(c->lanes);
         (void)hipFree(c->perm);
+        (void)hipFree(c->prog_ovf);
         c->draws = c->draws_pf = nullptr;
         c->lanes = nullptr;
         c->perm = nullptr;
+        c->prog_ovf = nullptr;
         c->prog_cap = 0;
         c->traced_valid = false;
         SF_HIP(c, hipMalloc(&c->draws, (size_t)packets * 2 * 4));
         SF_HIP(c, hipMalloc(&c->lanes, (size_t)packets * 8 * sizeof(PacketLane)));
         SF_HIP(c, hipMalloc(&c->perm, (size_t)packets * 4));
+        SF_HIP(c, hipMalloc(&c->prog_ovf, ((size_t)packets + 3) / 4 * 4));   // >= one entry per wave
         c->prog_cap = packets;
     }
     if (!c->prog_seeded || seed != c->prog_seed || counter0 != c->prog_next) {
@@ -710,14 +735,43 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     }
     const uint32_t ppw = 64u / pl;                   // packets per wave
     const uint32_t waves = (packets + ppw - 1) / ppw;
-    const size_t lds = (size_t)SF_LDS_WAVE_FLOATS(16) * 4;
+    uint32_t levels = SF_PROGRESSIVE_LEVELS;
+    if (c->prog_adapt) {
+        if (!c->h_prog_depth) {
+            SF_HIP(c, hipHostMalloc(&c->h_prog_depth, 4, hipHostMallocDefault));
+            *c->h_prog_depth = -1;
+            SF_HIP(c, hipMalloc(&c->prog_ovf_cnt, 2 * 4));
+            SF_HIP(c, hipMemsetAsync(c->prog_ovf_cnt, 0, 2 * 4, s));
+        }
+        const int32_t seen = *(volatile int32_t*)c->h_prog_depth;   // max depth of a finished batch
+        if (seen >= 0 && (uint32_t)seen + 1u < levels) levels = (uint32_t)seen + 1u < 4u ? 4u : (uint32_t)seen + 1u;
+    }
+    const bool adaptive = levels < SF_PROGRESSIVE_LEVELS;
+    uint32_t* ovf_cnt = adaptive ? c->prog_ovf_cnt + c->prog_par : nullptr;
+    const size_t lds = (size_t)SF_LDS_WAVE_FLOATS(levels) * 4;
     if (sse)
         hipLaunchKernelGGL(sf_progressive_trace_sse, dim3(waves), dim3(64), lds, s, a, (const uint32_t*)c->draws,
-                           counter0, packets, c->ticket, c->lanes, c->owner, perm);
+                           counter0, packets, c->ticket, c->lanes, c->owner, perm, levels,
+                           adaptive ? c->prog_ovf : nullptr, ovf_cnt);
     else
         hipLaunchKernelGGL(sf_progressive_trace, dim3(waves), dim3(64), lds, s, a, (const uint32_t*)c->draws,
-                           counter0, packets, c->ticket, c->lanes, c->owner, perm);
+                           counter0, packets, c->ticket, c->lanes, c->owner, perm, levels,
+                           adaptive ? c->prog_ovf : nullptr, ovf_cnt);
     SF_HIP(c, hipGetLastError());
+    if (adaptive) {   // re-trace the waves that needed more levels (reads this batch's list, zeroes the next)
+        const size_t lds_fix = (size_t)SF_LDS_WAVE_FLOATS(SF_PROGRESSIVE_LEVELS) * 4;
+        const dim3 fg(SF_PROG_FIXUP_BLOCKS);
+        if (sse)
+            hipLaunchKernelGGL(sf_progressive_fixup_sse, fg, dim3(64), lds_fix, s, a, (const uint32_t*)c->draws,
+                               counter0, packets, c->ticket, c->lanes, c->owner, perm, (const uint32_t*)c->prog_ovf,
+                               c->prog_ovf_cnt, c->prog_par);
+        else
+            hipLaunchKernelGGL(sf_progressive_fixup, fg, dim3(64), lds_fix, s, a, (const uint32_t*)c->draws,
+                               counter0, packets, c->ticket, c->lanes, c->owner, perm, (const uint32_t*)c->prog_ovf,
+                               c->prog_ovf_cnt, c->prog_par);
+        SF_HIP(c, hipGetLastError());
+        c->prog_par ^= 1u;
+    }
     if (c->pf_stream) {   // the next prefetch may overwrite this batch's draws after this point
         SF_HIP(c, hipEventRecord(c->traced, s));
         c->traced_valid = true;
@@ -725,6 +779,7 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     hipLaunchKernelGGL(sf_progressive_scatter, dim3((packets * pl + 255) / 256), dim3(256), 0, s, a, packets, c->ticket,
                        (const PacketLane*)c->lanes, (const unsigned long long*)c->owner);
     SF_HIP(c, hipGetLastError());
+    if (c->prog_adapt) SF_HIP(c, hipMemcpyAsync(c->h_prog_depth, c->stats, 4, hipMemcpyDeviceToHost, s));
     c->ticket += packets;
     c->prog_next = counter0 + packets;
     c->rays += (int64_t)pl * packets;                // m_RaysPerSecond += 8 / 4 (Sphereflake.cpp:184-186)

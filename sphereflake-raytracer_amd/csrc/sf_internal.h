@@ -124,6 +124,10 @@ struct PostArgs {
     uint8_t* rgba;                    // final image, W x H x RGBA8, row j = G-buffer row j
 };
 
+#ifndef SF_PROGRESSIVE_LEVELS
+#define SF_PROGRESSIVE_LEVELS 16        // frame-less mode: LDS traversal levels
+#endif
+#define SF_PROG_FIXUP_BLOCKS 256u      // grid of sf_progressive_fixup (grid-stride over the overflow list)
 #define SF_PROG_MAX_BINS 65536u        // frame-less mode: packet bins (counting sort in one workgroup)
 #define SF_PROG_PREFETCH_MIN 65536u    // frame-less batches from this many packets prefetch the next draws
 #define SF_PROG_BIN_MIN 65536u         // frame-less batches below this many packets trace in draw order

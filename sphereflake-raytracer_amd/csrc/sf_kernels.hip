@@ -37,7 +37,6 @@
 #pragma clang fp contract(off)
 
 #define SF_MAX_LEVELS 31         // SF_MAX_DEPTH_LIMIT (ebits is 32 bits)
-#define SF_PROGRESSIVE_LEVELS 16
 
 namespace {
 
@@ -1298,14 +1297,15 @@ extern "C" __global__ __launch_bounds__(256) void sf_packet_place(FrameArgs a, c
 template <int PW>
 __device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint32_t* draws, uint64_t counter0,
                                                   uint32_t packets, uint64_t ticket0, PacketLane* lanes,
-                                                  unsigned long long* owner, const uint32_t* perm)
+                                                  unsigned long long* owner, const uint32_t* perm, uint32_t wave,
+                                                  uint32_t levels, uint32_t* ovf_list, uint32_t* ovf_cnt)
 {
     extern __shared__ float lds[];
     constexpr uint32_t PPW = 64u / PW;   // packets per wave
     const DeviceConsts* __restrict__ K = a.consts;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t slot = blockIdx.x * PPW + lane / PW;   // position in the (binned) trace order
-    if (blockIdx.x * PPW >= packets) return;   // wave-uniform
+    const uint32_t slot = wave * PPW + lane / PW;   // position in the (binned) trace order
+    if (wave * PPW >= packets) return;   // wave-uniform
     const bool valid = slot < packets;
     const uint32_t packet = valid ? (perm ? perm[slot] : slot) : slot;
     const uint32_t q = lane % PW;
@@ -1329,7 +1329,7 @@ __device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint
     int32_t maxd = -1;
     bool overflowed = false;
     stage_root(lds, a.root);
-    traverse<PW>(K, a.root, lds, SF_PROGRESSIVE_LEVELS, dx, dy, dz, valid, h, maxd, overflowed, a.flags);
+    traverse<PW>(K, a.root, lds, levels, dx, dy, dz, valid, h, maxd, overflowed, a.flags);
 
     PacketLane out;
     shade(dx, dy, dz, h, K->lut, out.px, out.py, out.pz, out.nx, out.ny, out.nz);
@@ -1349,23 +1349,68 @@ __device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint
         const int32_t cur_k = __hip_atomic_load(&a.stats[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (maxd > cur_d) atomicMax(&a.stats[0], maxd);
         if (key < cur_k) atomicMin(&a.stats[1], key);
-        if (anyov) atomicAdd(&a.stats[2], 1);
+        if (anyov && !ovf_list) atomicAdd(&a.stats[2], 1);
     }
+    // adaptive levels: a wave that needed more is re-traced whole by sf_progressive_fixup (its partial
+    // lanes, owner words and stats are all superseded or implied by the complete traversal)
+    if (anyov && ovf_list) {
+        const uint32_t k = wave_fetch_add(ovf_cnt, 1u);
+        ovf_list[k] = wave;   // uniform value and address
+    }
+}
+
+template <int PW>
+__device__ __forceinline__ void progressive_fixup(const FrameArgs& a, const uint32_t* draws, uint64_t counter0,
+                                                  uint32_t packets, uint64_t ticket0, PacketLane* lanes,
+                                                  unsigned long long* owner, const uint32_t* perm,
+                                                  const uint32_t* ovf_list, uint32_t* counters, uint32_t parity)
+{
+    if (blockIdx.x == 0 && threadIdx.x == 0) counters[parity ^ 1u] = 0u;   // the next batch's list
+    const uint32_t n = counters[parity];
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x)
+        progressive_trace<PW>(a, draws, counter0, packets, ticket0, lanes, owner, perm,
+                              __builtin_amdgcn_readfirstlane(ovf_list[i]),
+                              SF_PROGRESSIVE_LEVELS, nullptr, nullptr);
 }
 
 extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace(FrameArgs a, const uint32_t* draws,
                                                                        uint64_t counter0, uint32_t packets,
                                                                        uint64_t ticket0, PacketLane* lanes,
-                                                                       unsigned long long* owner, const uint32_t* perm)
+                                                                       unsigned long long* owner, const uint32_t* perm,
+                                                                       uint32_t levels, uint32_t* ovf_list,
+                                                                       uint32_t* ovf_cnt)
 {
-    progressive_trace<8>(a, draws, counter0, packets, ticket0, lanes, owner, perm);
+    progressive_trace<8>(a, draws, counter0, packets, ticket0, lanes, owner, perm, blockIdx.x, levels, ovf_list,
+                         ovf_cnt);
 }
 extern "C" __global__ __launch_bounds__(64) void sf_progressive_trace_sse(FrameArgs a, const uint32_t* draws,
                                                                            uint64_t counter0, uint32_t packets,
                                                                            uint64_t ticket0, PacketLane* lanes,
-                                                                           unsigned long long* owner, const uint32_t* perm)
+                                                                           unsigned long long* owner, const uint32_t* perm,
+                                                                           uint32_t levels, uint32_t* ovf_list,
+                                                                           uint32_t* ovf_cnt)
 {
-    progressive_trace<4>(a, draws, counter0, packets, ticket0, lanes, owner, perm);
+    progressive_trace<4>(a, draws, counter0, packets, ticket0, lanes, owner, perm, blockIdx.x, levels, ovf_list,
+                         ovf_cnt);
+}
+extern "C" __global__ __launch_bounds__(64) void sf_progressive_fixup(FrameArgs a, const uint32_t* draws,
+                                                                       uint64_t counter0, uint32_t packets,
+                                                                       uint64_t ticket0, PacketLane* lanes,
+                                                                       unsigned long long* owner, const uint32_t* perm,
+                                                                       const uint32_t* ovf_list, uint32_t* counters,
+                                                                       uint32_t parity)
+{
+    progressive_fixup<8>(a, draws, counter0, packets, ticket0, lanes, owner, perm, ovf_list, counters, parity);
+}
+extern "C" __global__ __launch_bounds__(64) void sf_progressive_fixup_sse(FrameArgs a, const uint32_t* draws,
+                                                                           uint64_t counter0, uint32_t packets,
+                                                                           uint64_t ticket0, PacketLane* lanes,
+                                                                           unsigned long long* owner,
+                                                                           const uint32_t* perm,
+                                                                           const uint32_t* ovf_list,
+                                                                           uint32_t* counters, uint32_t parity)
+{
+    progressive_fixup<4>(a, draws, counter0, packets, ticket0, lanes, owner, perm, ovf_list, counters, parity);
 }
 
 // Last writer wins by ticket (= the reference worker's sequential packet order).

@@ -455,3 +455,31 @@ def test_split_render_bit_exact_and_stable():
             assert st.max_depth == fx["stats"]["max_depth"] and st.overflow_tiles == 0
         finally:
             del os.environ["SF_SPLIT_BUCKETS"]
+
+
+def test_progressive_adaptive_levels_fixup(monkeypatch):
+    """Frame-less batches provision LDS levels for the deepest level seen so far + 1; a wave that needs
+    more is re-traced by sf_progressive_fixup. Moving the camera from the depth-5 view (levels 6) to the
+    depth-8 view forces that path: the frame equals the same calls with SF_PROGRESSIVE_LEVELS always
+    (SF_PROG_ADAPT=0), bit for bit, and nothing is left unresolved."""
+    W, H = 640, 360
+
+    def run():
+        with sf.Sphereflake(W, H) as s:
+            s.SetCamera(sf.config_camera(W, H, 1.0))
+            s.Progressive(5, 70000, counter0=0)
+            s.Synchronize()
+            s.SetCamera(sf.config_camera(W, H, 0.25))
+            for _ in range(3):
+                s.Progressive(5, 70000)
+            s.Synchronize()
+            pos, nrm, _, _ = s.download()
+            return pos, nrm, s.stats()
+
+    pos, nrm, st = run()
+    monkeypatch.setenv("SF_PROG_ADAPT", "0")
+    epos, enrm, est = run()
+    assert np.array_equal(pos.view(np.uint32), epos.view(np.uint32))
+    assert np.array_equal(nrm.view(np.uint32), enrm.view(np.uint32))
+    assert (st.max_depth, st.closest) == (est.max_depth, est.closest)
+    assert st.max_depth >= 8 and st.overflow_tiles == 0 and est.overflow_tiles == 0
