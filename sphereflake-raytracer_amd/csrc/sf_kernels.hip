@@ -1267,15 +1267,26 @@ extern "C" __global__ __launch_bounds__(1024) void sf_packet_scan(uint32_t* bin_
     uint32_t s_ = 0u;
 #pragma unroll
     for (uint32_t j = 0; j < SF_PROG_MAX_BINS / 1024u; ++j) s_ += v[j];
-    part[t] = s_;
-    __syncthreads();
-    for (uint32_t o = 1u; o < 1024u; o <<= 1) {   // inclusive Hillis-Steele scan of the partials
-        const uint32_t v = t >= o ? part[t - o] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
+    // exclusive scan of the 1024 partials: in-wave shuffles, then the 16 wave totals (two barriers)
+    const uint32_t lane = t & 63u, w = t >> 6;
+    uint32_t x = s_;
+#pragma unroll
+    for (uint32_t o = 1u; o < 64u; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        x += lane >= o ? y : 0u;
     }
-    uint32_t off = part[t] - s_;
+    if (lane == 63u) part[w] = x;
+    __syncthreads();
+    if (t == 0u) {
+        uint32_t acc = 0u;
+        for (uint32_t k = 0; k < 16u; ++k) {
+            const uint32_t y = part[k];
+            part[k] = acc;
+            acc += y;
+        }
+    }
+    __syncthreads();
+    uint32_t off = part[w] + x - s_;
 #pragma unroll
     for (uint32_t j = 0; j < SF_PROG_MAX_BINS / 1024u; ++j) {
         if (b0 + j < b1) bin_cnt[b0 + j] = off;
