@@ -128,7 +128,7 @@ struct PostArgs {
 #define SF_PROGRESSIVE_LEVELS 16        // frame-less mode: LDS traversal levels
 #endif
 #define SF_PROG_FIXUP_BLOCKS 256u      // grid of sf_progressive_fixup (grid-stride over the overflow list)
-#define SF_PROG_MAX_BINS 65536u        // frame-less mode: packet bins (counting sort in one workgroup)
+#define SF_PROG_MAX_BINS 32768u        // frame-less mode: packet bins (counting sort in one workgroup's LDS)
 #define SF_PROG_PREFETCH_MIN 65536u    // frame-less batches from this many packets prefetch the next draws
 #define SF_PROG_BIN_MIN 65536u         // frame-less batches below this many packets trace in draw order
                                        // (binning pays once the batch is several waves per slot)

@@ -1257,17 +1257,17 @@ extern "C" __global__ __launch_bounds__(256) void sf_packet_bin(FrameArgs a, con
 
 extern "C" __global__ __launch_bounds__(1024) void sf_packet_scan(uint32_t* bin_cnt, uint32_t nbins)
 {
-    // thread t: bins [t * per, (t + 1) * per) -> exclusive offsets in place (the place cursors)
-    // (nbins <= SF_PROG_MAX_BINS = 64 x 1024: a thread's counts are loaded at once and kept)
-    __shared__ uint32_t part[1024];
+    // Counts -> exclusive offsets in place (the place cursors). Staged through LDS so that global
+    // reads and writes are coalesced; thread t scans bins [t * per, (t + 1) * per) of the staged copy
+    // (index padded by 1 per 32 against bank conflicts).
+    __shared__ uint32_t cnt[SF_PROG_MAX_BINS + SF_PROG_MAX_BINS / 32u];
+    __shared__ uint32_t part[16];
     const uint32_t t = threadIdx.x, per = (nbins + 1023u) / 1024u, b0 = t * per, b1 = min(nbins, b0 + per);
-    uint32_t v[SF_PROG_MAX_BINS / 1024u];
-#pragma unroll
-    for (uint32_t j = 0; j < SF_PROG_MAX_BINS / 1024u; ++j) v[j] = b0 + j < b1 ? bin_cnt[b0 + j] : 0u;
+    for (uint32_t i = t; i < nbins; i += 1024u) cnt[i + (i >> 5)] = bin_cnt[i];
+    __syncthreads();
     uint32_t s_ = 0u;
-#pragma unroll
-    for (uint32_t j = 0; j < SF_PROG_MAX_BINS / 1024u; ++j) s_ += v[j];
-    // exclusive scan of the 1024 partials: in-wave shuffles, then the 16 wave totals (two barriers)
+    for (uint32_t b = b0; b < b1; ++b) s_ += cnt[b + (b >> 5)];
+    // exclusive scan of the 1024 partials: in-wave shuffles, then the 16 wave totals
     const uint32_t lane = t & 63u, w = t >> 6;
     uint32_t x = s_;
 #pragma unroll
@@ -1287,11 +1287,13 @@ extern "C" __global__ __launch_bounds__(1024) void sf_packet_scan(uint32_t* bin_
     }
     __syncthreads();
     uint32_t off = part[w] + x - s_;
-#pragma unroll
-    for (uint32_t j = 0; j < SF_PROG_MAX_BINS / 1024u; ++j) {
-        if (b0 + j < b1) bin_cnt[b0 + j] = off;
-        off += v[j];
+    for (uint32_t b = b0; b < b1; ++b) {
+        const uint32_t c = cnt[b + (b >> 5)];
+        cnt[b + (b >> 5)] = off;
+        off += c;
     }
+    __syncthreads();
+    for (uint32_t i = t; i < nbins; i += 1024u) bin_cnt[i] = cnt[i + (i >> 5)];
 }
 
 extern "C" __global__ __launch_bounds__(256) void sf_packet_place(FrameArgs a, const uint32_t* draws, uint64_t counter0,
