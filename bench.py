@@ -7,6 +7,12 @@ the depth-8 camera (BASELINE configs[2]: main.cpp:92-96 camera position scaled b
 G-buffer stays resident in HBM (the D2H copy into the host GBuffer is timed separately and reported
 as `d2h_ms`, never as `value`).
 
+The camera MOVES: step i renders frame f = i * N + rank of a camera path (the config camera with its
+yaw swept +-10 mrad around the config view at 1 mrad per frame, `frame_camera`), so the heavy-first tile
+schedule always works from the costs of a different view (the reference is an interactive app whose view changes every frame,
+main.cpp:304). `first_render_ms` is the first render of a fresh context (row-major tile order, no
+previous costs); `fixed_camera` repeats the timed loop on one unchanging view.
+
 Multi-GPU (`--gpus N`, launched by torch.distributed.run): one process per GPU. The frames of a
 camera path are independent units, so each rank renders its own 1920x1080 depth-8 frame per step
 (frame index = step * N + rank); no data-path collective, `scaling: weak`. The row-banded single-frame
@@ -60,10 +66,21 @@ def parse():
     return ap.parse_args()
 
 
+PATH_AMPLITUDE = 10                  # camera path: yaw sweeps +-10 mrad around the config view, 1 mrad/frame
+
+
+def path_yaw_offset(frame):
+    """Yaw offset (rad) of frame `frame` of the camera path: a triangle wave 0, -1, ..., -10, ..., +10, ..., 0
+    mrad (period 40 frames). The camera moves 1 mrad every frame yet stays within ~18 px of the BASELINE
+    view, so every frame is the config's workload (same max depth, same scene content)."""
+    a = PATH_AMPLITUDE
+    return 1e-3 * (abs((frame + a) % (4 * a) - 2 * a) - a)
+
+
 def frame_camera(width, height, k, frame):
-    """Frame `frame` of the camera path: the config camera with yaw advanced 1 mrad per frame."""
+    """Frame `frame` of the camera path: the config camera with yaw offset by path_yaw_offset(frame)."""
     cam = sf.config_camera(width, height, k)
-    cam.SetYaw(np.float32(sf.DEFAULT_YAW + 1e-3 * frame))
+    cam.SetYaw(np.float32(sf.DEFAULT_YAW + path_yaw_offset(frame)))
     return cam
 
 
@@ -71,41 +88,77 @@ KTIMING_PERIOD = 10                  # HIP events on every 10th timed render
 CPU_REPS = 40                        # ~1.2 s wall x 16 threads: ~20 s of CPU work
 
 
-def pmc_valu(kernel, cus=256):
-    """VALU issue of `kernel` from the committed PMC summary: wave-level VALU instructions per launch
-    against the VALU issue slots of the profiled dispatch (CUs x 4 SIMDs x cycles / 2: one wave64
-    VALU instruction issues over 2 cycles; cycles = GRBM_GUI_ACTIVE / 8 XCDs)."""
+BASELINE_CONFIGS = {(640, 360, 1.0): "configs[0]", (1280, 720, 0.8): "configs[1]", (1920, 1080, 0.25): "configs[2]",
+                    (3840, 2160, 0.22): "configs[3]", (16384, 16384, 0.2): "configs[4]"}
+
+
+def pmc_config_key(width, height, k, camera):
+    """The bench configuration a committed PMC summary was profiled on (scripts/pmc_summary.py --config)."""
+    return f"{width}x{height} K={k:g} {camera}"
+
+
+def load_pmc(kernel, config_key):
+    """Per-dispatch PMC means of `kernel` from profiles/pmc_traffic.json -- only when that summary was
+    profiled on this very configuration (None otherwise: counters are never replayed onto another config)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            c = json.load(f)["kernels"][kernel]
+            j = json.load(f)
+        if j.get("config") != config_key:
+            return None, None
+        return j["kernels"][kernel], j.get("source", path)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
+def pmc_valu(c, cus=256):
+    """VALU issue of `kernel` from the committed PMC summary: wave-level VALU instructions per launch
+    against the VALU issue slots of the profiled dispatch (CUs x 4 SIMDs x cycles / 2: one wave64
+    VALU instruction issues over 2 cycles; cycles = GRBM_GUI_ACTIVE / 8 XCDs)."""
+    if c is None:
+        return None
+    try:
         cycles = c["GRBM_GUI_ACTIVE"] / 8.0
         slots = cus * 4 * cycles / 2.0
         # wavefront occupancy: SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md), summed over the
         # chip -> mean resident waves; against the gfx950 peak of 8 waves per SIMD
         waves = 4.0 * c["SQ_WAVE_CYCLES"] / cycles
         peak_waves = cus * 4 * 8
-        return {"valu_insts": round(c["SQ_INSTS_VALU"]), "salu_insts": round(c["SQ_INSTS_SALU"]),
-                "issue_slots": round(slots), "valu_issue_frac": round(c["SQ_INSTS_VALU"] / slots, 4),
-                "occupancy": {"mean_waves": round(waves, 1), "peak_waves": peak_waves,
-                              "frac": round(waves / peak_waves, 4)},
-                "clock_mhz": round(cycles / c["profiled_dispatch_us"], 1), "source": "profiles/pmc_traffic.json"}
-    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        out = {"valu_insts": round(c["SQ_INSTS_VALU"]), "salu_insts": round(c["SQ_INSTS_SALU"]),
+               "issue_slots": round(slots), "valu_issue_frac": round(c["SQ_INSTS_VALU"] / slots, 4),
+               "occupancy": {"mean_waves": round(waves, 1), "peak_waves": peak_waves,
+                             "frac": round(waves / peak_waves, 4)},
+               "clock_mhz": round(cycles / c["profiled_dispatch_us"], 1), "source": "profiles/pmc_traffic.json"}
+        if "SQ_WAIT_INST_ANY" in c and c.get("SQ_WAVE_CYCLES"):
+            out["wait_inst_frac"] = round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+            out["wait_any_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+        return out
+    except (KeyError, ValueError, ZeroDivisionError):
         return None
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (scripts/prof_pmc.sh ->
+def pmc_traffic(c):
+    """HBM bytes per launch of the trace kernel from the committed PMC summary (scripts/prof_pmc.sh ->
     scripts/pmc_summary.py --json, separate rocprofv3 --pmc passes of this same bench command):
     WRITE_SIZE + 2 x FETCH_SIZE (gfx950 FETCH_SIZE counts half of a streaming read), KB -> bytes."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
-        with open(path) as f:
-            j = json.load(f)
-        c = j["kernels"][kernel]
-        return (c["WRITE_SIZE"] + 2.0 * c["FETCH_SIZE"]) * 1024.0, j.get("source", path)
-    except (OSError, KeyError, ValueError):
-        return None, None
+        return (c["WRITE_SIZE"] + 2.0 * c["FETCH_SIZE"]) * 1024.0
+    except (TypeError, KeyError, ValueError):
+        return None
+
+
+def cpu_share():
+    """Host cores this process may use: the affinity mask, capped by a cgroup v2 CPU quota if one is set."""
+    avail = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return avail, quota
 
 
 def cpu_baseline(width, height, k, threads):
@@ -116,7 +169,9 @@ def cpu_baseline(width, height, k, threads):
     if os.path.exists(ref):
         r = pyoracle.ref_bench(width, height, k, threads, CPU_REPS)
         r1 = pyoracle.ref_bench(width, height, k, 1, 3)   # also one thread
+        avail, quota = cpu_share()
         return {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": threads, "kind": "reference",
+                "cores_available": avail, "cgroup_cpu_quota": quota, "host_cores": os.cpu_count(),
                 "sample": f"{CPU_REPS} full {width}x{height} K={k} frames (reference 8-ray packet footprint, 8/9 "
                           f"pixel coverage), median; reference AVX path -O3 -mavx, {threads} threads",
                 "frame_ms": round(r["median_s"] * 1e3, 2),
@@ -285,7 +340,8 @@ def main():
     sh = stream.cuda_stream
 
     if args.mode == "frames":
-        views = [frame_camera(width, height, args.K, rank).corners()]   # frame index = rank
+        # frame index = step * N + rank along the camera path (warmup, timed loop)
+        views = [frame_camera(width, height, args.K, i * n + rank).corners() for i in range(args.warmup + args.steps)]
         rays_per_step_rank = width * height
         slab_rows = height
     else:
@@ -299,9 +355,17 @@ def main():
         send_p = torch.zeros((max_rows, width, 4), dtype=torch.float32, device=dev)
         send_n = torch.zeros_like(send_p)
 
+    first_ms = None
     if args.mode == "frames":
-        o, tl, tr, bl = views[0]
-        ctx.SetView(o, tl, tr, bl)
+        ctx.SetView(*views[0])
+        # the first render of a fresh context: row-major tile order, no cost history
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(stream):
+            e0.record(stream)
+            ctx.Render(kernel=kernel, stream=sh)
+            e1.record(stream)
+        torch.cuda.synchronize(dev)
+        first_ms = e0.elapsed_time(e1)
     # HIP events around the dominant (trace) kernel of every KTIMING_PERIOD-th render: an event pair
     # costs ~7 us of stream time per frame, so it is sampled (SF_BENCH_KTIMING=0: off, for A/B)
     ktiming = os.environ.get("SF_BENCH_KTIMING", "1") != "0"
@@ -311,12 +375,14 @@ def main():
 
     # whole-render events (kernel_ms) on the same sampled steps as the trace-kernel events: every
     # event record on the stream costs GPU time between kernels (measured ~7 us per pair per frame)
-    def run_step(i, timed):
+    def run_step(i, timed, view=None):
         timed = timed and ktiming and i % KTIMING_PERIOD == 0
         with torch.cuda.stream(stream):
             if timed:
                 ev_s[i].record(stream)
             if args.mode == "frames":
+                if view is not None:
+                    ctx.SetView(*view)
                 ctx.Render(kernel=kernel, stream=sh)
             else:
                 ctx.render_to(slab_p.data_ptr(), slab_n.data_ptr(), band_rows=args.band_rows, band_count=n,
@@ -333,8 +399,9 @@ def main():
                     shard.gather_frame(send_p.cpu(), height, args.band_rows)
                     shard.gather_frame(send_n.cpu(), height, args.band_rows)
 
+    moving = args.mode == "frames"
     for i in range(args.warmup):
-        run_step(i, False)
+        run_step(i, False, views[i] if moving else None)
     ctx.kernel_timing(ktiming, period=KTIMING_PERIOD)   # samples timed renders 0, 10, 20, ...
     torch.cuda.synchronize(dev)
     if dist_on:
@@ -342,7 +409,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        run_step(i, True)
+        run_step(i, True, views[args.warmup + i] if moving else None)
     torch.cuda.synchronize(dev)
     if dist_on:
         dist.barrier()
@@ -355,6 +422,30 @@ def main():
                if ktiming else dt / args.steps * 1e3)   # whole render, sampled
     tk = ctx.kernel_timing(n=min(-(-args.steps // KTIMING_PERIOD), 64)) if ktiming else []   # the trace kernel alone, last timed renders
     trace_ms = float(np.mean(tk)) if len(tk) else kern_ms
+
+    # the same loop on one unchanging view (the config camera, frame 0 of the path): extra key, never `value`
+    fixed = None
+    if moving:
+        ctx.kernel_timing(False)
+        ctx.SetView(*views[0])
+        for i in range(args.warmup):
+            run_step(i, False)
+        torch.cuda.synchronize(dev)
+        if dist_on:
+            dist.barrier()
+        tf = time.perf_counter()
+        for i in range(args.steps):
+            run_step(i, False)
+        torch.cuda.synchronize(dev)
+        if dist_on:
+            dist.barrier()
+        t_fixed = (time.perf_counter() - tf) / args.steps
+        if dist_on:
+            tt = torch.tensor([t_fixed], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t_fixed = float(tt[0])
+        fixed = {"value": round(n * width * height / t_fixed / 1e6, 2), "frame_ms": round(t_fixed * 1e3, 4),
+                 "note": "same timed loop on the unchanging config view (heavy-first order from identical frames)"}
 
     t_step = dt / args.steps
     if dist_on:
@@ -394,7 +485,10 @@ def main():
     if rank == 0:
         per_launch_bytes = BYTES_PER_RAY * rays_per_step_rank
         achieved = per_launch_bytes / (trace_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(TRACE_KERNEL)
+        camera = "moving" if moving else "fixed"
+        pmc, _ = load_pmc(TRACE_KERNEL, pmc_config_key(width, height, args.K, camera))
+        traffic = pmc_traffic(pmc)
+        cfg_name = BASELINE_CONFIGS.get((width, height, round(args.K, 4)))
         out = {
             "metric": "Mrays/sec into G-buffer at 1920x1080 depth-8; frame time ms",
             "value": round(value, 2),
@@ -407,13 +501,19 @@ def main():
             "scaling": "weak" if args.mode == "frames" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (deterministic fixed-camera frames; no dataset)",
-            "config": {"workload": f"{width}x{height} primary-ray G-buffer, depth-8 camera K={args.K} "
-                                   f"(BASELINE configs[2]), {args.kernel} kernel",
-                       "width": width, "height": height, "K": args.K, "max_depth": st.max_depth,
+            "data": "synthetic (deterministic camera path: config camera, yaw swept +-10 mrad at 1 mrad per frame; "
+                    "no dataset)"
+                    if moving else "synthetic (deterministic fixed-camera frames; no dataset)",
+            "config": {"workload": f"{width}x{height} primary-ray G-buffer, camera K={args.K:g} (reference max "
+                                   f"depth {st.max_depth})"
+                                   + (f", BASELINE {cfg_name}" if cfg_name else "")
+                                   + f", {camera} camera, {args.kernel} kernel",
+                       "width": width, "height": height, "K": args.K, "max_depth": st.max_depth, "camera": camera,
                        "parallelism": f"frames x{n}" if args.mode == "frames" else f"row-bands x{n} + RCCL gather"},
             "frame_ms": round(t_step * 1e3, 4),
             "kernel_ms": round(kern_ms_max, 4),
+            "first_render_ms": round(first_ms, 4) if first_ms is not None else None,
+            "fixed_camera": fixed,
             "post": post,
             "d2h": d2h,
             "frameless": prog,
@@ -424,15 +524,25 @@ def main():
                          "note": "path is VALU/latency-bound (SURVEY.md §8(d), see `valu`); achieved = 32 B/ray x "
                                  "rays per launch / mean duration of the trace kernel (HIP events around it on its "
                                  "launch stream); traffic = PMC WRITE_SIZE + 2 x FETCH_SIZE per launch "
-                                 "(profiles/pmc_traffic.json)"},
-            "valu": pmc_valu(TRACE_KERNEL),
+                                 "(profiles/pmc_traffic.json, only when profiled on this config, else null)"},
+            "valu": pmc_valu(pmc),
         }
         if check is not None:
             out["check_rows_bit_exact"] = check
         if not args.no_cpu_baseline and n == 1:
-            thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+            avail, quota = cpu_share()
+            thr = args.cpu_threads or (min(avail, quota) if quota else avail)
             try:
-                out["cpu_baseline"] = cpu_baseline(width, height, args.K, thr)
+                cb = cpu_baseline(width, height, args.K, thr)
+                if "value" in cb and cb["value"] > 0:
+                    cb["gpu_cpu_ratio"] = round(value / cb["value"], 1)
+                    if cb.get("kind") == "reference":
+                        # linear extrapolation of the measured share to every host core (an estimate,
+                        # labelled as such: SMT and memory bandwidth make it optimistic for the CPU)
+                        allc = cb["value"] * (os.cpu_count() or thr) / thr
+                        cb["all_host_cores_estimate"] = {"value": round(allc, 1), "gpu_cpu_ratio": round(value / allc, 1),
+                                                         "note": "measured value x host_cores / cores (linear)"}
+                out["cpu_baseline"] = cb
             except Exception as e:  # never lose the GPU number over the baseline leg
                 out["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(out), flush=True)

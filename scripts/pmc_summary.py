@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc counter CSVs per kernel (mean per dispatch).
-Usage: pmc_summary.py [--json OUT] <dir>...   (--json also writes the means, for bench.py's roofline traffic)"""
+Usage: pmc_summary.py [--json OUT [--config KEY]] <dir>...
+  --json also writes the means, for bench.py's roofline traffic and `valu`; --config names the bench
+  configuration the passes profiled (bench.py pmc_config_key, e.g. "1920x1080 K=0.25 moving"): bench.py
+  reports the counters only for that configuration."""
 import csv
 import glob
 import json
@@ -10,8 +13,11 @@ from collections import defaultdict
 
 args = sys.argv[1:]
 out_json = None
+config = None
 if args and args[0] == "--json":
     out_json, args = args[1], args[2:]
+if args and args[0] == "--config":
+    config, args = args[1], args[2:]
 acc = defaultdict(lambda: defaultdict(list))
 dur = defaultdict(list)
 for d in args:
@@ -37,4 +43,4 @@ if out_json:
     with open(out_json, "w") as f:
         rel = sorted({os.path.relpath(d, os.getcwd()) for d in args})
         json.dump({"source": "rocprofv3 --pmc passes of scripts/prof_pmc.sh (" + ", ".join(rel) + "); "
-                             "FETCH_SIZE/WRITE_SIZE in KB per dispatch", "kernels": means}, f, indent=1)
+                             "FETCH_SIZE/WRITE_SIZE in KB per dispatch", "config": config, "kernels": means}, f, indent=1)

@@ -10,12 +10,12 @@ mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 tail -3 $OUT/pytest_gpu.log
 scripts/prof_pmc.sh $TAG/pmc
-python3 scripts/pmc_summary.py --json $OUT/pmc_traffic.json $OUT/pmc/*/ > $OUT/pmc_summary.txt
+python3 scripts/pmc_summary.py --json $OUT/pmc_traffic.json --config "1920x1080 K=0.25 moving" $OUT/pmc/*/ > $OUT/pmc_summary.txt
 cp $OUT/pmc_traffic.json $R/profiles/pmc_traffic.json
 timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
 tail -1 $OUT/bench.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-extras > $OUT/stats.log 2>&1
 cat $(find $OUT/stats -name "*kernel_stats.csv")
-python3 $R/scripts/trace_avg.py $(find $OUT/stats -name "*kernel_trace.csv") sf_trace_queue2 200 | tee $OUT/trace_avg.txt
+python3 $R/scripts/trace_avg.py $(find $OUT/stats -name "*kernel_trace.csv") sf_trace_queue2 200 31 | tee $OUT/trace_avg.txt
 grep '^{' $OUT/stats.log | tail -1

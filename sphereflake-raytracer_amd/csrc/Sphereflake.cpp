@@ -3,6 +3,7 @@
 #include "Sphereflake.hpp"
 
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <ctime>
 
@@ -32,6 +33,8 @@ Sphereflake::~Sphereflake()
 {
     m_Deinitialize = true;
     if (m_Worker.joinable()) m_Worker.join();
+    const int rc = m_WorkerError.exchange(SF_OK);
+    if (rc != SF_OK) std::fprintf(stderr, "sphereflake: frame-less loop failed: %s\n", sf_strerror(rc));
     sf_destroy(m_Ctx);
     if (m_Pinned) {
         sf_host_unregister(m_GBuffer.positions.data());
@@ -58,30 +61,63 @@ void Sphereflake::Render(const sf_render_params* params)
 
 // Frame-less mode: like the reference's worker threads (seeded from time(NULL), Sphereflake.cpp:88-89),
 // a host thread keeps tracing batches of random packets into the persistent G-buffer.
-void Sphereflake::Initialize()
+void Sphereflake::Initialize() { Initialize((uint32_t)time(NULL)); }
+
+void Sphereflake::Initialize(uint32_t seed, uint32_t batch)
 {
     if (m_Worker.joinable()) return;
-    m_Seed = (uint32_t)time(NULL);
-    m_Worker = std::thread([this] { ProgressiveLoop(); });
+    if (batch == 0) throw std::runtime_error("sphereflake: Initialize batch must be > 0");
+    ThrowWorkerError();
+    m_Deinitialize = false;
+    {
+        std::lock_guard<std::mutex> lk(m_Mutex);
+        m_Seed = seed;
+        m_SobolCounter = 0;
+    }
+    m_Worker = std::thread([this, batch] { ProgressiveLoop(batch); });
 }
 
-void Sphereflake::ProgressiveLoop()
+// Batches of 2^18 packets take ~1.2 ms at 1080p (binning + draw prefetch pay from 2^16). Every context
+// call is made under m_Mutex (sf.h: one context per host thread at a time); the first failure stops the
+// loop and is kept for the main thread (ThrowWorkerError).
+void Sphereflake::ProgressiveLoop(uint32_t batch)
 {
-    const uint32_t batch = 1u << 18;   // ~1.4 ms per batch at 1080p (binning + draw prefetch pay from 2^16)
     while (!m_Deinitialize) {
-        {
-            std::lock_guard<std::mutex> lk(m_Mutex);
-            int rc = sf_progressive(m_Ctx, m_Seed, m_SobolCounter, batch, nullptr);
-            if (rc != SF_OK) return;
-            m_SobolCounter += batch;
-            m_Stale = true;
+        std::lock_guard<std::mutex> lk(m_Mutex);
+        int rc = sf_progressive(m_Ctx, m_Seed, m_SobolCounter, batch, nullptr);
+        if (rc == SF_OK) rc = sf_synchronize(m_Ctx);
+        if (rc != SF_OK) {
+            int expected = SF_OK;
+            m_WorkerError.compare_exchange_strong(expected, rc);
+            return;
         }
-        sf_synchronize(m_Ctx);
+        m_SobolCounter += batch;
+        m_Stale = true;
     }
+}
+
+void Sphereflake::ThrowWorkerError() const
+{
+    const int rc = m_WorkerError.exchange(SF_OK);
+    if (rc != SF_OK) throw std::runtime_error(std::string("sphereflake: frame-less loop failed: ") + sf_strerror(rc));
+}
+
+void Sphereflake::Deinitialize()
+{
+    m_Deinitialize = true;
+    if (m_Worker.joinable()) m_Worker.join();
+    ThrowWorkerError();
+}
+
+uint64_t Sphereflake::GetPacketsTraced() const
+{
+    std::lock_guard<std::mutex> lk(m_Mutex);
+    return m_SobolCounter;
 }
 
 const GBuffer& Sphereflake::GetGBuffer() const
 {
+    ThrowWorkerError();
     std::lock_guard<std::mutex> lk(m_Mutex);
     if (m_Stale) {
         Check(sf_download(m_Ctx, &m_GBuffer.positions[0].x, &m_GBuffer.normals[0].x, nullptr, nullptr));
@@ -92,30 +128,48 @@ const GBuffer& Sphereflake::GetGBuffer() const
 
 int Sphereflake::GetMaxDepthReached() const
 {
+    ThrowWorkerError();
+    std::lock_guard<std::mutex> lk(m_Mutex);
     sf_stats s;
     Check(sf_get_stats(m_Ctx, &s));
     return s.max_depth;
 }
 
-void Sphereflake::ResetMaxDepthReached() { Check(sf_reset_max_depth(m_Ctx)); }
+void Sphereflake::ResetMaxDepthReached()
+{
+    std::lock_guard<std::mutex> lk(m_Mutex);
+    Check(sf_reset_max_depth(m_Ctx));
+}
 
 long long Sphereflake::GetRaysPerSecond() const
 {
+    ThrowWorkerError();
+    std::lock_guard<std::mutex> lk(m_Mutex);
     sf_stats s;
     Check(sf_get_stats(m_Ctx, &s));
     return (long long)s.rays;
 }
 
-void Sphereflake::ResetRaysPerSecond() { Check(sf_reset_rays(m_Ctx)); }
+void Sphereflake::ResetRaysPerSecond()
+{
+    std::lock_guard<std::mutex> lk(m_Mutex);
+    Check(sf_reset_rays(m_Ctx));
+}
 
 float Sphereflake::GetClosestSphereDistance() const
 {
+    ThrowWorkerError();
+    std::lock_guard<std::mutex> lk(m_Mutex);
     sf_stats s;
     Check(sf_get_stats(m_Ctx, &s));
     return s.closest;
 }
 
-void Sphereflake::ResetClosestSphereDistance() { Check(sf_reset_closest(m_Ctx)); }
+void Sphereflake::ResetClosestSphereDistance()
+{
+    std::lock_guard<std::mutex> lk(m_Mutex);
+    Check(sf_reset_closest(m_Ctx));
+}
 
 SSAO::SSAO(Sphereflake& flake, int downScale) : m_Flake(flake)
 {

@@ -15,7 +15,9 @@
 //     device: a host thread keeps launching batches of random 8-ray packets until destruction.
 //   - GetGBuffer() downloads the device G-buffer (D2H) when it is stale, by DMA into the vectors'
 //     storage, page-locked at construction (sf_host_register).
-//   - Errors throw std::runtime_error carrying sf_strerror() (the reference had no error path).
+//   - Errors throw std::runtime_error carrying sf_strerror() (the reference had no error path). A failure
+//     of the Initialize() loop stops the loop and is rethrown by the next GetGBuffer(), stats getter or
+//     Deinitialize() (the destructor reports it on stderr instead of throwing).
 #pragma once
 
 #include <atomic>
@@ -58,8 +60,16 @@ public:
     Sphereflake(const Sphereflake&) = delete;
     Sphereflake& operator=(const Sphereflake&) = delete;
 
-    // Frame-less progressive mode (reference Initialize(), Sphereflake.cpp:67-74).
+    // Frame-less progressive mode (reference Initialize(), Sphereflake.cpp:67-74): a host thread keeps
+    // tracing batches of `batch` random packets of one worker stream. The reference seeds from time(NULL)
+    // (Sphereflake.cpp:88-89); the overload takes an explicit seed (tests, reproducible runs).
     void Initialize();
+    void Initialize(uint32_t seed, uint32_t batch = 1u << 18);
+    // Stop the frame-less loop and join its thread (the reference does this only in its destructor,
+    // Sphereflake.cpp:57-65). Rethrows the first error the loop met, if any.
+    void Deinitialize();
+    // Packets the frame-less loop has traced so far (= its next Sobol counter).
+    uint64_t GetPacketsTraced() const;
 
     void SetView(const sf_vec3& origin, const sf_vec3& topLeft, const sf_vec3& topRight, const sf_vec3& bottomLeft);
 
@@ -81,7 +91,8 @@ public:
 
 private:
     static void Check(int rc);
-    void ProgressiveLoop();
+    void ProgressiveLoop(uint32_t batch);
+    void ThrowWorkerError() const;   // rethrows the frame-less loop's first error (held until reported once)
 
     size_t m_Width, m_Height;
     sf_ctx* m_Ctx = nullptr;
@@ -91,6 +102,7 @@ private:
     mutable std::mutex m_Mutex;
     std::thread m_Worker;
     std::atomic<bool> m_Deinitialize{ false };
+    mutable std::atomic<int> m_WorkerError{ SF_OK };   // first failure of the frame-less loop
     uint64_t m_SobolCounter = 0;
     uint32_t m_Seed = 0;
 };

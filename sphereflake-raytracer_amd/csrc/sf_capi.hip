@@ -113,7 +113,6 @@ struct sf_ctx {
     int occ_key = -1, occ_blocks = 0;            // cached occupancy (waves per block, levels) -> blocks per CU
     uint32_t max_blocks = 0;                     // diagnostics: env SF_MAX_BLOCKS caps the persistent grid
     int variant = SF_VARIANT_AVX;                // reference path reproduced (sf_set_variant)
-    uint32_t prio_tiles = 2048;                  // tuning knob: env SF_PRIO_TILES (heaviest order positions at s_setprio 3)
     // frame-less progressive mode
     uint32_t* mt_state = nullptr;      // 624 words + next index (std::mt19937 layout)
     uint32_t* draws = nullptr;         // 2 per packet
@@ -162,7 +161,11 @@ struct sf_ctx {
     uint32_t* order_meta = nullptr;    // [0] work units in tile_order, [1] first split bucket
     uint32_t split_buckets = SF_SPLIT_AUTO;   // env SF_SPLIT_BUCKETS = k: top k buckets (0: never split)
     uint32_t order_n = 0;              // tile count the current tile_order is a permutation of (0: none)
-    hipStream_t order_stream = nullptr;   // the stream it was computed on (used only on the same stream)
+    // Stream ordering across calls: every call that enqueues work on the context's buffers first joins
+    // the stream of the previous such call (ctx_join), so renders, frame-less batches, post-processing
+    // and downloads issued on different streams of one context run in call order, as on one stream.
+    hipStream_t last_stream = nullptr; // stream of the latest enqueued work (nullptr: the context stream)
+    hipEvent_t join_ev = nullptr;      // recorded on last_stream when a call switches streams
     bool use_order = true;             // env SF_ORDER=0: row-major order always
     // Measurement: HIP events around the main trace kernel of each render (sf_set_kernel_timing)
     static constexpr int kTimed = 64;
@@ -189,11 +192,34 @@ struct sf_ctx {
         }                                                        \
     } while (0)
 
+// Order work about to be enqueued on `s` after everything the context enqueued before, on whatever
+// stream (one event record + wait, only when the stream changes; same-stream calls cost nothing).
+static int ctx_join(sf_ctx* c, hipStream_t s)
+{
+    hipStream_t last = c->last_stream ? c->last_stream : c->stream;
+    if (s == last) return SF_OK;
+    if (!c->join_ev) SF_HIP(c, hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
+    SF_HIP(c, hipEventRecord(c->join_ev, last));
+    SF_HIP(c, hipStreamWaitEvent(s, c->join_ev, 0));
+    c->last_stream = s;
+    return SF_OK;
+}
+
+// Host-synchronous drain: all work the context enqueued on any stream is done.
+static int ctx_drain(sf_ctx* c)
+{
+    if (int rc = ctx_join(c, c->stream)) return rc;
+    SF_HIP(c, hipStreamSynchronize(c->stream));
+    return SF_OK;
+}
+
 static void free_ctx(sf_ctx* c)
 {
     if (!c) return;
     DevGuard g(c->device);
+    if (c->last_stream) (void)hipStreamSynchronize(c->last_stream);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->join_ev) (void)hipEventDestroy(c->join_ev);
     (void)hipFree(c->pos);
     (void)hipFree(c->nrm);
     (void)hipFree(c->min_t);
@@ -252,6 +278,7 @@ static int upload_consts(sf_ctx* c)
     }
     std::memcpy(c->host_consts.lut, kLut, sizeof kLut);
     sfhost::sobol_matrices(c->host_consts.sobol);
+    if (int rc_ = ctx_drain(c)) return rc_;   // no kernel of the context may still read the block
     SF_HIP(c, hipMemcpyAsync(c->consts, &c->host_consts, sizeof(DeviceConsts), hipMemcpyHostToDevice, c->stream));
     SF_HIP(c, hipStreamSynchronize(c->stream));
     return SF_OK;
@@ -261,6 +288,7 @@ static int reset_stats_dev(sf_ctx* c, int which)
 {
     // which: bit0 max depth, bit1 closest
     int32_t init[2] = { -1, sf_float_key(FLT_MAX) };
+    if (int rc_ = ctx_join(c, c->stream)) return rc_;   // after every render that updates the words
     if (which & 1) SF_HIP(c, hipMemcpyAsync(c->stats + 0, &init[0], 4, hipMemcpyHostToDevice, c->stream));
     if (which & 2) SF_HIP(c, hipMemcpyAsync(c->stats + 1, &init[1], 4, hipMemcpyHostToDevice, c->stream));
     SF_HIP(c, hipStreamSynchronize(c->stream));
@@ -320,7 +348,6 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if (const char* ev = std::getenv("SF_SPLIT_BUCKETS")) c->split_buckets = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_FLAGS")) c->flags = (uint32_t)std::strtoul(ev, nullptr, 0);
-    if (const char* ev = std::getenv("SF_PRIO_TILES")) c->prio_tiles = (uint32_t)std::strtoul(ev, nullptr, 0);
     if (const char* ev = std::getenv("SF_TRACE_WAVES")) {
         const int w = std::atoi(ev);
         c->waves_per_block = (w == 1 || w == 2 || w == 4) ? (uint32_t)w : SF_TRACE_WAVES;
@@ -465,6 +492,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
     hipStream_t s = p.stream ? (hipStream_t)p.stream : c->stream;
     DevGuard g(c->device);
     if (tile_rows == 0) return SF_OK;
+    if (int rc = ctx_join(c, s)) return rc;
 
     FrameArgs a = frame_args(c);
     a.tile_rows = tile_rows;
@@ -545,9 +573,8 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             if (c->use_order) {
                 a.tile_cost = c->tile_cost;
                 a.chunk_cnt = c->chunk_cnt;
-                a.tile_order = (c->order_n == ntiles && c->order_stream == s) ? c->tile_order : nullptr;
+                a.tile_order = c->order_n == ntiles ? c->tile_order : nullptr;   // ordered by ctx_join
                 a.order_meta = c->order_meta;
-                a.prio_tiles = c->prio_tiles;
             }
             const bool timed = c->timing && c->ev_phase == 0;
             if (c->timing) c->ev_phase = (c->ev_phase + 1u) % c->ev_period;
@@ -573,7 +600,6 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                                    c->tile_order);
                 SF_HIP(c, hipGetLastError());
                 c->order_n = ntiles;
-                c->order_stream = s;
             }
         } else {
             const dim3 grid((ntiles + wpb - 1) / wpb);
@@ -628,6 +654,7 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     if (packets == 0) return SF_OK;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     DevGuard g(c->device);
+    if (int rc = ctx_join(c, s)) return rc;
     if (!c->mt_state) {
         SF_HIP(c, hipMalloc(&c->mt_state, 625 * 4));
         SF_HIP(c, hipMalloc(&c->owner, (size_t)c->W * c->H * 8));
@@ -790,7 +817,7 @@ int sf_synchronize(sf_ctx* c)
 {
     if (!c) return SF_EINVAL;
     DevGuard g(c->device);
-    SF_HIP(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = ctx_drain(c)) return rc_;
     int32_t st[3];
     SF_HIP(c, hipMemcpy(st, c->stats, 12, hipMemcpyDeviceToHost));
     if (st[2] != 0) return SF_EDEPTH;
@@ -820,6 +847,7 @@ int sf_download_async(sf_ctx* c, float* pos4, float* nrm4, float* min_t, uint32_
     DevGuard g(c->device);
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     const size_t npx = (size_t)c->W * c->H;
+    if (int rc = ctx_join(c, s)) return rc;
     if (pos4) SF_HIP(c, hipMemcpyAsync(pos4, c->pos, npx * 16, hipMemcpyDeviceToHost, s));
     if (nrm4) SF_HIP(c, hipMemcpyAsync(nrm4, c->nrm, npx * 16, hipMemcpyDeviceToHost, s));
     if (min_t) SF_HIP(c, hipMemcpyAsync(min_t, c->min_t, npx * 4, hipMemcpyDeviceToHost, s));
@@ -870,6 +898,7 @@ int sf_post_process(sf_ctx* c, const sf_post_params* prm, const float* pos4, con
     DevGuard g(c->device);
     hipStream_t s = prm->stream ? (hipStream_t)prm->stream : c->stream;
     const size_t npx = (size_t)c->W * c->H;
+    if (int rc = ctx_join(c, s)) return rc;
     if (!c->noise) {
         static float host_noise[SF_NOISE_SIZE * SF_NOISE_SIZE * 4];
         sfhost::ssao_noise(host_noise);
@@ -949,7 +978,7 @@ int sf_set_variant(sf_ctx* c, int variant)
     if (!c || (variant != SF_VARIANT_AVX && variant != SF_VARIANT_SSE)) return SF_EINVAL;
     if (variant == c->variant) return SF_OK;
     DevGuard g(c->device);
-    SF_HIP(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = ctx_drain(c)) return rc_;
     c->variant = variant;
     c->order_n = 0;       // tile costs of the other variant's frames: start over
     *c->h_depth = -1;     // level hint likewise
@@ -962,7 +991,7 @@ int sf_set_tile_trace(sf_ctx* c, int enable)
 {
     if (!c) return SF_EINVAL;
     DevGuard g(c->device);
-    SF_HIP(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = ctx_drain(c)) return rc_;
     if (!enable) {
         (void)hipFree(c->tile_trace);
         c->tile_trace = nullptr;
@@ -970,8 +999,8 @@ int sf_set_tile_trace(sf_ctx* c, int enable)
     }
     if (!c->tile_trace) {
         const size_t ntiles = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8);
-        SF_HIP(c, hipMalloc(&c->tile_trace, (ntiles * 3 + 8) * 8));
-        SF_HIP(c, hipMemset(c->tile_trace, 0, (ntiles * 3 + 8) * 8));
+        SF_HIP(c, hipMalloc(&c->tile_trace, (ntiles * 3 + SF_DIAG_SLOTS) * 8));
+        SF_HIP(c, hipMemset(c->tile_trace, 0, (ntiles * 3 + SF_DIAG_SLOTS) * 8));
     }
     return SF_OK;
 }
@@ -982,9 +1011,10 @@ int sf_get_tile_trace(sf_ctx* c, uint64_t* out, size_t n)
     DevGuard g(c->device);
     const size_t ntiles = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8);
     if (n < ntiles * 3) return SF_EINVAL;
-    SF_HIP(c, hipStreamSynchronize(c->stream));
-    // n >= 3 * tiles + 8 also returns the 8 segment sums of stamp builds (zeros otherwise)
-    SF_HIP(c, hipMemcpy(out, c->tile_trace, (n >= ntiles * 3 + 8 ? ntiles * 3 + 8 : ntiles * 3) * 8,
+    if (int rc_ = ctx_drain(c)) return rc_;
+    // n >= 3 * tiles + SF_DIAG_SLOTS also returns the segment sums / event counts of the diagnostic
+    // builds (zeros otherwise)
+    SF_HIP(c, hipMemcpy(out, c->tile_trace, (n >= ntiles * 3 + SF_DIAG_SLOTS ? ntiles * 3 + SF_DIAG_SLOTS : ntiles * 3) * 8,
                         hipMemcpyDeviceToHost));
     return SF_OK;
 }
@@ -995,7 +1025,7 @@ int sf_get_tile_order(sf_ctx* c, uint32_t* order, uint32_t* cost, size_t n)
     DevGuard g(c->device);
     const size_t ntiles = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8);
     if (n < ntiles || (!order && !cost)) return SF_EINVAL;
-    SF_HIP(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = ctx_drain(c)) return rc_;
     if (c->order_n != ntiles) return 0;
     uint32_t meta[2];
     SF_HIP(c, hipMemcpy(meta, c->order_meta, sizeof(meta), hipMemcpyDeviceToHost));
@@ -1034,7 +1064,7 @@ int sf_kernel_times(sf_ctx* c, float* ms, uint32_t n)
 {
     if (!c || !ms) return SF_EINVAL;
     DevGuard g(c->device);
-    SF_HIP(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = ctx_drain(c)) return rc_;
     const uint32_t k = n < c->ev_count ? n : c->ev_count;
     for (uint32_t i = 0; i < k; ++i) {   // the k most recent, oldest first
         const uint32_t slot = (c->ev_next + sf_ctx::kTimed - k + i) % sf_ctx::kTimed;
@@ -1048,7 +1078,7 @@ int sf_get_stats(sf_ctx* c, sf_stats* out)
 {
     if (!c || !out) return SF_EINVAL;
     DevGuard g(c->device);
-    SF_HIP(c, hipStreamSynchronize(c->stream));
+    if (int rc_ = ctx_drain(c)) return rc_;
     int32_t st[3];
     SF_HIP(c, hipMemcpy(st, c->stats, 12, hipMemcpyDeviceToHost));
     out->max_depth = st[0] < 0 ? 0 : st[0];

@@ -21,11 +21,12 @@
 #endif
 // Wave-coherent traversal LDS image, per wave (units: floats):
 //   [root: 16][cone: 8][(levels - 1) x (table 144 | E 32)]
-// A transform is 16 floats: [cx cy cz cc | col0.xyz - | col1.xyz - | col2.xyz -] (cc = Dot(centre, centre)).
+// A transform is 4 float4 {cx cy cz cc}, {col0.xyz -}, {col1.xyz -}, {col2.xyz -} (cc = Dot(centre, centre));
+// a level table stores them in 4 planes of 9 float4 (plane k = float4 k of children 0..8).
 #define SF_LDS_ROOT 16
 #define SF_LDS_CONE 8                     // the wave's ray cone {ax, ay, az, cosT, sinT, -, -, -}
-#define SF_LDS_CHILD 16
-#define SF_LDS_TABLE (9 * SF_LDS_CHILD)   // the 9 child transforms of the node open at a level
+#define SF_LDS_PLANE 36                   // one float4 of each of the 9 children (column planes)
+#define SF_LDS_TABLE (4 * SF_LDS_PLANE)   // the 9 child transforms of the node open at a level
 #define SF_LDS_E 32                       // 64 lanes x u16: per-lane child-expand bits of that node
 #define SF_LDS_LEVEL (SF_LDS_TABLE + SF_LDS_E)
 // levels - 1 level images: the deepest provisioned level's table is never read (see traverse)
@@ -37,6 +38,9 @@
 #define SF_QUEUE_STRIDE 32u
 #define SF_QUEUE_WORD(parity, k) (SF_QUEUE_STRIDE + ((parity) * SF_QUEUES + (k)) * SF_QUEUE_STRIDE)
 #define SF_COUNTER_WORDS (SF_QUEUE_STRIDE + 2u * SF_QUEUES * SF_QUEUE_STRIDE)
+
+// 64-bit diagnostic slots after the per-tile trace (segment sums of PHASES=1, event counts of COUNTS=1)
+#define SF_DIAG_SLOTS 16
 
 #define SF_FLAG_NO_LOD_CULL 1u    // disable the leaf-threshold skip (A/B only; results identical)
 #define SF_FLAG_NO_CONE_CULL 2u   // disable the per-child ray-cone cull (A/B only; results identical)
@@ -100,7 +104,6 @@ struct FrameArgs {
     const uint32_t* order_meta;       // with tile_order: [0] units in it, [1] first split bucket
     uint32_t* chunk_cnt;              // out (with tile_cost): per 64-tile chunk, cost-bucket histogram
     uint32_t packet_lanes;            // frame-less mode: 8 (AVX variant) or 4 (SSE variant, 2x2 footprint)
-    uint32_t prio_tiles;              // order positions traced at raised wave priority (s_setprio)
 };
 
 // Headless SSAO post-process (Shaders/post_ssao.glsl, post_ssao_blur.glsl,

@@ -176,8 +176,9 @@ __device__ __forceinline__ bool group_any(bool p)
 //   self       hs = active && any_g(tca >= 0) && any_g(d2 <= r^2); accept lanes with d2 <= r^2 && t < minT
 // For per-ray groups these are exactly the reference's per-lane tests.
 // ------------------------------------------------------------------------------------------
-// Per-wave LDS image (floats): [root: 16][per level: table 9 x 16 | E 32]. A transform is 16 floats:
-// [cx cy cz cc | col0.xyz - | col1.xyz - | col2.xyz -] (cc = Dot(centre, centre)).
+// Per-wave LDS image (floats): [root: 16][cone: 8][per level: table 4 planes x 9 x 4 | E 32]. A transform
+// is 4 float4: {cx cy cz cc}, {col0.xyz -}, {col1.xyz -}, {col2.xyz -} (cc = Dot(centre, centre)); the root
+// keeps them contiguous, a level table in planes (plane k = float4 k of the 9 children, SF_LDS_PLANE apart).
 struct TraverseLds {
     float* base;
     __device__ __forceinline__ float* root() const { return base; }
@@ -248,14 +249,18 @@ __device__ __forceinline__ void wave_atomic_add_u64(uint64_t* p, uint64_t v)
 #elif defined(SF_COUNTS)
 // Diagnostic build only (make COUNTS=1): per-wave event counts instead of stamps, summed into
 // phase_sums[k]: 0 nodes whose children are tested, 1 child-loop iterations, 2 iterations no lane
-// hits (bounding), 3 children entered, 4 leaf skips.
-#define SF_STAMP_DECL uint64_t ph_sum[7] = {0, 0, 0, 0, 0, 0, 0}
+// hits (bounding), 3 children entered, 4 leaf skips; lane utilisation: 5 active lanes summed over
+// child-loop iterations, 6 bounding-hit lanes summed over them, 7 active lanes summed over expanded
+// nodes, 8 inline leaf self tests, 9 their active lanes, 10 child-loop iterations at node depth >= 4,
+// 11 their active lanes, 12/13/14 iterations with <= 4 / <= 16 / <= 32 active lanes, 15 waves traced.
+#define SF_STAMP_DECL uint64_t ph_sum[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}
 #define SF_STAMP(k)
 #define SF_COUNT(k, v) (ph_sum[k] += (v))
 #define SF_STAMP_FLUSH(p)                                                                      \
     do {                                                                                       \
         if (p) {                                                                               \
-            for (int k_ = 0; k_ < 5; ++k_) wave_atomic_add_u64((uint64_t*)(p) + k_, ph_sum[k_]);  \
+            ph_sum[15] = 1;                                                                    \
+            for (int k_ = 0; k_ < 16; ++k_) wave_atomic_add_u64((uint64_t*)(p) + k_, ph_sum[k_]); \
         }                                                                                      \
     } while (0)
 #else
@@ -314,7 +319,8 @@ template <int PW>   // packet width of the semantics: 0 per ray, 8 (AVX) or 4 (S
 __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ Lbase,
                                          uint32_t levels, float dx, float dy, float dz, bool valid, HitState& h,
                                          int32_t& maxd, bool& overflowed, uint32_t K_flags,
-                                         uint64_t* phase_sums = nullptr, uint32_t axl = 36u)
+                                         uint64_t* phase_sums = nullptr, uint32_t axl = 36u,
+                                         uint64_t* tile_counts = nullptr)
 {
     constexpr bool PACKET = PW != 0;
     const uint32_t lane = threadIdx.x & 63u;
@@ -380,7 +386,9 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     float b[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) b[j] = K->child[bi][4u * bc + j];
-    const uint32_t slot = bi * SF_LDS_CHILD + (bc == 3u ? 0u : 4u + 4u * bc);
+    // level table in column planes: plane k (0 = {centre, cc}, 1..3 = columns 0..2) holds the 9 children's
+    // float4 contiguously, so the build's float4 stores from consecutive lanes are conflict-free
+    const uint32_t slot = (bc == 3u ? 0u : bc + 1u) * SF_LDS_PLANE + bi * 4u;
 
     uint32_t d = 0;                 // uniform: depth of the open (expanded) node
     uint32_t cN = 0;                // uniform: its index in the parent's table
@@ -417,13 +425,15 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     // ---- expand the node at `node` (depth d, transform in LDS): build its 9 child transforms into
     // table(d), then test the children (depth d+1) for the lanes in `act`. Returns this lane's 9-bit
     // "child expands" vector; *pend = the wave's mask of children some lane expands.
-    auto expand = [&](const float* node, uint32_t d, bool act, uint32_t& pend) -> uint32_t {
+    // (node: its 4 float4 at node, node + ps, node + 2 ps, node + 3 ps: ps = 4 for the root image,
+    // SF_LDS_PLANE for a level table)
+    auto expand = [&](const float* node, uint32_t ps, uint32_t d, bool act, uint32_t& pend) -> uint32_t {
         d = __builtin_amdgcn_readfirstlane(d);   // wave-uniform: depth constants come by scalar loads
         lds_fence();
         const float4 pc = *reinterpret_cast<const float4*>(node);
-        const float4 p0 = *reinterpret_cast<const float4*>(node + 4);
-        const float4 p1 = *reinterpret_cast<const float4*>(node + 8);
-        const float4 p2 = *reinterpret_cast<const float4*>(node + 12);
+        const float4 p0 = *reinterpret_cast<const float4*>(node + ps);
+        const float4 p1 = *reinterpret_cast<const float4*>(node + 2u * ps);
+        const float4 p2 = *reinterpret_cast<const float4*>(node + 3u * ps);
         const float4 dtn = depth_consts(K, d);        // this node: r^2, (4/3) r
         const float4 dtc = depth_consts(K, d + 1u);   // children: (2r)^2, T
         self_test(pc, d, act, idxN, dtn.y);
@@ -478,6 +488,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             // are formed only where a lane's own bit is needed (its E bit).
             const uint64_t actm = wave_ballot(act);
             SF_COUNT(0, 1);
+            SF_COUNT(7, __builtin_popcountll(actm));
             while (M) {   // uniform loop over the children some lane can reach, in index order
                 const uint32_t i = __builtin_ctz(M);
                 M &= M - 1u;
@@ -488,6 +499,13 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 const float d2 = cc - tca * tca;
                 const bool f0 = tca >= 0.0f, f1 = d2 <= R2b;
                 const uint64_t hbm = actm & wave_ballot(f0) & wave_ballot(f1);   // bounding (SIMD_AVX.h:247-258)
+                SF_COUNT(5, __builtin_popcountll(actm));
+                SF_COUNT(6, __builtin_popcountll(hbm));
+                SF_COUNT(10, d >= 4u ? 1 : 0);
+                SF_COUNT(11, d >= 4u ? __builtin_popcountll(actm) : 0);
+                SF_COUNT(12, __builtin_popcountll(actm) <= 4 ? 1 : 0);
+                SF_COUNT(13, __builtin_popcountll(actm) <= 16 ? 1 : 0);
+                SF_COUNT(14, __builtin_popcountll(actm) <= 32 ? 1 : 0);
                 if (hbm == 0ull) {
                     SF_COUNT(2, 1);
                     continue;
@@ -553,7 +571,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     // Lane selects: no LDS traffic and no lane-0-only region in the loop.
     uint32_t stk_pc = 0u, stk_ix = 0u;
     uint32_t pend;
-    uint32_t eN = expand(L.root(), 0u, ex0, pend);
+    uint32_t eN = expand(L.root(), 4u, 0u, ex0, pend);
 
     for (;;) {
         d = __builtin_amdgcn_readfirstlane(d);
@@ -567,7 +585,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 continue;
             }
             const bool a = ((eN >> c) & 1u) != 0u;
-            const float* node = L.table(d) + c * SF_LDS_CHILD;
+            const float* node = L.table(d) + c * 4u;
             if (lod_cull) {
                 // A child none of whose children can pass LOD for any ray (sfhost::leaf_threshold) only
                 // needs its own sphere: test it here, in its DFS turn, without a push or a level.
@@ -575,6 +593,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 const float4 pc = *reinterpret_cast<const float4*>(node);
                 if (__builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, d + 1u)))) {
                     SF_COUNT(4, 1);
+                    SF_COUNT(8, 1);
+                    SF_COUNT(9, __builtin_popcountll(wave_ballot(a)));
                     maxd = (int32_t)d + 1 > maxd ? (int32_t)d + 1 : maxd;   // Sphereflake.h:157-160
                     self_test(pc, d + 1u, a, 9u * idxN + 1u + c, depth_consts(K, d + 1u).y);
                     anc = anc & (h.depth != (int32_t)d + 1);   // the child is finished
@@ -590,7 +610,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             d += 1u;
             maxd = (int32_t)d > maxd ? (int32_t)d : maxd;            // Sphereflake.h:157-160
             SF_STAMP(1);
-            eN = expand(node, d, a, pend);
+            eN = expand(node, SF_LDS_PLANE, d, a, pend);
             SF_STAMP(2);
             continue;
         }
@@ -612,6 +632,16 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         SF_STAMP(5);
     }
     SF_STAMP_FLUSH(phase_sums);
+#ifdef SF_COUNTS
+    // per tile (COUNTS=1 builds): expanded nodes | child iterations << 16 | bounding-hit iterations << 32 |
+    // inline leaf tests << 48 (16 bits each, saturating)
+    if (tile_counts) {
+        auto sat = [](uint64_t v) { return v > 0xffffull ? 0xffffull : v; };
+        *tile_counts = sat(ph_sum[0]) | (sat(ph_sum[1]) << 16) | (sat(ph_sum[1] - ph_sum[2]) << 32) | (sat(ph_sum[8]) << 48);
+    }
+#else
+    (void)tile_counts;
+#endif
 }
 
 struct Tile {
@@ -722,8 +752,9 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     HitState h;
     int32_t maxd = -1;
     bool overflowed = false;
+    uint64_t tile_counts = 0;
     traverse<0>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed, a.flags,
-                    FIXUP ? nullptr : a.phase_sums, half == 0u ? 36u : half == 1u ? 20u : 52u);
+                    FIXUP ? nullptr : a.phase_sums, half == 0u ? 36u : half == 1u ? 20u : 52u, &tile_counts);
     if (!FIXUP && a.tile_trace) {
         // diagnostics only: never read by the kernel, never feeds an output value. Every lane stores
         // the same (uniform) words: no lane-0-only region.
@@ -734,7 +765,11 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
         __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         a.tile_trace[3u * tile + 0u] = t_start;
         a.tile_trace[3u * tile + 1u] = t_end;
+#ifdef SF_COUNTS
+        a.tile_trace[3u * tile + 2u] = tile_counts;   // COUNTS=1 builds: the tile's event counts instead
+#else
         a.tile_trace[3u * tile + 2u] = ((uint64_t)xcc << 32) | hw;
+#endif
     }
 
     if (!FIXUP && a.tile_cost && half <= 1u) {
@@ -875,11 +910,7 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
             t = u & SF_UNIT_TILE_MASK;
             half = u >> SF_UNIT_HALF_SHIFT;
         }
-        // the heaviest tiles of the previous render bound the frame: give their waves issue priority
-        const bool prio = at.tile_order && g < at.prio_tiles;
-        if (prio) __builtin_amdgcn_s_setprio(3);
         const TileStats st = trace_tile<false>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity, half);
-        if (prio) __builtin_amdgcn_s_setprio(0);
         maxd = st.maxd > maxd ? st.maxd : maxd;
         closest = fminf(closest, st.closest);
     }

@@ -294,6 +294,7 @@ class Sphereflake:
         self._mutex = threading.Lock()
         self._seed = 0
         self._counter = 0
+        self._worker_error = None
 
     # lifetime --------------------------------------------------------------
     def close(self):
@@ -370,6 +371,7 @@ class Sphereflake:
         mint = np.empty((H, W), np.float32) if aux else None
         idx = np.empty((H, W), np.uint32) if aux else None
         vp = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+        self._raise_worker_error()
         with self._mutex:
             _check(lib().sf_download(self._ctx, vp(pos), vp(nrm), vp(mint), vp(idx)), "download", self._ctx)
         return pos, nrm, mint, idx
@@ -468,7 +470,7 @@ class Sphereflake:
             _check(lib().sf_set_tile_trace(self._ctx, int(bool(enable))), "sf_set_tile_trace", self._ctx)
             return None
         n = ((self.width + 7) // 8) * ((self.height + 7) // 8)
-        out = np.zeros(3 * n + 8, np.uint64)
+        out = np.zeros(3 * n + 16, np.uint64)   # + SF_DIAG_SLOTS
         _check(lib().sf_get_tile_trace(self._ctx, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), out.size),
                "sf_get_tile_trace", self._ctx)
         self.phase_sums = out[3 * n:]          # segment cycle sums of stamp builds (zeros otherwise)
@@ -502,8 +504,10 @@ class Sphereflake:
 
     # stats (Sphereflake.h:30-58) --------------------------------------------
     def stats(self) -> sf_stats:
+        self._raise_worker_error()
         s = sf_stats()
-        _check(lib().sf_get_stats(self._ctx, ctypes.byref(s)), "sf_get_stats", self._ctx)
+        with self._mutex:
+            _check(lib().sf_get_stats(self._ctx, ctypes.byref(s)), "sf_get_stats", self._ctx)
         return s
 
     def GetMaxDepthReached(self) -> int:
@@ -526,25 +530,54 @@ class Sphereflake:
         _check(lib().sf_reset_closest(self._ctx), "ResetClosestSphereDistance")
 
     # frame-less progressive mode (Sphereflake.cpp:67-74, 86-214) -------------
-    def Progressive(self, seed: int, packets: int, counter0: int | None = None):
+    def Progressive(self, seed: int, packets: int, counter0: int | None = None, stream=None):
         """Trace `packets` random 8-ray packets of one reference worker stream (seed, Sobol counter)."""
         c0 = self._counter if counter0 is None else int(counter0)
         with self._mutex:
-            _check(lib().sf_progressive(self._ctx, seed & 0xffffffff, c0, packets, None), "sf_progressive", self._ctx)
+            _check(lib().sf_progressive(self._ctx, seed & 0xffffffff, c0, packets, stream), "sf_progressive",
+                   self._ctx)
         self._counter = c0 + packets
 
     def Initialize(self, seed: int | None = None, batch: int = 1 << 18):
-        """Start the frame-less progressive loop on a host thread (reference Initialize())."""
+        """Start the frame-less progressive loop on a host thread (reference Initialize(),
+        Sphereflake.cpp:67-74; seeded from time() like Sphereflake.cpp:88-89 unless `seed` is given).
+        The loop's first error stops it and is re-raised by the next GetGBuffer / stats call /
+        Deinitialize."""
         import time
         if self._worker is not None:
             return
+        self._raise_worker_error()
         self._seed = int(time.time()) if seed is None else int(seed)
+        self._counter = 0
         self._stop.clear()
 
         def loop():
-            while not self._stop.is_set():
-                self.Progressive(self._seed, batch)
-                self.Synchronize()
+            try:
+                while not self._stop.is_set():
+                    with self._mutex:
+                        _check(lib().sf_progressive(self._ctx, self._seed & 0xffffffff, self._counter, batch, None),
+                               "sf_progressive", self._ctx)
+                        _check(lib().sf_synchronize(self._ctx), "sf_synchronize", self._ctx)
+                        self._counter += batch
+            except Exception as e:   # kept for the caller's thread
+                self._worker_error = e
 
         self._worker = threading.Thread(target=loop, daemon=True)
         self._worker.start()
+
+    def Deinitialize(self):
+        """Stop the frame-less loop and join it (the reference does this in its destructor)."""
+        self._stop.set()
+        if self._worker is not None:
+            self._worker.join()
+            self._worker = None
+        self._raise_worker_error()
+
+    def GetPacketsTraced(self) -> int:
+        with self._mutex:
+            return self._counter
+
+    def _raise_worker_error(self):
+        e, self._worker_error = getattr(self, "_worker_error", None), None
+        if e is not None:
+            raise RuntimeError(f"frame-less loop failed: {e}") from e

@@ -7,16 +7,70 @@
 //   of the last frame to out.bin and prints "max_depth rays closest(hex)" on stdout. With image.bin,
 //   also runs the headless SSAO chain as main.cpp:312-330 does (radius from GetClosestSphereDistance,
 //   camera = origin) and writes the RGBA8 image.
+//
+// usage: class_drive --initialize W H corners(12) out.bin seed batch ms
+//   the frame-less mode as main.cpp:120-121 starts it: SetView, Initialize(seed, batch), let the loop run
+//   `ms` milliseconds (reading GetGBuffer meanwhile, as the render loop does), Deinitialize; writes the
+//   G-buffer and prints "packets max_depth rays" (the frame equals `packets / batch` sequential
+//   sf_progressive(seed, k * batch, batch) calls, which the test checks).
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <exception>
+#include <thread>
 
 #include "Sphereflake.hpp"
 
 using namespace SphereflakeRaytracer;
 
+static int initialize_mode(int argc, char** argv)
+{
+    if (argc < 19) return 2;
+    const size_t W = std::strtoul(argv[2], nullptr, 10), H = std::strtoul(argv[3], nullptr, 10);
+    float v[12];
+    for (int k = 0; k < 12; ++k) v[k] = std::strtof(argv[4 + k], nullptr);
+    const uint32_t seed = (uint32_t)std::strtoul(argv[17], nullptr, 0);
+    const uint32_t batch = (uint32_t)std::strtoul(argv[18], nullptr, 0);
+    const int ms = argc > 19 ? std::atoi(argv[19]) : 200;
+    Sphereflake flake(W, H);
+    // --initialize-noview: no SetView, so the loop's first batch fails (SF_ENOVIEW); the error must
+    // surface in this thread (GetGBuffer / Deinitialize throw), not vanish with the worker
+    if (std::strcmp(argv[1], "--initialize-noview") != 0)
+        flake.SetView(sf_vec3(v[0], v[1], v[2]), sf_vec3(v[3], v[4], v[5]), sf_vec3(v[6], v[7], v[8]),
+                      sf_vec3(v[9], v[10], v[11]));
+    flake.Initialize(seed, batch);
+    const auto t0 = std::chrono::steady_clock::now();
+    size_t reads = 0;
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(ms)) {
+        const GBuffer& g = flake.GetGBuffer();   // the render loop's per-frame read (main.cpp:306-310)
+        if (g.positions.size() != W * H) return 3;
+        ++reads;
+        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    }
+    flake.Deinitialize();
+    const uint64_t packets = flake.GetPacketsTraced();
+    const GBuffer& g = flake.GetGBuffer();
+    FILE* out = std::fopen(argv[16], "wb");
+    if (!out) return 4;
+    std::fwrite(g.positions.data(), sizeof(sf_vec4), g.positions.size(), out);
+    std::fwrite(g.normals.data(), sizeof(sf_vec4), g.normals.size(), out);
+    std::fclose(out);
+    std::printf("%llu %d %lld %zu\n", (unsigned long long)packets, flake.GetMaxDepthReached(),
+                flake.GetRaysPerSecond(), reads);
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
+    if (argc > 1 && std::strncmp(argv[1], "--initialize", 12) == 0) {
+        try {
+            return initialize_mode(argc, argv);
+        } catch (const std::exception& e) {
+            std::fprintf(stderr, "%s\n", e.what());
+            return 1;
+        }
+    }
     if (argc < 16) {
         std::fprintf(stderr, "usage: %s W H o.xyz tl.xyz tr.xyz bl.xyz out.bin [frames]\n", argv[0]);
         return 2;

@@ -1,0 +1,108 @@
+"""GPU tests of the frame-less Initialize() mode of the drop-in classes (reference Initialize() +
+DoImagePart, /root/reference/sphereflake/Sphereflake.cpp:67-74,86-214):
+- the C++ class (csrc/Sphereflake.hpp) run as main.cpp:120-121 starts it -- SetView, Initialize, the
+  render loop reading GetGBuffer meanwhile, then stop -- must leave exactly the G-buffer of the same
+  number of sequential sf_progressive batches of that seed (bit for bit), count 8 rays per packet and
+  join its thread;
+- the Python mirror likewise;
+- a failure inside the loop (no view set) must surface in the caller's thread instead of ending the
+  worker silently."""
+import os
+import subprocess
+import time
+
+import numpy as np
+import pytest
+
+from conftest import PKG
+
+pytestmark = pytest.mark.gpu
+
+import sphereflake_amd as sf  # noqa: E402
+
+DRIVE = os.path.join(PKG, "build", "class_drive")
+W, H, K = 160, 96, 0.25
+SEED, BATCH = 777, 4096
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    sf.build()
+    assert sf.device_count() >= 1, "no HIP device visible: GPU tests must run on an MI355X"
+    assert os.path.exists(DRIVE), "class_drive not built (make -C sphereflake-raytracer_amd)"
+
+
+def sequential_frame(packets):
+    """The G-buffer of packets / BATCH sequential sf_progressive calls of one worker stream."""
+    assert packets % BATCH == 0
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for k in range(packets // BATCH):
+            s.Progressive(SEED, BATCH, k * BATCH)
+        pos, nrm, _, _ = s.download()
+        st = s.stats()
+    return pos, nrm, st
+
+
+def check_layout(pos, nrm):
+    written = pos[..., 3] == 1.0
+    assert written.any(), "the frame-less loop wrote no pixel"
+    # unwritten pixels keep the zero-initialised vec4 (glm default ctor); written ones are (x, y, z, 1)
+    assert np.all(pos[~written] == 0.0) and np.all(nrm[~written] == 0.0)
+    assert np.all(nrm[written][:, 3] == 1.0)
+    return written
+
+
+def test_cpp_initialize_equals_sequential_batches(tmp_path):
+    corners = sf.config_camera(W, H, K).corners()
+    out = tmp_path / "init.bin"
+    args = [DRIVE, "--initialize", str(W), str(H)] + [float(x).hex() for c in corners for x in c]
+    r = subprocess.run(args + [str(out), str(SEED), str(BATCH), "300"], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr
+    packets, max_depth, rays, reads = (int(x) for x in r.stdout.split())
+    assert packets > 0 and packets % BATCH == 0, packets
+    assert reads > 0
+    assert rays == 8 * packets                      # m_RaysPerSecond += 8 per packet (Sphereflake.cpp:184)
+    g = np.fromfile(out, np.float32).reshape(2, H, W, 4)
+    check_layout(g[0], g[1])
+    pos, nrm, st = sequential_frame(packets)
+    assert np.array_equal(g[0].view(np.uint32), pos.view(np.uint32))
+    assert np.array_equal(g[1].view(np.uint32), nrm.view(np.uint32))
+    assert max_depth == st.max_depth
+
+
+def test_cpp_initialize_error_surfaces(tmp_path):
+    corners = sf.config_camera(W, H, K).corners()
+    args = [DRIVE, "--initialize-noview", str(W), str(H)] + [float(x).hex() for c in corners for x in c]
+    r = subprocess.run(args + [str(tmp_path / "x.bin"), str(SEED), str(BATCH), "100"], capture_output=True,
+                       text=True, timeout=100)
+    assert r.returncode == 1
+    assert "frame-less loop failed" in r.stderr and "view" in r.stderr.lower(), r.stderr
+
+
+def test_python_initialize_equals_sequential_batches():
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        s.Initialize(SEED, batch=BATCH)
+        t0 = time.time()
+        while time.time() - t0 < 0.3:
+            s.GetGBuffer()
+            time.sleep(0.005)
+        s.Deinitialize()
+        packets = s.GetPacketsTraced()
+        pos, nrm, _, _ = s.download()
+        rays = s.GetRaysPerSecond()
+    assert packets > 0 and packets % BATCH == 0
+    assert rays == 8 * packets
+    check_layout(pos, nrm)
+    p2, n2, _ = sequential_frame(packets)
+    assert np.array_equal(pos.view(np.uint32), p2.view(np.uint32))
+    assert np.array_equal(nrm.view(np.uint32), n2.view(np.uint32))
+
+
+def test_python_initialize_error_surfaces():
+    with sf.Sphereflake(W, H) as s:
+        s.Initialize(SEED, batch=BATCH)   # no view: the first batch fails with SF_ENOVIEW
+        time.sleep(0.1)
+        with pytest.raises(RuntimeError, match="frame-less loop failed"):
+            s.Deinitialize()

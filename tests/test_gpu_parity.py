@@ -483,3 +483,29 @@ def test_progressive_adaptive_levels_fixup(monkeypatch):
     assert np.array_equal(nrm.view(np.uint32), enrm.view(np.uint32))
     assert (st.max_depth, st.closest) == (est.max_depth, est.closest)
     assert st.max_depth >= 8 and st.overflow_tiles == 0 and est.overflow_tiles == 0
+
+
+def test_progressive_full_size_batches_binned_equal_unbinned(monkeypatch):
+    """The bench / Initialize() batch shape: 1920x1080 at the depth-8 camera, batches of 2^18 packets
+    (sf_packet_scan over 32 400 bins, 32 per scan thread, staged through LDS). Binning only changes the
+    trace order: two such batches continuing one stream give the frame, stats and ray count of the
+    same calls traced in draw order (SF_PROG_BIN=0), bit for bit. A scan that lost or duplicated a
+    packet in the permutation would leave pixels of the missing packets unwritten or stale."""
+    W, H, K, B = 1920, 1080, 0.25, 1 << 18
+
+    def run():
+        with sf.Sphereflake(W, H) as s:
+            s.SetCamera(sf.config_camera(W, H, K))
+            s.Progressive(99, B, counter0=0)
+            s.Progressive(99, B)
+            s.Synchronize()
+            pos, nrm, _, _ = s.download()
+            return pos, nrm, s.stats()
+
+    pos, nrm, st = run()
+    monkeypatch.setenv("SF_PROG_BIN", "0")
+    epos, enrm, est = run()
+    assert np.array_equal(pos.view(np.uint32), epos.view(np.uint32))
+    assert np.array_equal(nrm.view(np.uint32), enrm.view(np.uint32))
+    assert (st.max_depth, st.closest, st.rays) == (est.max_depth, est.closest, est.rays)
+    assert st.rays == 2 * 8 * B and (pos[..., 3] == 1.0).sum() > W * H // 2
