@@ -91,25 +91,31 @@ def test_renders_on_alternating_streams_stay_ordered():
     stream 1 and the c2 view on stream 2, alternated without host synchronisation, must leave exactly
     the golden c2 frame (overlapping renders would race on the per-context tile queues and interleave
     A's and c2's pixels), with the frame-less mode and a download joining in between."""
-    import torch
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")   # raw HIP streams (no torch import: it pages in for minutes on a fresh box)
+    hs = [ctypes.c_void_p(), ctypes.c_void_p()]
+    for h in hs:
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
     fx = load_frame("c2")
     W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
     cam_b = sf.config_camera(W, H, K)
     cam_a = sf.config_camera(W, H, K)
     cam_a.SetYaw(np.float32(sf.DEFAULT_YAW + 0.05))
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    s1, s2 = hs[0].value, hs[1].value
     with sf.Sphereflake(W, H) as s:
         for _ in range(6):
             s.SetCamera(cam_a)
-            s.Render(stream=s1.cuda_stream)
+            s.Render(stream=s1)
             s.SetCamera(cam_b)
-            s.Render(stream=s2.cuda_stream)
+            s.Render(stream=s2)
         pos, nrm, _, _ = s.download()
         assert frame_digest(pos, nrm) == fx["frame_digest"]
         # frame-less batches on stream 1 after a render on stream 2, then a full frame on stream 2 again
         s.SetCamera(cam_a)
-        s.Progressive(12345, 1 << 16, 0, stream=s1.cuda_stream)
+        s.Progressive(12345, 1 << 16, 0, stream=s1)
         s.SetCamera(cam_b)
-        s.Render(stream=s2.cuda_stream)
+        s.Render(stream=s2)
         pos, nrm, _, _ = s.download()
         assert frame_digest(pos, nrm) == fx["frame_digest"]
+    for h in hs:
+        hip.hipStreamDestroy(h)
