@@ -15,9 +15,11 @@ previous costs); `fixed_camera` repeats the timed loop on one unchanging view.
 
 Multi-GPU (`--gpus N`, launched by torch.distributed.run): one process per GPU. The frames of a
 camera path are independent units, so each rank renders its own 1920x1080 depth-8 frame per step
-(frame index = step * N + rank); no data-path collective, `scaling: weak`. The row-banded single-frame
-mode with an RCCL gather to rank 0 is `--mode rows` (strong scaling, reported
-with and without the gather).
+(frame index = step * N + rank); no data-path collective, `scaling: weak`. `--mode rows` renders ONE
+frame per step across N devices behind the C ABI (sf_group_*): interleaved 8-row
+bands, strided peer copies into device 0's G-buffer, driven by rank 0 alone (the other ranks only join
+the barriers); `scaling: strong`. `--mode rows-rccl` is the earlier per-rank variant (every rank traces
+its bands, torch RCCL gather + reassembly on rank 0).
 
 rank 0 prints ONE JSON line. `roofline` prices the dominant kernel against HBM (32 B/ray of G-buffer
 stores); `cpu_baseline` times the reference's own AVX packet path (oracle/_ref,
@@ -52,7 +54,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--mode", choices=["frames", "rows"], default="frames")
+    ap.add_argument("--mode", choices=["frames", "rows", "rows-rccl"], default="frames")
     ap.add_argument("--kernel", choices=["wave", "ray"], default="wave")
     ap.add_argument("--width", type=int, default=W)
     ap.add_argument("--height", type=int, default=H)
@@ -307,6 +309,82 @@ def transfer_rates(ctx, torch, dev, stream, width, height, kernel, frames=8):
             "note": "PCIe-inclusive figures; `value` is the HBM-resident render rate"}
 
 
+def run_rows(args, torch, dist, dist_on, rank, n, kernel):
+    """--mode rows: ONE frame per step over N devices from one process (sf_group_*): member k traces the
+    8-row bands b = k (mod N); members k > 0 ship theirs into member 0's G-buffer with strided peer copies.
+    The camera moves as in frames mode (frame i of the path at step i). When fewer than N devices are
+    visible (a one-GPU rehearsal) the members are N contexts on device 0, and the line says so."""
+    width, height, band = args.width, args.height, args.band_rows
+    visible = torch.cuda.device_count()
+    devices = list(range(n)) if visible >= n else [0] * n
+    views = [frame_camera(width, height, args.K, i).corners() for i in range(args.warmup + args.steps)]
+    g = None
+    first_ms = trace_ms = None
+    if rank == 0:
+        g = sf.SphereflakeGroup(devices, width, height)
+        if kernel != sf.SF_KERNEL_WAVE:
+            raise SystemExit("--mode rows traces with the wave kernel")
+        g.SetView(*views[0])
+        t = time.perf_counter()
+        g.Render(band)
+        g.Synchronize()
+        first_ms = (time.perf_counter() - t) * 1e3
+        for i in range(args.warmup):
+            g.SetView(*views[i])
+            g.Render(band)
+        g.member_kernel_timing(0, True, period=KTIMING_PERIOD)
+        g.Synchronize()
+        g.reset_stats()
+    if dist_on:
+        dist.barrier()
+    t0 = time.perf_counter()
+    if rank == 0:
+        for i in range(args.steps):
+            g.SetView(*views[args.warmup + i])
+            g.Render(band)
+        g.Synchronize()
+    dt = time.perf_counter() - t0
+    if dist_on:
+        dist.barrier()
+    if rank != 0:
+        return
+    st = g.stats()
+    if st.overflow_tiles:
+        raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
+    tk = g.member_kernel_timing(0, n=min(-(-args.steps // KTIMING_PERIOD), 64))
+    trace_ms = float(np.mean(tk)) if len(tk) else dt / args.steps * 1e3
+    rays0 = sf.lib().sf_slab_rows(height, band, n, 0) * width   # member 0's rays per launch
+    t_step = dt / args.steps
+    value = width * height / t_step / 1e6
+    achieved = BYTES_PER_RAY * rays0 / (trace_ms * 1e-3) / 1e9
+    gather_bytes = sum(sf.lib().sf_slab_rows(height, band, n, k) for k in range(1, n)) * width * BYTES_PER_RAY
+    same_dev = len(set(devices)) < n
+    g.close()
+    out = {
+        "metric": "Mrays/sec into G-buffer at 1920x1080 depth-8; frame time ms",
+        "value": round(value, 2), "unit": "Mrays/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(t_step * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (deterministic camera path: config camera, yaw swept +-10 mrad at 1 mrad per frame; "
+                "no dataset)",
+        "config": {"workload": f"{width}x{height} primary-ray G-buffer, camera K={args.K:g}, one frame per step "
+                               f"cut into {band}-row bands over {n} members, moving camera",
+                   "width": width, "height": height, "K": args.K, "max_depth": st.max_depth, "camera": "moving",
+                   "devices": devices,
+                   "parallelism": f"row-bands x{n} (sf_group: strided peer copies into device 0)"
+                                  + (" [rehearsal: all members on device 0]" if same_dev else "")},
+        "frame_ms": round(t_step * 1e3, 4),
+        "first_render_ms": round(first_ms, 4),
+        "gather_bytes_per_frame": gather_bytes,
+        "rays_per_step": width * height, "rays_counted": int(st.rays),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": TRACE_KERNEL,
+                     "kernel_ms": round(trace_ms, 4),
+                     "note": "member 0's trace kernel over its bands (32 B/ray x its rays / HIP-event duration)"},
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -339,6 +417,12 @@ def main():
     ctx = sf.Sphereflake(width, height, device=dev.index)
     sh = stream.cuda_stream
 
+    if args.mode == "rows":
+        run_rows(args, torch, dist, dist_on, rank, max(n, args.gpus), kernel)   # N devices, one driving process
+        ctx.close()
+        if dist_on:
+            dist.destroy_process_group()
+        return
     if args.mode == "frames":
         # frame index = step * N + rank along the camera path (warmup, timed loop)
         views = [frame_camera(width, height, args.K, i * n + rank).corners() for i in range(args.warmup + args.steps)]
@@ -389,7 +473,7 @@ def main():
                               band_index=rank, compact=True, kernel=kernel, stream=sh)
             if timed:
                 ev_e[i].record(stream)
-            if args.mode == "rows" and dist_on:
+            if args.mode == "rows-rccl" and dist_on:
                 send_p[:slab_rows].copy_(slab_p)
                 send_n[:slab_rows].copy_(slab_n)
                 if backend == "nccl":
@@ -509,7 +593,7 @@ def main():
                                    + (f", BASELINE {cfg_name}" if cfg_name else "")
                                    + f", {camera} camera, {args.kernel} kernel",
                        "width": width, "height": height, "K": args.K, "max_depth": st.max_depth, "camera": camera,
-                       "parallelism": f"frames x{n}" if args.mode == "frames" else f"row-bands x{n} + RCCL gather"},
+                       "parallelism": f"frames x{n}" if args.mode == "frames" else f"row-bands x{n} + RCCL gather (per rank)"},
             "frame_ms": round(t_step * 1e3, 4),
             "kernel_ms": round(kern_ms_max, 4),
             "first_render_ms": round(first_ms, 4) if first_ms is not None else None,

@@ -241,9 +241,10 @@ int sf_set_tile_trace(sf_ctx* ctx, int enable);
 int sf_get_tile_trace(sf_ctx* ctx, uint64_t* out, size_t n);   /* n >= 3 * tiles; synchronises */
 /* Heavy-first tile schedule: the work units the next persistent render takes in order (computed from
    the last render's per-tile costs, heaviest cost bucket first, stable within a bucket; a unit is
-   tile | half << 30, half 0 = the whole 8x8 tile, 1/2 = its pixel rows 0-3/4-7 -- the tiles of the
-   heaviest bucket are traced as two half units) and those costs (shader cycles, one per tile).
-   Either pointer may be NULL; n >= 2 * tiles (order) or tiles (cost only). Returns the unit count,
+   tile | part << 29: part 0 = the whole 8x8 tile, 1/2 = its pixel rows 0-3/4-7, 3..6 = its 4x4 quarters --
+   the tiles of the heaviest buckets may be traced as 2 or 4 part units, env SF_SPLIT_BUCKETS /
+   SF_SPLIT_PARTS) and those costs (shader cycles, one per tile; a split tile's slowest part, scaled).
+   Either pointer may be NULL; n >= 4 * tiles (order) or tiles (cost only). Returns the unit count,
    0 when no order exists yet, or a negative SF_E*. Synchronises. */
 int sf_get_tile_order(sf_ctx* ctx, uint32_t* order, uint32_t* cost, size_t n);
 
@@ -257,6 +258,34 @@ int sf_set_kernel_timing(sf_ctx* ctx, int enable);
 /* Durations (ms) of the main trace kernel of the last min(n, 64) timed renders, oldest first;
    returns how many were written (>= 0) or a negative SF_E*. Synchronises. */
 int sf_kernel_times(sf_ctx* ctx, float* ms, uint32_t n);
+
+/* --- multi-GPU ------------------------------------------ */
+/* One process, n member devices (the reference's host thread pool, Sphereflake.cpp:67-74, becomes n
+   GPUs). The frame is cut into interleaved bands of band_rows rows, band b traced by member b % n;
+   member 0 holds the final G-buffer (its context's buffers): it writes its bands in place, member
+   k > 0 traces its bands into a compact slab on its device and copies it into member 0's G-buffer with
+   one strided peer copy per buffer over xGMI, queued on its own stream right behind its render (so a
+   member's copies overlap the other members' still-running traces). A device may appear more than once (n contexts on one GPU: the single-GPU test of the
+   path). Stats combine: max depth max, closest min, rays and overflow tiles summed. */
+typedef struct sf_group sf_group;
+int sf_group_create(const int* devices, int n, uint32_t width, uint32_t height, sf_group** out);
+void sf_group_destroy(sf_group* group);
+int sf_group_size(const sf_group* group);
+sf_ctx* sf_group_member(sf_group* group, int k);          /* member k's context (k = 0: the final G-buffer) */
+int sf_group_set_view(sf_group* group, const float origin[3], const float top_left[3],
+                      const float top_right[3], const float bottom_left[3]);
+int sf_group_set_variant(sf_group* group, int variant);
+/* One frame across the members (asynchronous; band_rows a multiple of 8, 0 = 8). Work queued on member
+   0's context afterwards (sf_download, sf_post_process, ...) sees the whole frame. */
+int sf_group_render(sf_group* group, uint32_t band_rows);
+int sf_group_synchronize(sf_group* group);
+int sf_group_download(sf_group* group, float* pos4, float* nrm4);   /* synchronous D2H of the frame */
+int sf_group_get_stats(sf_group* group, sf_stats* out);             /* synchronises */
+int sf_group_reset_stats(sf_group* group);                          /* all three counters, every member */
+int sf_group_last_hip_error(const sf_group* group);
+
+/* The context's own stream (hipStream_t) -- where calls with a NULL stream are queued. */
+void* sf_context_stream(sf_ctx* ctx);
 
 /* --- misc ---------------------------------------------------------------- */
 

@@ -30,6 +30,7 @@ def main():
             s.Render()
         tr = s.tile_trace()
         ph = s.phase_sums.astype(np.float64)
+        ut = s.unit_trace.copy()
     if a.counts:
         names = ["nodes tested", "child iterations", "no-lane-hit iterations", "children entered", "leaf skips"]
         per = a.reps
@@ -51,6 +52,13 @@ def main():
               ", ".join(f"{names[k]} {100 * ph[k] / tot:.1f}%" for k in (1, 6, 2, 3, 4, 5)))
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     np.save(a.out, tr)
+    if ut[:, 1].any():   # SF_FLAG_DIAG_UNITS: per work unit
+        np.save(a.out.replace(".npy", "_units.npy"), ut)
+        m = ut[:, 1] > 0
+        u0 = ut[m, 0].min()
+        du = (ut[m, 1] - ut[m, 0]) / 100.0
+        print(f"units {m.sum()} span {(ut[m, 1].max() - u0) / 100.0:.1f} us; unit us mean {du.mean():.2f} "
+              f"p99 {np.percentile(du, 99):.2f} max {du.max():.2f}")
     t0 = tr[:, 0].min()
     dur = (tr[:, 1] - tr[:, 0]) / 100.0   # us
     span = (tr[:, 1].max() - t0) / 100.0

@@ -24,7 +24,7 @@ extern "C" __global__ void sf_trace_queue1(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2(FrameArgs a);
 extern "C" __global__ void sf_trace_queue4(FrameArgs a);
 extern "C" __global__ void sf_order_scan(const uint32_t* chunk_cnt, uint32_t nc, uint32_t n_tiles,
-                                         uint32_t split_buckets, uint32_t spare, uint32_t* chunk_off,
+                                         uint32_t split_buckets, uint32_t parts, uint32_t spare, uint32_t* chunk_off,
                                          uint32_t* order_meta);
 extern "C" __global__ void sf_order_scatter(const uint32_t* cost, uint32_t n, uint32_t* chunk_cnt,
                                             const uint32_t* chunk_off, const uint32_t* order_meta, uint32_t* order);
@@ -158,8 +158,11 @@ struct sf_ctx {
     uint32_t* tile_order = nullptr;
     uint32_t* chunk_cnt = nullptr;     // per 64-tile chunk x SF_ORDER_BUCKETS (zeroed by sf_order_scatter)
     uint32_t* chunk_off = nullptr;
-    uint32_t* order_meta = nullptr;    // [0] work units in tile_order, [1] first split bucket
+    uint32_t* order_meta = nullptr;    // [0] work units in tile_order, [1] first split bucket, [2] parts per split tile
     uint32_t split_buckets = SF_SPLIT_AUTO;   // env SF_SPLIT_BUCKETS = k: top k buckets (0: never split)
+    uint32_t split_parts = 2;          // env SF_SPLIT_PARTS = 2 (halves) | 4 (quarters)
+    uint32_t* part_cost = nullptr;     // per tile: slowest part of a split tile (zeroed, reset by the last part)
+    uint32_t* part_done = nullptr;     // per tile: parts finished (zeroed, reset by the last part)
     uint32_t order_n = 0;              // tile count the current tile_order is a permutation of (0: none)
     // Stream ordering across calls: every call that enqueues work on the context's buffers first joins
     // the stream of the previous such call (ctx_join), so renders, frame-less batches, post-processing
@@ -251,6 +254,8 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->chunk_cnt);
     (void)hipFree(c->chunk_off);
     (void)hipFree(c->order_meta);
+    (void)hipFree(c->part_cost);
+    (void)hipFree(c->part_done);
     (void)hipFree(c->noise);
     (void)hipFree(c->ao);
     (void)hipFree(c->blur_h);
@@ -346,6 +351,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if (const char* ev = std::getenv("SF_PROG_PREFETCH")) c->prog_prefetch = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_ADAPT")) c->prog_adapt = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_SPLIT_BUCKETS")) c->split_buckets = (uint32_t)std::atoi(ev);
+    if (const char* ev = std::getenv("SF_SPLIT_PARTS")) c->split_parts = std::atoi(ev) == 4 ? 4u : 2u;
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_FLAGS")) c->flags = (uint32_t)std::strtoul(ev, nullptr, 0);
     if (const char* ev = std::getenv("SF_TRACE_WAVES")) {
@@ -374,8 +380,12 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if ((e = hipMalloc(&c->ovf_counters, SF_COUNTER_WORDS * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->ovf_list, ntiles * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->tile_cost, ntiles * 4)) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&c->tile_order, 2 * ntiles * 4)) != hipSuccess) return fail(e);   // <= 2 units per tile
-    if ((e = hipMalloc(&c->order_meta, 2 * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->tile_order, 4 * ntiles * 4)) != hipSuccess) return fail(e);   // <= 4 units per tile
+    if ((e = hipMalloc(&c->order_meta, 4 * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->part_cost, ntiles * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->part_done, ntiles * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMemsetAsync(c->part_cost, 0, ntiles * 4, c->stream)) != hipSuccess) return fail(e);
+    if ((e = hipMemsetAsync(c->part_done, 0, ntiles * 4, c->stream)) != hipSuccess) return fail(e);
     const size_t nchunks = (ntiles + 63) / 64;
     if ((e = hipMalloc(&c->chunk_cnt, nchunks * SF_ORDER_BUCKETS * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->chunk_off, nchunks * SF_ORDER_BUCKETS * 4)) != hipSuccess) return fail(e);
@@ -564,8 +574,8 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 c->occ_key = key;
             }
             uint32_t nblk = (uint32_t)c->occ_blocks * (uint32_t)c->cus;
-            // work units: tiles, or up to 2 per tile when the schedule may split tiles into halves
-            const uint32_t units_max = (c->use_order && c->split_buckets != 0u) ? 2u * ntiles : ntiles;
+            // work units: tiles, or up to `split_parts` per tile when the schedule may split tiles
+            const uint32_t units_max = (c->use_order && c->split_buckets != 0u) ? c->split_parts * ntiles : ntiles;
             const uint32_t need = (units_max + wpb - 1) / wpb;
             if (nblk > need) nblk = need;
             if (c->max_blocks && nblk > c->max_blocks) nblk = c->max_blocks;
@@ -573,6 +583,8 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             if (c->use_order) {
                 a.tile_cost = c->tile_cost;
                 a.chunk_cnt = c->chunk_cnt;
+                a.part_cost = c->part_cost;
+                a.part_done = c->part_done;
                 a.tile_order = c->order_n == ntiles ? c->tile_order : nullptr;   // ordered by ctx_join
                 a.order_meta = c->order_meta;
             }
@@ -593,7 +605,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 const uint32_t waves = nblk * wpb;   // resident waves of the persistent grid
                 const uint32_t spare = waves > ntiles ? waves - ntiles : 0u;
                 hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->chunk_cnt, nc, ntiles,
-                                   c->split_buckets, spare, c->chunk_off, c->order_meta);
+                                   c->split_buckets, c->split_parts, spare, c->chunk_off, c->order_meta);
                 SF_HIP(c, hipGetLastError());
                 hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost, ntiles,
                                    c->chunk_cnt, (const uint32_t*)c->chunk_off, (const uint32_t*)c->order_meta,
@@ -999,8 +1011,9 @@ int sf_set_tile_trace(sf_ctx* c, int enable)
     }
     if (!c->tile_trace) {
         const size_t ntiles = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8);
-        SF_HIP(c, hipMalloc(&c->tile_trace, (ntiles * 3 + SF_DIAG_SLOTS) * 8));
-        SF_HIP(c, hipMemset(c->tile_trace, 0, (ntiles * 3 + SF_DIAG_SLOTS) * 8));
+        // per tile {start, end, id}, the diagnostic slots, per work unit {start, end, unit} (<= 4 per tile)
+        SF_HIP(c, hipMalloc(&c->tile_trace, (ntiles * 15 + SF_DIAG_SLOTS) * 8));
+        SF_HIP(c, hipMemset(c->tile_trace, 0, (ntiles * 15 + SF_DIAG_SLOTS) * 8));
     }
     return SF_OK;
 }
@@ -1014,7 +1027,8 @@ int sf_get_tile_trace(sf_ctx* c, uint64_t* out, size_t n)
     if (int rc_ = ctx_drain(c)) return rc_;
     // n >= 3 * tiles + SF_DIAG_SLOTS also returns the segment sums / event counts of the diagnostic
     // builds (zeros otherwise)
-    SF_HIP(c, hipMemcpy(out, c->tile_trace, (n >= ntiles * 3 + SF_DIAG_SLOTS ? ntiles * 3 + SF_DIAG_SLOTS : ntiles * 3) * 8,
+    const size_t full = ntiles * 15 + SF_DIAG_SLOTS;
+    SF_HIP(c, hipMemcpy(out, c->tile_trace, (n >= full ? full : n >= ntiles * 3 + SF_DIAG_SLOTS ? ntiles * 3 + SF_DIAG_SLOTS : ntiles * 3) * 8,
                         hipMemcpyDeviceToHost));
     return SF_OK;
 }
@@ -1034,6 +1048,8 @@ int sf_get_tile_order(sf_ctx* c, uint32_t* order, uint32_t* cost, size_t n)
     if (cost) SF_HIP(c, hipMemcpy(cost, c->tile_cost, ntiles * 4, hipMemcpyDeviceToHost));
     return (int)meta[0];
 }
+
+void* sf_context_stream(sf_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int sf_device_buffers(sf_ctx* c, float** pos4, float** nrm4, float** min_t, uint32_t** hidx)
 {

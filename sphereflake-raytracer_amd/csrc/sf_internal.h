@@ -48,6 +48,10 @@
 // with SF_FLAG_DIAG_HALF_SEL rows 4-7. Other pixels are not written. Never set by the product path.
 #define SF_FLAG_DIAG_HALF 4u
 #define SF_FLAG_DIAG_HALF_SEL 8u
+// diagnostics (schedule studies): with the tile trace on, also record every work unit of the persistent
+// kernel by its order position g: {start, end, unit} (s_memrealtime) after the tile trace and the
+// diagnostic slots (room for 2 units per tile)
+#define SF_FLAG_DIAG_UNITS 0x20u
 
 struct DepthTables {
     float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)
@@ -103,6 +107,8 @@ struct FrameArgs {
     const uint32_t* tile_order;       // in (NULL = row-major): work units (SF_UNIT_*), heaviest first
     const uint32_t* order_meta;       // with tile_order: [0] units in it, [1] first split bucket
     uint32_t* chunk_cnt;              // out (with tile_cost): per 64-tile chunk, cost-bucket histogram
+    uint32_t* part_cost;              // per tile: max cycles over the parts of a split tile (reset by the last part)
+    uint32_t* part_done;              // per tile: parts of a split tile finished (reset by the last part)
     uint32_t packet_lanes;            // frame-less mode: 8 (AVX variant) or 4 (SSE variant, 2x2 footprint)
 };
 
@@ -136,17 +142,23 @@ struct PostArgs {
 #define SF_PROG_BIN_MIN 65536u         // frame-less batches below this many packets trace in draw order
                                        // (binning pays once the batch is several waves per slot)
 #define SF_ORDER_BUCKETS 32u           // log-spaced cost buckets of sf_tile_order (2 per octave from 2^8 cycles)
-// A work unit of the tile order: tile index | half << SF_UNIT_HALF_SHIFT. Half 0 = the whole 8x8 tile;
-// 1, 2 = its pixel rows 0-3 / 4-7 (the heaviest tiles are traced as two half units by two waves:
-// a tile's serial DFS otherwise bounds the frame).
-#define SF_UNIT_HALF_SHIFT 30u
-#define SF_UNIT_TILE_MASK ((1u << SF_UNIT_HALF_SHIFT) - 1u)
+// A work unit of the tile order: tile index | part << SF_UNIT_PART_SHIFT. Part 0 = the whole 8x8 tile;
+// 1, 2 = its pixel rows 0-3 / 4-7 (halves); 3..6 = its 4x4 quarters (q = part - 3: rows 4 (q >> 1).., columns
+// 4 (q & 1)..). The heaviest tiles are traced as 2 or 4 part units by as many waves: a tile's serial DFS
+// otherwise bounds the frame.
+#define SF_UNIT_PART_SHIFT 29u
+#define SF_UNIT_TILE_MASK ((1u << SF_UNIT_PART_SHIFT) - 1u)
+#define SF_PART_HALF0 1u
+#define SF_PART_QUARTER0 3u
 // Which tiles are split: env SF_SPLIT_BUCKETS = k splits the top k occupied cost buckets (at most an
 // eighth of the tiles). The default (SF_SPLIT_AUTO) splits only into idle wave slots: whole buckets,
 // heaviest first, while tiles + split tiles <= the persistent grid's waves. With more tiles than waves
 // (1920x1080: 32400 tiles, 7168 waves) nothing is split -- measured: splitting there costs +1.5-3.5 %;
 // at 640x360 (3600 tiles) it takes the frame from 0.198 to 0.144 ms.
 #define SF_SPLIT_AUTO 0xffffffffu
+// Parts a split tile is traced as (env SF_SPLIT_PARTS): 2 halves or 4 quarters. A split tile's cost for
+// the next schedule is its slowest part's, scaled to whole-tile terms (measured: the slowest half takes
+// ~0.68 of the whole tile, the slowest quarter ~0.5).
 
 namespace sfhost {
 void child_transforms(float child[9][16]);

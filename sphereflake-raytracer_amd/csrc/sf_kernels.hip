@@ -427,6 +427,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     // "child expands" vector; *pend = the wave's mask of children some lane expands.
     // (node: its 4 float4 at node, node + ps, node + 2 ps, node + 3 ps: ps = 4 for the root image,
     // SF_LDS_PLANE for a level table)
+    // (the node's own sphere is tested by the caller when the node is entered, before this)
     auto expand = [&](const float* node, uint32_t ps, uint32_t d, bool act, uint32_t& pend) -> uint32_t {
         d = __builtin_amdgcn_readfirstlane(d);   // wave-uniform: depth constants come by scalar loads
         lds_fence();
@@ -434,20 +435,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         const float4 p0 = *reinterpret_cast<const float4*>(node + ps);
         const float4 p1 = *reinterpret_cast<const float4*>(node + 2u * ps);
         const float4 p2 = *reinterpret_cast<const float4*>(node + 3u * ps);
-        const float4 dtn = depth_consts(K, d);        // this node: r^2, (4/3) r
+        const float4 dtn = depth_consts(K, d);        // this node: (4/3) r
         const float4 dtc = depth_consts(K, d + 1u);   // children: (2r)^2, T
-        self_test(pc, d, act, idxN, dtn.y);
-        // No child of this node can pass the LOD test for any ray (sfhost::leaf_threshold): skip the
-        // build and the child tests (per-ray semantics only, like the reachability cull below).
-        // (pushed nodes never qualify: leaf children are tested inline by the DFS loop; only the root)
-        if (lod_cull && d == 0u) {
-            const float leaf = depth_leaf(K, d);
-            if (__builtin_amdgcn_readfirstlane((int)(pc.w > leaf))) {
-                SF_COUNT(4, 1);
-                pend = 0u;
-                return 0u;
-            }
-        }
         // world = parent * child (SIMD_AVX.h:59-81), child translation scaled by (4/3) r (Sphereflake.h:162-172):
         // column 3 lanes multiply b0..b2 by s, the others by 1 (exact)
         const float sm = bc == 3u ? dtn.z : 1.0f;
@@ -499,6 +488,13 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 const float d2 = cc - tca * tca;
                 const bool f0 = tca >= 0.0f, f1 = d2 <= R2b;
                 const uint64_t hbm = actm & wave_ballot(f0) & wave_ballot(f1);   // bounding (SIMD_AVX.h:247-258)
+#ifdef SF_EXP_PAD   // experiment builds only: independent VALU filler per child iteration (issue-bound test)
+                {
+                    float pad = dx;
+#pragma unroll
+                    for (int k_ = 0; k_ < SF_EXP_PAD; ++k_) __asm__ volatile("v_mov_b32 %0, %0" : "+v"(pad));
+                }
+#endif
                 SF_COUNT(5, __builtin_popcountll(actm));
                 SF_COUNT(6, __builtin_popcountll(hbm));
                 SF_COUNT(10, d >= 4u ? 1 : 0);
@@ -570,8 +566,16 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     // DFS stack in VGPR lanes (lane L = level L): {pending children | cursor << 16}, heap index.
     // Lane selects: no LDS traffic and no lane-0-only region in the loop.
     uint32_t stk_pc = 0u, stk_ix = 0u;
-    uint32_t pend;
-    uint32_t eN = expand(L.root(), 4u, 0u, ex0, pend);
+    uint32_t pend = 0u, eN = 0u;
+    {
+        // the root: its own sphere, then -- unless no child of it can pass LOD for any ray
+        // (sfhost::leaf_threshold; per-ray semantics only) -- its children
+        lds_fence();
+        const float4 pc = *reinterpret_cast<const float4*>(L.root());
+        self_test(pc, 0u, ex0, 0u, depth_consts(K, 0u).y);
+        if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u))))) eN = expand(L.root(), 4u, 0u, ex0, pend);
+        else SF_COUNT(4, 1);
+    }
 
     for (;;) {
         d = __builtin_amdgcn_readfirstlane(d);
@@ -586,20 +590,19 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             }
             const bool a = ((eN >> c) & 1u) != 0u;
             const float* node = L.table(d) + c * 4u;
-            if (lod_cull) {
-                // A child none of whose children can pass LOD for any ray (sfhost::leaf_threshold) only
-                // needs its own sphere: test it here, in its DFS turn, without a push or a level.
-                lds_fence();
-                const float4 pc = *reinterpret_cast<const float4*>(node);
-                if (__builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, d + 1u)))) {
-                    SF_COUNT(4, 1);
-                    SF_COUNT(8, 1);
-                    SF_COUNT(9, __builtin_popcountll(wave_ballot(a)));
-                    maxd = (int32_t)d + 1 > maxd ? (int32_t)d + 1 : maxd;   // Sphereflake.h:157-160
-                    self_test(pc, d + 1u, a, 9u * idxN + 1u + c, depth_consts(K, d + 1u).y);
-                    anc = anc & (h.depth != (int32_t)d + 1);   // the child is finished
-                    continue;
-                }
+            // enter child c: its own sphere first (pre-order, see self_test), in one place for every child
+            lds_fence();
+            const float4 pc = *reinterpret_cast<const float4*>(node);
+            maxd = (int32_t)d + 1 > maxd ? (int32_t)d + 1 : maxd;   // Sphereflake.h:157-160
+            self_test(pc, d + 1u, a, 9u * idxN + 1u + c, depth_consts(K, d + 1u).y);
+            // A child none of whose children can pass LOD for any ray (sfhost::leaf_threshold) only needs its
+            // own sphere: no push, no level, no child build.
+            if (lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, d + 1u)))) {
+                SF_COUNT(4, 1);
+                SF_COUNT(8, 1);
+                SF_COUNT(9, __builtin_popcountll(wave_ballot(a)));
+                anc = anc & (h.depth != (int32_t)d + 1);   // the child is finished
+                continue;
             }
             // save the open node's state, enter child c
             stk_pc = writelane_u(pend | (cN << 16), d, stk_pc);
@@ -608,7 +611,6 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             idxN = 9u * idxN + 1u + c;
             cN = c;
             d += 1u;
-            maxd = (int32_t)d > maxd ? (int32_t)d : maxd;            // Sphereflake.h:157-160
             SF_STAMP(1);
             eN = expand(node, SF_LDS_PLANE, d, a, pend);
             SF_STAMP(2);
@@ -650,7 +652,7 @@ struct Tile {
 };
 
 // Tile of a wave: owned tile row k (band sharding) -> frame tile row.
-__device__ __forceinline__ Tile tile_of(const FrameArgs& a, uint32_t tile, uint32_t lane, uint32_t half = 0u)
+__device__ __forceinline__ Tile tile_of(const FrameArgs& a, uint32_t tile, uint32_t lane, uint32_t part = 0u)
 {
     const uint32_t tx = tile % a.tiles_x, k = tile / a.tiles_x;
     const uint32_t band = a.band_index + (k / a.tiles_per_band) * a.band_count;
@@ -662,8 +664,11 @@ __device__ __forceinline__ Tile tile_of(const FrameArgs& a, uint32_t tile, uint3
     Tile t;
     t.x = tx * SF_TILE + (l & 7u);
     t.y = ty * SF_TILE + (l >> 3);
-    // half unit: only the lanes of pixel rows 0-3 (half 1) or 4-7 (half 2) take part
-    t.valid = t.x < a.W && t.y < a.H && (half == 0u || (l >> 5) + 1u == half);
+    // part unit: only the lanes of pixel rows 0-3 / 4-7 (halves) or of one 4x4 block (quarters) take part
+    const uint32_t q = part - SF_PART_QUARTER0;
+    const bool in = part == 0u || (part < SF_PART_QUARTER0 ? (l >> 5) + SF_PART_HALF0 == part
+                                                           : ((l >> 5) == (q >> 1) && ((l >> 2) & 1u) == (q & 1u)));
+    t.valid = t.x < a.W && t.y < a.H && in;
     t.orow = a.compact ? (k * SF_TILE + (l >> 3)) : t.y;
     return t;
 }
@@ -728,6 +733,22 @@ __device__ __forceinline__ void wave_atomic_inc_nowait(uint32_t* p)
         : "memory");
 }
 
+// One lane's global atomic max on behalf of the wave, completed before it returns (EXEC forced to lane 0).
+__device__ __forceinline__ void wave_atomic_max(uint32_t* p, uint32_t v)
+{
+    uint64_t saved;
+    const uint32_t zero = 0u;
+    __asm__ volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "global_atomic_umax %1, %2, %3\n\t"
+        "s_waitcnt vmcnt(0)\n\t"
+        "s_mov_b64 exec, %0\n\t"
+        : "=&s"(saved)
+        : "v"(zero), "v"(v), "s"(p)
+        : "memory");
+}
+
 __device__ __forceinline__ uint32_t cost_bucket(uint32_t c)
 {
     const uint32_t k = __float_as_uint((float)(c | 1u)) >> 22;   // exponent and 1 mantissa bit
@@ -735,15 +756,25 @@ __device__ __forceinline__ uint32_t cost_bucket(uint32_t c)
     return b < SF_ORDER_BUCKETS ? b : (k < (135u << 1) ? 0u : SF_ORDER_BUCKETS - 1u);
 }
 
+// The ray-cone axis lane of a unit: the centre pixel of what it traces -- (4, 4) for a whole tile,
+// (4, 2) / (4, 6) for the halves, (2 + 4 (q & 1), 2 + 4 (q >> 1)) for quarter q.
+__device__ __forceinline__ uint32_t part_axis_lane(uint32_t part)
+{
+    if (part == 0u) return 36u;
+    if (part < SF_PART_QUARTER0) return part == SF_PART_HALF0 ? 20u : 52u;
+    const uint32_t q = part - SF_PART_QUARTER0;
+    return (2u + 4u * (q >> 1)) * 8u + 2u + 4u * (q & 1u);
+}
+
 template <bool FIXUP>
 __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __restrict__ L, uint32_t tile,
                                                 uint32_t levels, uint32_t* overflow_list, uint32_t* overflow_count,
-                                                uint32_t half = 0u)
+                                                uint32_t part = 0u)
 {
     const DeviceConsts* __restrict__ K = a.consts;
     const uint32_t lane = threadIdx.x & 63u;
-    if (a.flags & SF_FLAG_DIAG_HALF) half = (a.flags & SF_FLAG_DIAG_HALF_SEL) ? 2u : 1u;
-    const Tile t = tile_of(a, tile, lane, half);
+    if (a.flags & SF_FLAG_DIAG_HALF) part = (a.flags & SF_FLAG_DIAG_HALF_SEL) ? 2u : 1u;
+    const Tile t = tile_of(a, tile, lane, part);
     const uint64_t t_start = a.tile_trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint64_t c_start = (!FIXUP && a.tile_cost) ? __builtin_amdgcn_s_memtime() : 0ull;
     float dx, dy, dz;
@@ -754,7 +785,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     bool overflowed = false;
     uint64_t tile_counts = 0;
     traverse<0>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed, a.flags,
-                    FIXUP ? nullptr : a.phase_sums, half == 0u ? 36u : half == 1u ? 20u : 52u, &tile_counts);
+                    FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
     if (!FIXUP && a.tile_trace) {
         // diagnostics only: never read by the kernel, never feeds an output value. Every lane stores
         // the same (uniform) words: no lane-0-only region.
@@ -772,14 +803,30 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
 #endif
     }
 
-    if (!FIXUP && a.tile_cost && half <= 1u) {
+    if (!FIXUP && a.tile_cost && !(a.flags & SF_FLAG_DIAG_HALF)) {
         // scheduling hint for the next render (sf_order_scan / sf_order_scatter); uniform values.
-        // A split tile is counted once, by its first half, at twice that half's cost.
-        const uint64_t cyc = (__builtin_amdgcn_s_memtime() - c_start) << (half ? 1u : 0u);
-        const uint32_t cost = cyc > 0xffffffffull ? 0xffffffffu : (uint32_t)cyc;
-        a.tile_cost[tile] = cost;
-        const uint32_t slot = __builtin_amdgcn_readfirstlane((tile >> 6) * SF_ORDER_BUCKETS + cost_bucket(cost));
-        wave_atomic_inc_nowait(a.chunk_cnt + slot);
+        const uint64_t cyc = __builtin_amdgcn_s_memtime() - c_start;
+        uint32_t cost = cyc > 0xffffffffull ? 0xffffffffu : (uint32_t)cyc;
+        bool last = true;
+        if (part != 0u) {
+            // a split tile: the slowest of its parts, in whole-tile terms (x 3/2 for halves, x 2 for
+            // quarters), recorded by the part that finishes last
+            const uint32_t scaled = part < SF_PART_QUARTER0 ? cost + (cost >> 1) : (cost > 0x7fffffffu ? 0xffffffffu : 2u * cost);
+            const uint32_t nparts = part < SF_PART_QUARTER0 ? 2u : 4u;
+            wave_atomic_max(a.part_cost + tile, scaled);
+            last = wave_fetch_add(a.part_done + tile, 1u) == nparts - 1u;
+            if (last) {
+                cost = __builtin_amdgcn_readfirstlane(
+                    (int)__hip_atomic_load(a.part_cost + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                a.part_cost[tile] = 0u;   // for the next render (uniform values and addresses)
+                a.part_done[tile] = 0u;
+            }
+        }
+        if (last) {
+            a.tile_cost[tile] = cost;
+            const uint32_t slot = __builtin_amdgcn_readfirstlane((tile >> 6) * SF_ORDER_BUCKETS + cost_bucket(cost));
+            wave_atomic_inc_nowait(a.chunk_cnt + slot);
+        }
     }
     if (!FIXUP && overflowed) {
         // a deeper re-trace (sf_fixup_wave) rewrites this whole tile
@@ -899,7 +946,7 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
             k = (k + 1u) & (SF_QUEUES - 1u);
             continue;
         }
-        uint32_t t = g, half = 0u;
+        uint32_t t = g, part = 0u;
         if (at.tile_order) {      // heaviest tiles of the previous render first (scalar load)
 #if defined(__HIP_DEVICE_COMPILE__)
             typedef const __attribute__((address_space(4))) uint32_t* ConstU32;
@@ -908,9 +955,16 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
             const uint32_t u = at.tile_order[g];
 #endif
             t = u & SF_UNIT_TILE_MASK;
-            half = u >> SF_UNIT_HALF_SHIFT;
+            part = u >> SF_UNIT_PART_SHIFT;
         }
-        const TileStats st = trace_tile<false>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity, half);
+        const uint64_t u_start = (at.flags & SF_FLAG_DIAG_UNITS) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        const TileStats st = trace_tile<false>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity, part);
+        if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace) {   // diagnostics only (uniform words)
+            uint64_t* ut = at.tile_trace + 3u * (at.tiles_x * at.tile_rows) + SF_DIAG_SLOTS + 3u * g;
+            ut[0] = u_start;
+            ut[1] = __builtin_amdgcn_s_memrealtime();
+            ut[2] = t | (part << SF_UNIT_PART_SHIFT);
+        }
         maxd = st.maxd > maxd ? st.maxd : maxd;
         closest = fminf(closest, st.closest);
     }
@@ -940,7 +994,8 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 #define SF_SCAN_BATCH 16   // chunk counts a scan thread loads at once (independent loads, one wait)
 
 extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t* __restrict__ chunk_cnt, uint32_t nc,
-                                                                   uint32_t n_tiles, uint32_t split_buckets, uint32_t spare,
+                                                                   uint32_t n_tiles, uint32_t split_buckets, uint32_t parts,
+                                                                   uint32_t spare,
                                                                    uint32_t* __restrict__ chunk_off,
                                                                    uint32_t* __restrict__ order_meta)
 {
@@ -971,14 +1026,14 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t*
     __syncthreads();
     __shared__ uint32_t split_from;
     if (tid == 0) {
-        // Split tiles into two half units each, heaviest buckets first (bucket 0 never): automatically
-        // as many whole buckets as fit into `spare` idle wave slots, or the top `split_buckets` occupied
+        // Split tiles into `parts` units each, heaviest buckets first (bucket 0 never): automatically as
+        // many whole buckets as fit into `spare` idle wave slots, or the top `split_buckets` occupied
         // buckets (at most an eighth of the tiles). Then bucket totals (in units) -> exclusive offsets,
         // heaviest first.
         int bs = (int)SF_ORDER_BUCKETS;
         uint32_t nsplit = 0u;
         if (split_buckets == SF_SPLIT_AUTO) {
-            for (int bb = (int)SF_ORDER_BUCKETS - 1; bb >= 1 && nsplit + tot[bb] <= spare; --bb) {
+            for (int bb = (int)SF_ORDER_BUCKETS - 1; bb >= 1 && (nsplit + tot[bb]) * (parts - 1u) <= spare; --bb) {
                 nsplit += tot[bb];
                 bs = bb;
             }
@@ -993,15 +1048,16 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t*
         split_from = (uint32_t)bs;
         uint32_t acc = 0u;
         for (int bb = (int)SF_ORDER_BUCKETS - 1; bb >= 0; --bb) {
-            const uint32_t x = tot[bb] * (bb >= bs ? 2u : 1u);
+            const uint32_t x = tot[bb] * (bb >= bs ? parts : 1u);
             tot[bb] = acc;
             acc += x;
         }
         order_meta[0] = acc;            // units of the next render
         order_meta[1] = (uint32_t)bs;   // first split bucket
+        order_meta[2] = parts;          // units per split tile
     }
     __syncthreads();
-    const uint32_t mult = b >= split_from ? 2u : 1u;
+    const uint32_t mult = b >= split_from ? parts : 1u;
     uint32_t off = tot[b] + part[k][b] * mult;
     for (uint32_t cb = c0; cb < c1; cb += SF_SCAN_BATCH) {
         uint32_t v[SF_SCAN_BATCH];
@@ -1022,7 +1078,8 @@ extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t
                                                                     uint32_t* __restrict__ order)
 {
     const uint32_t c = blockIdx.x, lane = threadIdx.x, i = c * 64u + lane;
-    const uint32_t split_from = order_meta[1];
+    const uint32_t split_from = order_meta[1], parts = order_meta[2];
+    const uint32_t first = parts == 4u ? SF_PART_QUARTER0 : SF_PART_HALF0;
     const uint32_t bk = i < n ? cost_bucket(cost[i]) : SF_ORDER_BUCKETS;   // sentinel: no tile
     const uint32_t offs = chunk_off[c * SF_ORDER_BUCKETS + (lane & (SF_ORDER_BUCKETS - 1u))];   // lane b: bucket b
     uint64_t pending = __builtin_amdgcn_ballot_w64(bk < SF_ORDER_BUCKETS);
@@ -1032,9 +1089,8 @@ extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t
         const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)offs, (int)b);
         if (bk == b) {
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (b >= split_from) {   // two half units, adjacent
-                order[off + 2u * rank] = i | (1u << SF_UNIT_HALF_SHIFT);
-                order[off + 2u * rank + 1u] = i | (2u << SF_UNIT_HALF_SHIFT);
+            if (b >= split_from) {   // `parts` part units, adjacent
+                for (uint32_t p = 0; p < parts; ++p) order[off + parts * rank + p] = i | ((first + p) << SF_UNIT_PART_SHIFT);
             } else {
                 order[off + rank] = i;
             }

@@ -121,6 +121,20 @@ SIGNATURES = {
     "sf_last_hip_error": (ctypes.c_int, [_CTX]),
     "sf_abi_version": (ctypes.c_int, []),
     "sf_device_count": (ctypes.c_int, []),
+    "sf_context_stream": (ctypes.c_void_p, [_CTX]),
+    "sf_group_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                                       ctypes.POINTER(ctypes.c_void_p)]),
+    "sf_group_destroy": (None, [ctypes.c_void_p]),
+    "sf_group_size": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_group_member": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int]),
+    "sf_group_set_view": (ctypes.c_int, [ctypes.c_void_p, _F, _F, _F, _F]),
+    "sf_group_set_variant": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "sf_group_render": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    "sf_group_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_group_download": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "sf_group_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(sf_stats)]),
+    "sf_group_last_hip_error": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_group_reset_stats": (ctypes.c_int, [ctypes.c_void_p]),
 }
 
 _lib = None
@@ -470,21 +484,22 @@ class Sphereflake:
             _check(lib().sf_set_tile_trace(self._ctx, int(bool(enable))), "sf_set_tile_trace", self._ctx)
             return None
         n = ((self.width + 7) // 8) * ((self.height + 7) // 8)
-        out = np.zeros(3 * n + 16, np.uint64)   # + SF_DIAG_SLOTS
+        out = np.zeros(15 * n + 16, np.uint64)   # tiles, SF_DIAG_SLOTS, units (SF_FLAG_DIAG_UNITS)
         _check(lib().sf_get_tile_trace(self._ctx, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), out.size),
                "sf_get_tile_trace", self._ctx)
-        self.phase_sums = out[3 * n:]          # segment cycle sums of stamp builds (zeros otherwise)
+        self.phase_sums = out[3 * n:3 * n + 16]   # segment cycle sums / event counts of diagnostic builds
+        self.unit_trace = out[3 * n + 16:].reshape(4 * n, 3)   # per order position (SF_FLAG_DIAG_UNITS)
         return out[:3 * n].reshape(n, 3)
 
     def tile_order(self):
-        """Heavy-first schedule: (units, cost) uint32 arrays -- the work units (tile | half << 30) the
+        """Heavy-first schedule: (units, cost) uint32 arrays -- the work units (tile | part << 29) the
         next persistent render takes in order, and the last render's per-tile shader cycles they were
         computed from -- or None before any ordered render."""
         n = ((self.width + 7) // 8) * ((self.height + 7) // 8)
-        order = np.zeros(2 * n, np.uint32)
+        order = np.zeros(4 * n, np.uint32)
         cost = np.zeros(n, np.uint32)
         P = ctypes.POINTER(ctypes.c_uint32)
-        k = lib().sf_get_tile_order(self._ctx, order.ctypes.data_as(P), cost.ctypes.data_as(P), 2 * n)
+        k = lib().sf_get_tile_order(self._ctx, order.ctypes.data_as(P), cost.ctypes.data_as(P), 4 * n)
         if k < 0:
             _check(k, "sf_get_tile_order", self._ctx)
         return (order[:k], cost) if k else None
@@ -581,3 +596,94 @@ class Sphereflake:
         e, self._worker_error = getattr(self, "_worker_error", None), None
         if e is not None:
             raise RuntimeError(f"frame-less loop failed: {e}") from e
+
+
+class SphereflakeGroup:
+    """Single-process multi-GPU renderer (sf_group_*): interleaved 8-row bands traced on
+    the member devices, gathered by strided peer copies into member 0's G-buffer. `devices` may repeat a
+    device (n contexts on one GPU)."""
+
+    def __init__(self, devices, width: int, height: int):
+        self.width, self.height = int(width), int(height)
+        devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+        h = ctypes.c_void_p()
+        _check(lib().sf_group_create(devs, len(devices), self.width, self.height, ctypes.byref(h)), "sf_group_create")
+        self._g = h
+
+    def close(self):
+        if getattr(self, "_g", None):
+            lib().sf_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc != SF_OK:
+            err = SphereflakeError(rc, what)
+            if rc == SF_EHIP:
+                err.hip_error = lib().sf_group_last_hip_error(self._g)
+            raise err
+
+    def size(self) -> int:
+        return lib().sf_group_size(self._g)
+
+    def member(self, k: int):
+        """Member k's context handle (k = 0 holds the final G-buffer)."""
+        return lib().sf_group_member(self._g, k)
+
+    def SetView(self, origin, topLeft, topRight, bottomLeft):
+        o, tl, tr, bl = (_f32(v, 3) for v in (origin, topLeft, topRight, bottomLeft))
+        self._check(lib().sf_group_set_view(self._g, _fp(o), _fp(tl), _fp(tr), _fp(bl)), "sf_group_set_view")
+
+    def SetCamera(self, cam: Camera):
+        self.SetView(*cam.corners())
+
+    def SetVariant(self, variant):
+        v = {"avx": SF_VARIANT_AVX, "sse": SF_VARIANT_SSE}.get(variant, variant)
+        self._check(lib().sf_group_set_variant(self._g, int(v)), "sf_group_set_variant")
+
+    def Render(self, band_rows: int = 8):
+        self._check(lib().sf_group_render(self._g, int(band_rows)), "sf_group_render")
+
+    def Synchronize(self):
+        self._check(lib().sf_group_synchronize(self._g), "sf_group_synchronize")
+
+    def download(self):
+        H, W = self.height, self.width
+        pos = np.empty((H, W, 4), np.float32)
+        nrm = np.empty((H, W, 4), np.float32)
+        self._check(lib().sf_group_download(self._g, pos.ctypes.data_as(ctypes.c_void_p),
+                                            nrm.ctypes.data_as(ctypes.c_void_p)), "sf_group_download")
+        return pos, nrm
+
+    def member_kernel_timing(self, k: int, enable: bool | None = None, n: int = 64, period: int = 1):
+        """Sphereflake.kernel_timing on member k's context (its main trace kernel)."""
+        ctx = self.member(k)
+        if enable is not None:
+            _check(lib().sf_set_kernel_timing(ctx, max(1, int(period)) if enable else 0), "sf_set_kernel_timing", ctx)
+            return None
+        out = np.zeros(n, np.float32)
+        got = lib().sf_kernel_times(ctx, out.ctypes.data_as(_F), n)
+        if got < 0:
+            _check(got, "sf_kernel_times", ctx)
+        return out[:got]
+
+    def reset_stats(self):
+        self._check(lib().sf_group_reset_stats(self._g), "sf_group_reset_stats")
+
+    def stats(self) -> sf_stats:
+        """Over the members: max depth, closest distance, rays summed (accumulating across renders
+        like the reference's counters until reset_stats)."""
+        s = sf_stats()
+        self._check(lib().sf_group_get_stats(self._g, ctypes.byref(s)), "sf_group_get_stats")
+        return s

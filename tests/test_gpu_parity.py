@@ -369,18 +369,19 @@ def cost_bucket(c):
     return np.where((b >= 0) & (b < 32), b, np.where(k < (135 << 1), 0, 31))
 
 
-def expected_units(cost, split_buckets, spare=0):
+def expected_units(cost, split_buckets, spare=0, parts=2):
     """Host restatement of sf_order_scan + sf_order_scatter: tiles stably sorted by cost bucket, heaviest
-    first; split tiles become two adjacent half units (tile | 1 << 30, tile | 2 << 30). split_buckets
-    None (auto): whole buckets from the heaviest while the split count fits `spare` idle waves; k: the
-    top k occupied buckets, at most an eighth of the tiles. Bucket 0 is never split."""
+    first; split tiles become `parts` adjacent part units (halves tile | 1 << 29, tile | 2 << 29; quarters
+    tile | 3..6 << 29). split_buckets None (auto): whole buckets from the heaviest while the extra units
+    fit `spare` idle waves; k: the top k occupied buckets, at most an eighth of the tiles. Bucket 0 is
+    never split."""
     n = len(cost)
     bk = cost_bucket(cost)
     cnt = np.bincount(bk, minlength=32)
     bs, nsplit = 32, 0
     if split_buckets is None:
         for b in range(31, 0, -1):
-            if nsplit + cnt[b] > spare:
+            if (nsplit + cnt[b]) * (parts - 1) > spare:
                 break
             nsplit += int(cnt[b])
             bs = b
@@ -392,23 +393,26 @@ def expected_units(cost, split_buckets, spare=0):
         while bs < 32 and 8 * nsplit > n:
             nsplit -= int(cnt[bs])
             bs += 1
+    first = 3 if parts == 4 else 1
     units = []
     for t in np.lexsort((np.arange(n), -bk)):
         if bk[t] >= bs:
-            units += [t | (1 << 30), t | (2 << 30)]
+            units += [t | ((first + p) << 29) for p in range(parts)]
         else:
             units.append(t)
     return np.array(units, np.uint32), nsplit
 
 
-@pytest.mark.parametrize("W,H,split", [(1920, 1080, None), (1920, 1080, 1), (1920, 1080, 3), (3840, 2160, 1),
-                                       (100, 60, 1), (100, 60, None), (640, 360, None)])
-def test_tile_order_is_stable_heavy_first_schedule(W, H, split, monkeypatch):
+@pytest.mark.parametrize("W,H,split,parts", [(1920, 1080, None, 2), (1920, 1080, 1, 2), (1920, 1080, 3, 2),
+                                             (3840, 2160, 1, 2), (100, 60, 1, 2), (100, 60, None, 2), (640, 360, None, 2),
+                                             (1920, 1080, 2, 4), (640, 360, None, 4), (100, 60, None, 4)])
+def test_tile_order_is_stable_heavy_first_schedule(W, H, split, parts, monkeypatch):
     """The next render's work units (sf_order_scan + sf_order_scatter) are exactly the stable sort of
-    the last render's tile costs by bucket, heaviest first, with the heaviest tiles as half units: every
-    tile covered once (whole, or both halves)."""
+    the last render's tile costs by bucket, heaviest first, with the heaviest tiles as 2 or 4 part units:
+    every tile covered once (whole, or all its parts)."""
     if split is not None:
         monkeypatch.setenv("SF_SPLIT_BUCKETS", str(split))
+    monkeypatch.setenv("SF_SPLIT_PARTS", str(parts))
     n = ((W + 7) // 8) * ((H + 7) // 8)
     with sf.Sphereflake(W, H) as s:
         s.SetCamera(sf.config_camera(W, H, 0.25))
@@ -416,15 +420,17 @@ def test_tile_order_is_stable_heavy_first_schedule(W, H, split, monkeypatch):
         s.Render()
         units, cost = s.tile_order()
     if split is None:   # auto: recover the idle-wave count from the split made (<= spare < next bucket)
-        n_split = len(units) - n
-        exp, nsplit = expected_units(cost, None, n_split)
+        n_extra = len(units) - n
+        exp, nsplit = expected_units(cost, None, n_extra, parts)
     else:
-        exp, nsplit = expected_units(cost, split)
+        exp, nsplit = expected_units(cost, split, parts=parts)
     assert np.array_equal(units, exp)
-    assert len(units) == n + nsplit
-    tiles, half = units & ((1 << 30) - 1), units >> 30
-    assert np.array_equal(np.sort(tiles[half <= 1]), np.arange(n, dtype=np.uint32))
-    assert np.array_equal(np.sort(tiles[half == 1]), np.sort(tiles[half == 2]))
+    assert len(units) == n + nsplit * (parts - 1)
+    tiles, part = units & ((1 << 29) - 1), units >> 29
+    first = 3 if parts == 4 else 1
+    assert np.array_equal(np.sort(tiles[(part == 0) | (part == first)]), np.arange(n, dtype=np.uint32))
+    for p in range(1, parts):
+        assert np.array_equal(np.sort(tiles[part == first]), np.sort(tiles[part == first + p]))
     if split is None and W * H >= 1920 * 1080:
         assert nsplit == 0   # auto: more tiles than resident waves, nothing split
     elif split is None and W * H <= 100 * 60:
@@ -433,12 +439,15 @@ def test_tile_order_is_stable_heavy_first_schedule(W, H, split, monkeypatch):
         assert nsplit > 0
 
 
-def test_split_render_bit_exact_and_stable():
-    """With half units in the schedule (renders 2+), c3 stays bit-exact, splitting the heaviest bucket
-    and with every tile split-eligible (SF_SPLIT_BUCKETS=32: the cap of one eighth of the tiles applies)."""
+@pytest.mark.parametrize("parts", [2, 4])
+def test_split_render_bit_exact_and_stable(parts, monkeypatch):
+    """With part units in the schedule (renders 2+: halves or quarters), c3 stays bit-exact, splitting the
+    heaviest bucket and with every tile split-eligible (SF_SPLIT_BUCKETS=32: the cap of one eighth of the
+    tiles applies)."""
     fx = load_frame("c3")
     W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
     import os
+    monkeypatch.setenv("SF_SPLIT_PARTS", str(parts))
     for split in ("1", "32"):
         os.environ["SF_SPLIT_BUCKETS"] = split
         try:
@@ -451,7 +460,7 @@ def test_split_render_bit_exact_and_stable():
                     assert bad_rows(fx["row_digest_aux"], aux_digests(mint, idx)) == [], f"split {split} render {k}"
                 units, _ = s.tile_order()
                 st = s.stats()
-            assert (units >> 30).max() == 2
+            assert (units >> 29).max() == (6 if parts == 4 else 2)
             assert st.max_depth == fx["stats"]["max_depth"] and st.overflow_tiles == 0
         finally:
             del os.environ["SF_SPLIT_BUCKETS"]
