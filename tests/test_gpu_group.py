@@ -26,7 +26,7 @@ def single(W, H, cam):
     with sf.Sphereflake(W, H) as s:
         s.SetCamera(cam)
         s.Render()
-        pos, nrm = s.download()
+        pos, nrm, _, _ = s.download()
         return pos, nrm, s.stats()
 
 
