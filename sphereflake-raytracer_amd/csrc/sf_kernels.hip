@@ -133,6 +133,17 @@ __device__ __forceinline__ float wave_min(float v)
 // Wave64 ballot straight on the compare mask (no bool -> int -> compare round trip).
 __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
+// dst = (lane in m) ? src : dst, in dst's own register (tied operand): one v_cndmask on an SGPR lane
+// mask, no per-lane bool materialised and no copy between a pre- and a post-update register
+__device__ __forceinline__ void sel_in_place(float& dst, float src, uint64_t m)
+{
+    __asm__("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(dst) : "v"(src), "s"(m));
+}
+__device__ __forceinline__ void sel_in_place(uint32_t& dst, uint32_t src, uint64_t m)
+{
+    __asm__("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(dst) : "v"(src), "s"(m));
+}
+
 // Exact near root, kept out of line so the compiler cannot if-convert the rare exact path of the
 // fast LOD bracket into every child test.
 __device__ __attribute__((noinline)) float near_root_exact(float tca, float d2, float R2)
@@ -332,9 +343,10 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     h.cx = h.cy = h.cz = 0.f;
     h.index = 0xffffffffu;
     h.depth = -1;
-    h.hit = false;
-    // Per lane: the current best sphere is an ancestor of the node being expanded (see the self test).
-    bool anc = false;
+    h.hit = false;   // set on return: hit <=> depth >= 0
+    // Lanes whose current best sphere is an ancestor of the node being expanded (see the self test):
+    // a wave lane mask, so the tie-break and its updates are scalar mask algebra.
+    uint64_t ancm = 0ull;
 
     // ---- root node (depth 0): bounding sphere + LOD, centre straight from the kernel arguments
     const float rcx = root[9], rcy = root[10], rcz = root[11];
@@ -399,26 +411,26 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     // accepts strictly smaller t, so on an exact tie the earlier node in post-order wins. Pre-order
     // differs from post-order only for ancestor/descendant pairs, hence: a tie is accepted iff the
     // current best is an ancestor of this node (`anc`). Same result as the reference's order in every case.
-    auto self_test = [&](const float4 pc, uint32_t dd, bool act, uint32_t idx, float R2s) {
+    // (actm: the lanes for which the node is visited)
+    auto self_test = [&](const float4 pc, uint32_t dd, uint64_t actm, uint32_t idx, float R2s) {
         const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
         const float d2 = pc.w - tca * tca;
         const bool f0 = tca >= 0.0f, in = d2 <= R2s;
-        bool hs;
-        if constexpr (PACKET) hs = act && group_any<PW>(f0) && group_any<PW>(in);
-        else hs = act & f0 & in;
-        const uint64_t hsm = PACKET ? wave_ballot(hs) : (wave_ballot(act) & wave_ballot(f0) & wave_ballot(in));
+        uint64_t hsm;
+        if constexpr (PACKET) hsm = actm & wave_ballot(group_any<PW>(f0) && group_any<PW>(in));
+        else hsm = actm & wave_ballot(f0) & wave_ballot(in);
         if (hsm) {
             const float ts = near_root(tca, d2, R2s);
-            // bitwise, not short-circuit: selects instead of divergent branches
-            const bool acc = hs & ((ts < h.minT) | ((ts == h.minT) & anc));
-            h.minT = acc ? ts : h.minT;
-            h.cx = acc ? pc.x : h.cx;
-            h.cy = acc ? pc.y : h.cy;
-            h.cz = acc ? pc.z : h.cz;
-            h.index = acc ? idx : h.index;
-            h.depth = acc ? (int32_t)dd : h.depth;
-            h.hit = h.hit | acc;
-            anc = anc | acc;
+            const uint64_t accm = hsm & (wave_ballot(ts < h.minT) | (wave_ballot(ts == h.minT) & ancm));
+            sel_in_place(h.minT, ts, accm);
+            sel_in_place(h.cx, pc.x, accm);
+            sel_in_place(h.cy, pc.y, accm);
+            sel_in_place(h.cz, pc.z, accm);
+            sel_in_place(h.index, idx, accm);
+            uint32_t hd = (uint32_t)h.depth;
+            sel_in_place(hd, dd, accm);
+            h.depth = (int32_t)hd;
+            ancm |= accm;
         }
     };
 
@@ -428,7 +440,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     // (node: its 4 float4 at node, node + ps, node + 2 ps, node + 3 ps: ps = 4 for the root image,
     // SF_LDS_PLANE for a level table)
     // (the node's own sphere is tested by the caller when the node is entered, before this)
-    auto expand = [&](const float* node, uint32_t ps, uint32_t d, bool act, uint32_t& pend) -> uint32_t {
+    // (act: the lanes visiting the node, as a per-lane bool for the packet semantics and as the wave mask actm)
+    auto expand = [&](const float* node, uint32_t ps, uint32_t d, bool act, uint64_t actm, uint32_t& pend) -> uint32_t {
         d = __builtin_amdgcn_readfirstlane(d);   // wave-uniform: depth constants come by scalar loads
         lds_fence();
         const float4 pc = *reinterpret_cast<const float4*>(node);
@@ -475,15 +488,28 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             // Per-ray semantics. "Any lane" tests are scalar ANDs of ballots of single compares
             // (each ballot is the compare's own lane mask: no bool materialisation); per-lane bools
             // are formed only where a lane's own bit is needed (its E bit).
-            const uint64_t actm = wave_ballot(act);
             SF_COUNT(0, 1);
             SF_COUNT(7, __builtin_popcountll(actm));
+            // child i's {centre, cc}: a broadcast LDS read of plane 0 of the table just stored (one LDS
+            // instruction instead of four v_readlane on the VALU); the deepest provisioned level keeps no
+            // table, there the centre lanes are read back
+            const bool tab = d + 1u < levels;
+            const float* ctab = L.table(d);
             while (M) {   // uniform loop over the children some lane can reach, in index order
                 const uint32_t i = __builtin_ctz(M);
                 M &= M - 1u;
                 SF_COUNT(1, 1);
-                const float cx = readlane_f(x, 27u + i), cy = readlane_f(y, 27u + i);
-                const float cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
+                float cx, cy, cz, cc;
+#ifndef SF_CHILD_READLANE
+                if (tab) {
+                    const float4 c4 = *reinterpret_cast<const float4*>(ctab + i * 4u);
+                    cx = c4.x, cy = c4.y, cz = c4.z, cc = c4.w;
+                } else
+#endif
+                {
+                    cx = readlane_f(x, 27u + i), cy = readlane_f(y, 27u + i);
+                    cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
+                }
                 const float tca = (cx * dx + cy * dy) + cz * dz;
                 const float d2 = cc - tca * tca;
                 const bool f0 = tca >= 0.0f, f1 = d2 <= R2b;
@@ -521,15 +547,12 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 const uint64_t tinym = wave_ballot(tiny);
                 uint64_t exm = hbm & wave_ballot(yes) & ~tinym;
                 const uint64_t undm = hbm & ((wave_ballot(maybe) & ~wave_ballot(yes)) | tinym);
-                bool exi = act & f0 & f1 & yes & !tiny;
                 if (undm) {   // rare: exact IEEE root for the undecided lanes
-                    const bool und = act & f0 & f1 & ((maybe & !yes) | tiny);
                     const float te = near_root_exact(tca, d2, R2b);
-                    exi = und ? (te < T) : exi;
-                    exm = wave_ballot(exi);
+                    exm = (exm & ~undm) | (undm & wave_ballot(te < T));
                 }
-                e = exi ? (e | (1u << i)) : e;
-                pm |= (exm != 0ull ? 1u : 0u) << i;
+                sel_in_place(e, e | (1u << i), exm);   // the lanes of exm get bit i
+                if (exm != 0ull) pm |= 1u << i;
                 SF_COUNT(3, exm != 0ull ? 1 : 0);
             }
         } else {
@@ -572,8 +595,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         // (sfhost::leaf_threshold; per-ray semantics only) -- its children
         lds_fence();
         const float4 pc = *reinterpret_cast<const float4*>(L.root());
-        self_test(pc, 0u, ex0, 0u, depth_consts(K, 0u).y);
-        if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u))))) eN = expand(L.root(), 4u, 0u, ex0, pend);
+        self_test(pc, 0u, wave_ballot(ex0), 0u, depth_consts(K, 0u).y);
+        if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u))))) eN = expand(L.root(), 4u, 0u, ex0, wave_ballot(ex0), pend);
         else SF_COUNT(4, 1);
     }
 
@@ -589,19 +612,20 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 continue;
             }
             const bool a = ((eN >> c) & 1u) != 0u;
+            const uint64_t am = wave_ballot(a);
             const float* node = L.table(d) + c * 4u;
             // enter child c: its own sphere first (pre-order, see self_test), in one place for every child
             lds_fence();
             const float4 pc = *reinterpret_cast<const float4*>(node);
             maxd = (int32_t)d + 1 > maxd ? (int32_t)d + 1 : maxd;   // Sphereflake.h:157-160
-            self_test(pc, d + 1u, a, 9u * idxN + 1u + c, depth_consts(K, d + 1u).y);
+            self_test(pc, d + 1u, am, 9u * idxN + 1u + c, depth_consts(K, d + 1u).y);
             // A child none of whose children can pass LOD for any ray (sfhost::leaf_threshold) only needs its
             // own sphere: no push, no level, no child build.
             if (lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, d + 1u)))) {
                 SF_COUNT(4, 1);
                 SF_COUNT(8, 1);
-                SF_COUNT(9, __builtin_popcountll(wave_ballot(a)));
-                anc = anc & (h.depth != (int32_t)d + 1);   // the child is finished
+                SF_COUNT(9, __builtin_popcountll(am));
+                ancm &= wave_ballot(h.depth != (int32_t)d + 1);   // the child is finished
                 continue;
             }
             // save the open node's state, enter child c
@@ -612,12 +636,12 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             cN = c;
             d += 1u;
             SF_STAMP(1);
-            eN = expand(node, SF_LDS_PLANE, d, a, pend);
+            eN = expand(node, SF_LDS_PLANE, d, a, am, pend);
             SF_STAMP(2);
             continue;
         }
         // ---- the node at depth d is finished: a best sphere at depth d is no longer an ancestor
-        anc = anc & (h.depth != (int32_t)d);
+        ancm &= wave_ballot(h.depth != (int32_t)d);
         SF_STAMP(4);
         if (d == 0u) break;
         // ---- back to the parent
@@ -633,6 +657,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         (void)__builtin_amdgcn_readfirstlane(eN);   // (stamp builds: close the pop segment after its reads)
         SF_STAMP(5);
     }
+    h.hit = h.depth >= 0;
     SF_STAMP_FLUSH(phase_sums);
 #ifdef SF_COUNTS
     // per tile (COUNTS=1 builds): expanded nodes | child iterations << 16 | bounding-hit iterations << 32 |
