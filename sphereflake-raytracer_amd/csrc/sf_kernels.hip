@@ -724,6 +724,11 @@ struct TileStats {
 // loop let the structurizer run lanes in different iterations, which breaks wave-uniform code.
 __device__ __forceinline__ uint32_t wave_fetch_add(uint32_t* p, uint32_t v)
 {
+    {   // the address is uniform: say so, so that it can go to the asm in an SGPR pair
+        const uint64_t pi = reinterpret_cast<uint64_t>(p);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pi), hi = __builtin_amdgcn_readfirstlane((uint32_t)(pi >> 32));
+        p = reinterpret_cast<uint32_t*>((uint64_t)lo | ((uint64_t)hi << 32));
+    }
     uint32_t r, out;
     uint64_t saved;
     const uint32_t zero = 0u;
@@ -923,6 +928,7 @@ template <int WAVES>
 __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 {
     extern __shared__ float lds[];
+    const uint64_t w_start = __builtin_amdgcn_s_memrealtime();
     const uint32_t wv = threadIdx.x >> 6;
     // SF_QUEUES tile queues per render, one cache line each: queue k hands out tiles k, k + 8, k + 16, ...
     // A wave starts on its own XCD's queue and moves on to the next one when it runs dry. One queue
@@ -949,6 +955,11 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
     uint32_t k = __builtin_amdgcn_readfirstlane(xcc) & (SF_QUEUES - 1u), dry = 0u;
     int32_t maxd = -1;
     float closest = FLT_MAX;   // per lane
+    // The first unit of every wave is static: wave w (in dispatch order) takes unit w, so the head of the
+    // heavy-first order starts as the waves arrive instead of behind ~900 simultaneous atomics per queue;
+    // the queues hand out units nwaves, nwaves + 1, ...
+    const uint32_t nwaves = gridDim.x * WAVES;
+    uint32_t first = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + wv);   // (wv is wave-uniform)
     for (;;) {
         // Re-read the launch arguments every tile (scalar loads from the kernarg segment) instead of
         // keeping ~40 of them live in SGPRs across the whole persistent loop.
@@ -964,12 +975,20 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 #else
         at = a;
 #endif
-        const uint32_t q = wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u);   // uniform
-        const uint32_t g = q * SF_QUEUES + k;   // position in the render's unit order
-        if (g >= nunits) {        // queue k is empty: the next one; done when all are
-            if (++dry == SF_QUEUES) break;
-            k = (k + 1u) & (SF_QUEUES - 1u);
-            continue;
+        uint32_t g;                // position in the render's unit order
+        if (first != ~0u) {
+            g = first;
+            first = ~0u;
+            if (g >= nunits) break;   // (then the queues are empty too)
+        } else {
+            // (an agent-coherent load of the queue word before the atomic, to skip dry queues, made
+            // the frame 1.7x slower: it contends with the atomics on the line)
+            g = nwaves + wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u) * SF_QUEUES + k;   // uniform
+            if (g >= nunits) {    // queue k is empty: the next one; done when all are
+                if (++dry == SF_QUEUES) break;
+                k = (k + 1u) & (SF_QUEUES - 1u);
+                continue;
+            }
         }
         uint32_t t = g, part = 0u;
         if (at.tile_order) {      // heaviest tiles of the previous render first (scalar load)
@@ -994,6 +1013,12 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
         closest = fminf(closest, st.closest);
     }
     publish_stats(a, maxd, closest, 0u);
+    if ((a.flags & SF_FLAG_DIAG_UNITS) && a.tile_trace) {   // diagnostics: this wave's {start, end}, at the buffer's end
+        uint64_t* wt = a.tile_trace + 15u * (a.tiles_x * a.tile_rows) + SF_DIAG_SLOTS - 2u * nwaves
+                       + 2u * __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + wv);
+        wt[0] = w_start;
+        wt[1] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue1(FrameArgs a)

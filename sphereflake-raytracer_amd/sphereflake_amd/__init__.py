@@ -489,6 +489,7 @@ class Sphereflake:
                "sf_get_tile_trace", self._ctx)
         self.phase_sums = out[3 * n:3 * n + 16]   # segment cycle sums / event counts of diagnostic builds
         self.unit_trace = out[3 * n + 16:].reshape(4 * n, 3)   # per order position (SF_FLAG_DIAG_UNITS)
+        self.raw_trace = out   # (SF_FLAG_DIAG_UNITS: per persistent wave {start, end} at the end of the buffer)
         return out[:3 * n].reshape(n, 3)
 
     def tile_order(self):
