@@ -110,6 +110,7 @@ struct sf_ctx {
     bool persistent = true;                      // tuning knob: env SF_PERSISTENT=0 -> one workgroup per tile group
     uint32_t flags = 0;                          // SF_FLAG_* A/B switches: env SF_FLAGS
     int cus = 256;
+    uint32_t queues = SF_QUEUES;                 // persistent trace: tile queues, one per XCD (power of 2)
     int occ_key = -1, occ_blocks = 0;            // cached occupancy (waves per block, levels) -> blocks per CU
     uint32_t max_blocks = 0;                     // diagnostics: env SF_MAX_BLOCKS caps the persistent grid
     int variant = SF_VARIANT_AVX;                // reference path reproduced (sf_set_variant)
@@ -345,6 +346,15 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     c->H = height;
     c->fixup_blocks = prop.multiProcessorCount;
     c->cus = prop.multiProcessorCount;
+    {   // gfx950: 32 CUs per XCD; a compute partition of the chip exposes fewer XCDs (then fewer queues)
+        uint32_t x = c->cus >= 32 ? (uint32_t)c->cus / 32u : 1u, q = 1u;
+        while (q * 2u <= x && q * 2u <= SF_QUEUES) q *= 2u;
+        c->queues = q;
+        if (const char* ev = std::getenv("SF_NQUEUES")) {
+            const int v = std::atoi(ev);
+            if (v == 1 || v == 2 || v == 4 || v == 8) c->queues = (uint32_t)v;
+        }
+    }
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_ORDER")) c->use_order = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_BIN")) c->prog_bin = std::atoi(ev) != 0;
@@ -475,6 +485,7 @@ static FrameArgs frame_args(const sf_ctx* c)
     a.consts = c->consts;
     a.stats = c->stats;
     a.flags = c->flags;
+    a.queues = c->queues;
     return a;
 }
 

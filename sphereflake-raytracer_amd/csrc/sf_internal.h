@@ -110,6 +110,7 @@ struct FrameArgs {
     uint32_t* part_cost;              // per tile: max cycles over the parts of a split tile (reset by the last part)
     uint32_t* part_done;              // per tile: parts of a split tile finished (reset by the last part)
     uint32_t packet_lanes;            // frame-less mode: 8 (AVX variant) or 4 (SSE variant, 2x2 footprint)
+    uint32_t queues;                  // persistent trace: tile queues in use (one per XCD, power of 2 <= SF_QUEUES)
 };
 
 // Headless SSAO post-process (Shaders/post_ssao.glsl, post_ssao_blur.glsl,

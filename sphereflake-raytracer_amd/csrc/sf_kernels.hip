@@ -930,7 +930,8 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
     extern __shared__ float lds[];
     const uint64_t w_start = __builtin_amdgcn_s_memrealtime();
     const uint32_t wv = threadIdx.x >> 6;
-    // SF_QUEUES tile queues per render, one cache line each: queue k hands out tiles k, k + 8, k + 16, ...
+    // a.queues (<= SF_QUEUES) tile queues per render, one cache line each: queue k hands out the units
+    // after the static first ones with index = k mod a.queues
     // A wave starts on its own XCD's queue and moves on to the next one when it runs dry. One queue
     // for the whole chip serialises ~100 atomics/us on one address (measured: ~11 us per fetch).
     if (blockIdx.x == 0 && threadIdx.x < SF_QUEUES)
@@ -952,7 +953,13 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
     stage_root(L, a.root);
     uint32_t xcc;
     __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    uint32_t k = __builtin_amdgcn_readfirstlane(xcc) & (SF_QUEUES - 1u), dry = 0u;
+    // One queue per XCD (a.queues of them); a wave drains its own XCD's queue and then exits. Stealing
+    // from the other queues once the own one ran dry cost every wave up to 7 more atomics on queue words
+    // contended chip-wide at the end of the frame: the last wave exited ~60 us after the last tile
+    // ended. Every queue still drains: its XCD's waves only leave when it is empty, and queue units exist
+    // only when the grid is the full persistent grid, which spans every XCD.
+    const uint32_t nq = a.queues;
+    const uint32_t k = __builtin_amdgcn_readfirstlane(xcc) & (nq - 1u);
     int32_t maxd = -1;
     float closest = FLT_MAX;   // per lane
     // The first unit of every wave is static: wave w (in dispatch order) takes unit w, so the head of the
@@ -983,12 +990,8 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
         } else {
             // (an agent-coherent load of the queue word before the atomic, to skip dry queues, made
             // the frame 1.7x slower: it contends with the atomics on the line)
-            g = nwaves + wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u) * SF_QUEUES + k;   // uniform
-            if (g >= nunits) {    // queue k is empty: the next one; done when all are
-                if (++dry == SF_QUEUES) break;
-                k = (k + 1u) & (SF_QUEUES - 1u);
-                continue;
-            }
+            g = nwaves + wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u) * nq + k;   // uniform
+            if (g >= nunits) break;   // the XCD's queue is empty
         }
         uint32_t t = g, part = 0u;
         if (at.tile_order) {      // heaviest tiles of the previous render first (scalar load)
