@@ -24,8 +24,8 @@ extern "C" __global__ void sf_trace_queue1(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2(FrameArgs a);
 extern "C" __global__ void sf_trace_queue4(FrameArgs a);
 extern "C" __global__ void sf_order_scan(const uint32_t* chunk_cnt, uint32_t nc, uint32_t n_tiles,
-                                         uint32_t split_buckets, uint32_t parts, uint32_t spare, uint32_t* chunk_off,
-                                         uint32_t* order_meta);
+                                         uint32_t split_buckets, uint32_t parts, uint32_t spare, uint32_t prio_buckets,
+                                         uint32_t* chunk_off, uint32_t* order_meta);
 extern "C" __global__ void sf_order_scatter(const uint32_t* cost, uint32_t n, uint32_t* chunk_cnt,
                                             const uint32_t* chunk_off, const uint32_t* order_meta, uint32_t* order);
 extern "C" __global__ void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list, uint32_t* counters,
@@ -111,6 +111,7 @@ struct sf_ctx {
     uint32_t flags = 0;                          // SF_FLAG_* A/B switches: env SF_FLAGS
     int cus = 256;
     uint32_t queues = SF_QUEUES;                 // persistent trace: tile queues, one per XCD (power of 2)
+    uint32_t prio_buckets = 6;                   // top cost buckets (3 octaves) traced at raised wave priority (env SF_PRIO_BUCKETS)
     int occ_key = -1, occ_blocks = 0;            // cached occupancy (waves per block, levels) -> blocks per CU
     uint32_t max_blocks = 0;                     // diagnostics: env SF_MAX_BLOCKS caps the persistent grid
     int variant = SF_VARIANT_AVX;                // reference path reproduced (sf_set_variant)
@@ -159,9 +160,9 @@ struct sf_ctx {
     uint32_t* tile_order = nullptr;
     uint32_t* chunk_cnt = nullptr;     // per 64-tile chunk x SF_ORDER_BUCKETS (zeroed by sf_order_scatter)
     uint32_t* chunk_off = nullptr;
-    uint32_t* order_meta = nullptr;    // [0] work units in tile_order, [1] first split bucket, [2] parts per split tile
+    uint32_t* order_meta = nullptr;    // [0] work units in tile_order, [1] first split bucket, [2] parts per split tile, [3] first raised-priority bucket
     uint32_t split_buckets = SF_SPLIT_AUTO;   // env SF_SPLIT_BUCKETS = k: top k buckets (0: never split)
-    uint32_t split_parts = 2;          // env SF_SPLIT_PARTS = 2 (halves) | 4 (quarters)
+    uint32_t split_parts = 4;          // env SF_SPLIT_PARTS = 2 (halves) | 4 (quarters); 640x360: 0.122 -> 0.097 ms with quarters
     uint32_t* part_cost = nullptr;     // per tile: slowest part of a split tile (zeroed, reset by the last part)
     uint32_t* part_done = nullptr;     // per tile: parts finished (zeroed, reset by the last part)
     uint32_t order_n = 0;              // tile count the current tile_order is a permutation of (0: none)
@@ -363,6 +364,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if (const char* ev = std::getenv("SF_SPLIT_BUCKETS")) c->split_buckets = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_SPLIT_PARTS")) c->split_parts = std::atoi(ev) == 4 ? 4u : 2u;
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
+    if (const char* ev = std::getenv("SF_PRIO_BUCKETS")) c->prio_buckets = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_FLAGS")) c->flags = (uint32_t)std::strtoul(ev, nullptr, 0);
     if (const char* ev = std::getenv("SF_TRACE_WAVES")) {
         const int w = std::atoi(ev);
@@ -616,7 +618,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 const uint32_t waves = nblk * wpb;   // resident waves of the persistent grid
                 const uint32_t spare = waves > ntiles ? waves - ntiles : 0u;
                 hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->chunk_cnt, nc, ntiles,
-                                   c->split_buckets, c->split_parts, spare, c->chunk_off, c->order_meta);
+                                   c->split_buckets, c->split_parts, spare, c->prio_buckets, c->chunk_off, c->order_meta);
                 SF_HIP(c, hipGetLastError());
                 hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost, ntiles,
                                    c->chunk_cnt, (const uint32_t*)c->chunk_off, (const uint32_t*)c->order_meta,

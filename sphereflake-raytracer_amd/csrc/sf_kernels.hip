@@ -1004,6 +1004,19 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
             t = u & SF_UNIT_TILE_MASK;
             part = u >> SF_UNIT_PART_SHIFT;
         }
+        if (at.tile_order) {
+            // critical-path tiles (top cost buckets of the last render, order_meta[3]) at raised priority:
+            // the SIMD's issue arbitration serves them first, the cheap tiles absorb the wait
+#if defined(__HIP_DEVICE_COMPILE__)
+            typedef const __attribute__((address_space(4))) uint32_t* ConstU32;
+            const uint32_t pb = ((ConstU32)(const void*)at.order_meta)[3];
+            const uint32_t prev = ((ConstU32)(const void*)at.tile_cost)[t];
+#else
+            const uint32_t pb = at.order_meta[3], prev = at.tile_cost[t];
+#endif
+            if (cost_bucket(prev) >= pb) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         const uint64_t u_start = (at.flags & SF_FLAG_DIAG_UNITS) ? __builtin_amdgcn_s_memrealtime() : 0ull;
         const TileStats st = trace_tile<false>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity, part);
         if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace) {   // diagnostics only (uniform words)
@@ -1048,7 +1061,7 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 
 extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t* __restrict__ chunk_cnt, uint32_t nc,
                                                                    uint32_t n_tiles, uint32_t split_buckets, uint32_t parts,
-                                                                   uint32_t spare,
+                                                                   uint32_t spare, uint32_t prio_buckets,
                                                                    uint32_t* __restrict__ chunk_off,
                                                                    uint32_t* __restrict__ order_meta)
 {
@@ -1099,6 +1112,12 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t*
             while (bs < (int)SF_ORDER_BUCKETS && 8u * nsplit > n_tiles) nsplit -= tot[bs++];
         }
         split_from = (uint32_t)bs;
+        // the top `prio_buckets` occupied cost buckets run at raised wave priority next render (their
+        // serial DFS is the frame's critical path)
+        int btop = (int)SF_ORDER_BUCKETS - 1;
+        while (btop > 0 && tot[btop] == 0u) --btop;
+        const int bp = btop - (int)prio_buckets + 1;
+        order_meta[3] = prio_buckets == 0u ? SF_ORDER_BUCKETS : (uint32_t)(bp < 0 ? 0 : bp);
         uint32_t acc = 0u;
         for (int bb = (int)SF_ORDER_BUCKETS - 1; bb >= 0; --bb) {
             const uint32_t x = tot[bb] * (bb >= bs ? parts : 1u);

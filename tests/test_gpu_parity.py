@@ -534,3 +534,18 @@ def test_fewer_tile_queues_bit_exact(nq, monkeypatch):
                 s.Render()
                 pos, nrm, _, _ = s.download()
                 assert frame_digest(pos, nrm) == fx["frame_digest"], (name, nq)
+
+
+@pytest.mark.parametrize("prio", ["0", "1", "32"])
+def test_raised_priority_tiles_bit_exact(prio, monkeypatch):
+    """The top SF_PRIO_BUCKETS cost buckets of the last render run at raised wave priority (none / the
+    top one / all): scheduling only, frames equal the golden."""
+    monkeypatch.setenv("SF_PRIO_BUCKETS", prio)
+    fx = load_frame("c3")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for _ in range(3):
+            s.Render()
+            pos, nrm, _, _ = s.download()
+            assert frame_digest(pos, nrm) == fx["frame_digest"], prio
