@@ -14,7 +14,7 @@
 #define SF_TILE 8              // a wave64 traces one 8x8 pixel tile
 #define SF_WAVES_PER_BLOCK 4   // 256-thread workgroups (per-ray kernel)
 #ifndef SF_WAVES_PER_EU
-#define SF_WAVES_PER_EU 7      // occupancy target of the persistent trace kernels (waves per SIMD)
+#define SF_WAVES_PER_EU 8      // occupancy target of the persistent trace kernels (waves per SIMD)
 #endif
 #ifndef SF_TRACE_WAVES
 #define SF_TRACE_WAVES 2       // independent waves per workgroup of the wave kernels
@@ -25,10 +25,11 @@
 // a level table stores them in 4 planes of 9 float4 (plane k = float4 k of children 0..8).
 #define SF_LDS_ROOT 16
 #define SF_LDS_CONE 8                     // the wave's ray cone {ax, ay, az, cosT, sinT, -, -, -}
-#define SF_LDS_PLANE 36                   // one float4 of each of the 9 children (column planes)
-#define SF_LDS_TABLE (4 * SF_LDS_PLANE)   // the 9 child transforms of the node open at a level
+#define SF_LDS_PLANE 36                   // plane 0: {centre, cc} float4 of each of the 9 children
+#define SF_LDS_COLS 27                    // planes 1..3: column j (xyz, float3) of each of the 9 children
+#define SF_LDS_TABLE (SF_LDS_PLANE + 3 * SF_LDS_COLS)   // the 9 child transforms of the node open at a level
 #define SF_LDS_E 32                       // 64 lanes x u16: per-lane child-expand bits of that node
-#define SF_LDS_LEVEL (SF_LDS_TABLE + SF_LDS_E)
+#define SF_LDS_LEVEL (SF_LDS_TABLE + SF_LDS_E + 3)      // (+3: levels stay 16-byte aligned)
 // levels - 1 level images: the deepest provisioned level's table is never read (see traverse)
 #define SF_LDS_WAVE_FLOATS(levels) (SF_LDS_ROOT + SF_LDS_CONE + ((levels) - 1) * SF_LDS_LEVEL)
 

@@ -187,9 +187,10 @@ __device__ __forceinline__ bool group_any(bool p)
 //   self       hs = active && any_g(tca >= 0) && any_g(d2 <= r^2); accept lanes with d2 <= r^2 && t < minT
 // For per-ray groups these are exactly the reference's per-lane tests.
 // ------------------------------------------------------------------------------------------
-// Per-wave LDS image (floats): [root: 16][cone: 8][per level: table 4 planes x 9 x 4 | E 32]. A transform
-// is 4 float4: {cx cy cz cc}, {col0.xyz -}, {col1.xyz -}, {col2.xyz -} (cc = Dot(centre, centre)); the root
-// keeps them contiguous, a level table in planes (plane k = float4 k of the 9 children, SF_LDS_PLANE apart).
+// Per-wave LDS image (floats): [root: 16][cone: 8][per level: table | E 32 | pad 3]. A transform is
+// {cx cy cz cc} (cc = Dot(centre, centre)) and its three axis columns. The root keeps them as 4 contiguous
+// float4; a level table keeps plane 0 = the 9 children's {centre, cc} float4, then planes 1..3 = their
+// column j as float3 (9 x 3 floats each): 117 floats per level instead of 144, so 8 waves fit per SIMD.
 struct TraverseLds {
     float* base;
     __device__ __forceinline__ float* root() const { return base; }
@@ -398,9 +399,10 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     float b[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) b[j] = K->child[bi][4u * bc + j];
-    // level table in column planes: plane k (0 = {centre, cc}, 1..3 = columns 0..2) holds the 9 children's
-    // float4 contiguously, so the build's float4 stores from consecutive lanes are conflict-free
-    const uint32_t slot = (bc == 3u ? 0u : bc + 1u) * SF_LDS_PLANE + bi * 4u;
+    // where this lane's column goes in a level table: centre lanes (bc = 3) xyz + cc at plane 0, the others
+    // xyz in their column plane; the centre lanes' cc store goes to plane 0, the others' to a junk word of
+    // the cone block (so both stores are unconditional: no divergent region)
+    const uint32_t slot = bc == 3u ? bi * 4u : SF_LDS_PLANE + bc * SF_LDS_COLS + bi * 3u;
 
     uint32_t d = 0;                 // uniform: depth of the open (expanded) node
     uint32_t cN = 0;                // uniform: its index in the parent's table
@@ -437,17 +439,18 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     // ---- expand the node at `node` (depth d, transform in LDS): build its 9 child transforms into
     // table(d), then test the children (depth d+1) for the lanes in `act`. Returns this lane's 9-bit
     // "child expands" vector; *pend = the wave's mask of children some lane expands.
-    // (node: its 4 float4 at node, node + ps, node + 2 ps, node + 3 ps: ps = 4 for the root image,
-    // SF_LDS_PLANE for a level table)
+    // (node: {centre, cc} float4 at node; its columns j = 0..2 (xyz) at col + j * cs: col = node + 4,
+    // cs = 4 for the root image; col = the table's column planes + 3 c, cs = SF_LDS_COLS for child c of a level)
     // (the node's own sphere is tested by the caller when the node is entered, before this)
     // (act: the lanes visiting the node, as a per-lane bool for the packet semantics and as the wave mask actm)
-    auto expand = [&](const float* node, uint32_t ps, uint32_t d, bool act, uint64_t actm, uint32_t& pend) -> uint32_t {
+    auto expand = [&](const float* node, const float* col, uint32_t cs, uint32_t d, bool act, uint64_t actm,
+                      uint32_t& pend) -> uint32_t {
         d = __builtin_amdgcn_readfirstlane(d);   // wave-uniform: depth constants come by scalar loads
         lds_fence();
         const float4 pc = *reinterpret_cast<const float4*>(node);
-        const float4 p0 = *reinterpret_cast<const float4*>(node + ps);
-        const float4 p1 = *reinterpret_cast<const float4*>(node + 2u * ps);
-        const float4 p2 = *reinterpret_cast<const float4*>(node + 3u * ps);
+        const float3 p0 = *reinterpret_cast<const float3*>(col);
+        const float3 p1 = *reinterpret_cast<const float3*>(col + cs);
+        const float3 p2 = *reinterpret_cast<const float3*>(col + 2u * cs);
         const float4 dtn = depth_consts(K, d);        // this node: (4/3) r
         const float4 dtc = depth_consts(K, d + 1u);   // children: (2r)^2, T
         // world = parent * child (SIMD_AVX.h:59-81), child translation scaled by (4/3) r (Sphereflake.h:162-172):
@@ -460,7 +463,11 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         const float w = (x * x + y * y) + z * z;   // Dot(centre, centre) on the centre lanes (bc = 3)
         // table(levels-1) is never read: entering a child of the deepest provisioned level overflows
         // first. Not allocated, not stored (uniform branch).
-        if (d + 1u < levels) *reinterpret_cast<float4*>(L.table(d) + slot) = make_float4(x, y, z, w);
+        if (d + 1u < levels) {
+            float* const tb = L.table(d);
+            *reinterpret_cast<float3*>(tb + slot) = make_float3(x, y, z);
+            *(bc == 3u ? tb + slot + 3u : L.cone() + 5u + (lane & 1u)) = w;
+        }
         const float R2b = dtc.x;
         const float T = dtc.w;
         // Cone cull of child bi (centre c in lanes 27..35): no ray of the wave's cone can hit its bounding
@@ -596,7 +603,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         lds_fence();
         const float4 pc = *reinterpret_cast<const float4*>(L.root());
         self_test(pc, 0u, wave_ballot(ex0), 0u, depth_consts(K, 0u).y);
-        if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u))))) eN = expand(L.root(), 4u, 0u, ex0, wave_ballot(ex0), pend);
+        if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u))))) eN = expand(L.root(), L.root() + 4u, 4u, 0u, ex0, wave_ballot(ex0), pend);
         else SF_COUNT(4, 1);
     }
 
@@ -636,7 +643,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             cN = c;
             d += 1u;
             SF_STAMP(1);
-            eN = expand(node, SF_LDS_PLANE, d, a, am, pend);
+            eN = expand(node, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, a, am, pend);
             SF_STAMP(2);
             continue;
         }
