@@ -414,6 +414,14 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     kernel = sf.SF_KERNEL_WAVE if args.kernel == "wave" else sf.SF_KERNEL_PER_RAY
 
+    # a tiny render on a throw-away context first: loads the code object, so that `first_render_ms`
+    # below is the first render of a fresh context, not the process's first kernel launch
+    t_load = time.perf_counter()
+    with sf.Sphereflake(64, 64, device=dev.index) as warm:
+        warm.SetCamera(sf.config_camera(64, 64, args.K))
+        warm.Render()
+        warm.Synchronize()
+    module_load_ms = (time.perf_counter() - t_load) * 1e3
     ctx = sf.Sphereflake(width, height, device=dev.index)
     sh = stream.cuda_stream
 
@@ -597,6 +605,7 @@ def main():
             "frame_ms": round(t_step * 1e3, 4),
             "kernel_ms": round(kern_ms_max, 4),
             "first_render_ms": round(first_ms, 4) if first_ms is not None else None,
+            "process_first_launch_ms": round(module_load_ms, 3),
             "fixed_camera": fixed,
             "post": post,
             "d2h": d2h,
