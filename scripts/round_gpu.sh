@@ -17,5 +17,5 @@ tail -1 $OUT/bench.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-extras > $OUT/stats.log 2>&1
 cat $(find $OUT/stats -name "*kernel_stats.csv")
-python3 $R/scripts/trace_avg.py $(find $OUT/stats -name "*kernel_trace.csv") sf_trace_queue2 200 31 | tee $OUT/trace_avg.txt
+python3 $R/scripts/trace_avg.py $(find $OUT/stats -name "*kernel_trace.csv") sf_trace_queue2 200 32 | tee $OUT/trace_avg.txt
 grep '^{' $OUT/stats.log | tail -1
