@@ -11,3 +11,7 @@ timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
     bench.py --gpus 2 --steps 10 --warmup 3 --mode rows --no-cpu-baseline > gpurun_out/multi/rows.json 2> gpurun_out/multi/rows.err \
     || { tail -20 gpurun_out/multi/rows.err; exit 1; }
 cat gpurun_out/multi/rows.json
+timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 \
+    bench.py --gpus 2 --steps 10 --warmup 3 --mode rows-rccl --no-cpu-baseline > gpurun_out/multi/rows_rccl.json 2> gpurun_out/multi/rows_rccl.err \
+    || { tail -20 gpurun_out/multi/rows_rccl.err; exit 1; }
+cat gpurun_out/multi/rows_rccl.json
