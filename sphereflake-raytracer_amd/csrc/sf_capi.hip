@@ -27,7 +27,8 @@ extern "C" __global__ void sf_order_scan(const uint32_t* chunk_cnt, uint32_t nc,
                                          uint32_t split_buckets, uint32_t parts, uint32_t spare, uint32_t prio_buckets,
                                          uint32_t* chunk_off, uint32_t* order_meta);
 extern "C" __global__ void sf_order_scatter(const uint32_t* cost, uint32_t n, uint32_t* chunk_cnt,
-                                            const uint32_t* chunk_off, const uint32_t* order_meta, uint32_t* order);
+                                            const uint32_t* chunk_off, const uint32_t* order_meta, uint32_t* order,
+                                            uint32_t* rank_out);
 extern "C" __global__ void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list, uint32_t* counters,
                                          uint32_t parity);
 extern "C" __global__ void sf_trace_ray(FrameArgs a);
@@ -50,7 +51,8 @@ extern "C" __global__ void sf_progressive_fixup_sse(FrameArgs a, const uint32_t*
                                                     const uint32_t* ovf_list, uint32_t* counters, uint32_t parity);
 extern "C" __global__ void sf_packet_bin(FrameArgs a, const uint32_t* draws, uint64_t counter0, uint32_t packets,
                                          uint32_t pw, uint32_t bin_shift, uint32_t bins_x, uint32_t* bin_cnt);
-extern "C" __global__ void sf_packet_scan(uint32_t* bin_cnt, uint32_t nbins);
+extern "C" __global__ void sf_packet_scan(uint32_t* bin_cnt, uint32_t nbins, const uint32_t* rank);
+extern "C" __global__ void sf_bin_hist(const uint32_t* bin_cost, uint32_t nbins, uint32_t* chunk_cnt);
 extern "C" __global__ void sf_packet_place(FrameArgs a, const uint32_t* draws, uint64_t counter0, uint32_t packets,
                                            uint32_t pw, uint32_t bin_shift, uint32_t bins_x, uint32_t* bin_cur,
                                            uint32_t* perm);
@@ -122,6 +124,16 @@ struct sf_ctx {
     uint32_t prog_cap = 0;             // packets the scratch buffers hold
     uint32_t* perm = nullptr;          // binned trace order of a batch (prog_cap)
     uint32_t* bin_cnt = nullptr;       // SF_PROG_MAX_BINS packet-bin counters / cursors
+    // frame-less heavy-first trace order (env SF_PROG_ORDER=0: bins in index order): per bin the cycles of
+    // the last wave that started in it, its histogram per 64-bin chunk, and the bins' heavy-first rank
+    bool prog_order = true;
+    uint32_t* bin_cost = nullptr;
+    uint32_t* bin_rank = nullptr;
+    uint32_t* bin_order = nullptr;
+    uint32_t* bin_chunk_cnt = nullptr;
+    uint32_t* bin_chunk_off = nullptr;
+    uint32_t* bin_meta = nullptr;
+    uint32_t bin_key = 0;              // (shift, bins) of the batches whose costs bin_cost holds; 0 = none
     bool prog_bin = true;              // env SF_PROG_BIN=0: trace packets in draw order
     // Draw prefetch: after a large batch, the next batch's mt19937 draws (same stream, same size) are
     // generated on pf_stream while this batch traces -- the generator is one sequential workgroup.
@@ -238,6 +250,12 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->lanes);
     (void)hipFree(c->perm);
     (void)hipFree(c->bin_cnt);
+    (void)hipFree(c->bin_cost);
+    (void)hipFree(c->bin_rank);
+    (void)hipFree(c->bin_order);
+    (void)hipFree(c->bin_chunk_cnt);
+    (void)hipFree(c->bin_chunk_off);
+    (void)hipFree(c->bin_meta);
     if (c->pf_stream) (void)hipStreamSynchronize(c->pf_stream);
     if (c->h_prog_depth) (void)hipHostFree(c->h_prog_depth);
     (void)hipFree(c->prog_ovf);
@@ -361,6 +379,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if (const char* ev = std::getenv("SF_PROG_BIN")) c->prog_bin = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_PREFETCH")) c->prog_prefetch = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_ADAPT")) c->prog_adapt = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_PROG_ORDER")) c->prog_order = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_SPLIT_BUCKETS")) c->split_buckets = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_SPLIT_PARTS")) c->split_parts = std::atoi(ev) == 4 ? 4u : 2u;
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
@@ -622,7 +641,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 SF_HIP(c, hipGetLastError());
                 hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost, ntiles,
                                    c->chunk_cnt, (const uint32_t*)c->chunk_off, (const uint32_t*)c->order_meta,
-                                   c->tile_order);
+                                   c->tile_order, nullptr);
                 SF_HIP(c, hipGetLastError());
                 c->order_n = ntiles;
             }
@@ -737,6 +756,7 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     a.min_t = c->min_t;
     a.emit_aux = 1;
     a.packet_lanes = pl;
+    if (c->flags & SF_FLAG_DIAG_UNITS) a.tile_trace = c->tile_trace;   // per-wave diagnostics (sf_set_tile_trace)
     if (!prefetched) {
         hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(1024), 0, s, c->mt_state, c->draws, 2 * packets);
         SF_HIP(c, hipGetLastError());
@@ -776,10 +796,44 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
         }
         const uint32_t nbins = bx * by;
         const uint32_t pb = (packets + 255u) / 256u;
+        // Heavy-first: bins ranked by the cycles their waves took in the previous batch of the same
+        // binning (the view and the bins do not move between batches); the trace grid then starts with
+        // the heaviest packets instead of meeting them wherever their screen region falls.
+        const uint32_t* rank = nullptr;
+        if (c->prog_order) {
+            const uint32_t nc = (nbins + 63u) / 64u;
+            const uint32_t key = (shift << 24) | nbins;
+            if (!c->bin_cost) {
+                const size_t nc_max = (SF_PROG_MAX_BINS + 63u) / 64u;
+                SF_HIP(c, hipMalloc(&c->bin_cost, SF_PROG_MAX_BINS * 4));
+                SF_HIP(c, hipMalloc(&c->bin_rank, SF_PROG_MAX_BINS * 4));
+                SF_HIP(c, hipMalloc(&c->bin_order, SF_PROG_MAX_BINS * 4));
+                SF_HIP(c, hipMalloc(&c->bin_chunk_cnt, nc_max * SF_ORDER_BUCKETS * 4));
+                SF_HIP(c, hipMalloc(&c->bin_chunk_off, nc_max * SF_ORDER_BUCKETS * 4));
+                SF_HIP(c, hipMalloc(&c->bin_meta, 4 * 4));
+            }
+            if (c->bin_key == key) {
+                hipLaunchKernelGGL(sf_bin_hist, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->bin_cost, nbins,
+                                   c->bin_chunk_cnt);
+                hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->bin_chunk_cnt, nc, nbins,
+                                   0u, 2u, 0u, 0u, c->bin_chunk_off, c->bin_meta);
+                hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->bin_cost, nbins,
+                                   c->bin_chunk_cnt, (const uint32_t*)c->bin_chunk_off, (const uint32_t*)c->bin_meta,
+                                   c->bin_order, c->bin_rank);
+                SF_HIP(c, hipGetLastError());
+                rank = c->bin_rank;
+            } else {   // new binning: no costs yet (this batch records them)
+                SF_HIP(c, hipMemsetAsync(c->bin_cost, 0, SF_PROG_MAX_BINS * 4, s));
+                c->bin_key = key;
+            }
+            a.bin_cost = c->bin_cost;
+            a.bin_shift = shift;
+            a.bins_x = bx;
+        }
         SF_HIP(c, hipMemsetAsync(c->bin_cnt, 0, (size_t)nbins * 4, s));
         hipLaunchKernelGGL(sf_packet_bin, dim3(pb), dim3(256), 0, s, a, (const uint32_t*)c->draws, counter0, packets,
                            pl, shift, bx, c->bin_cnt);
-        hipLaunchKernelGGL(sf_packet_scan, dim3(1), dim3(1024), 0, s, c->bin_cnt, nbins);
+        hipLaunchKernelGGL(sf_packet_scan, dim3(1), dim3(1024), 0, s, c->bin_cnt, nbins, rank);
         hipLaunchKernelGGL(sf_packet_place, dim3(pb), dim3(256), 0, s, a, (const uint32_t*)c->draws, counter0, packets,
                            pl, shift, bx, c->bin_cnt, c->perm);
         SF_HIP(c, hipGetLastError());

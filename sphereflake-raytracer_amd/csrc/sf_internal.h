@@ -53,6 +53,8 @@
 // kernel by its order position g: {start, end, unit} (s_memrealtime) after the tile trace and the
 // diagnostic slots (room for 2 units per tile)
 #define SF_FLAG_DIAG_UNITS 0x20u
+// diagnostics only, WRONG results: the frame-less trace skips its per-pixel owner atomics (cost study)
+#define SF_FLAG_DIAG_NO_OWNER 0x40u
 
 struct DepthTables {
     float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)
@@ -112,6 +114,8 @@ struct FrameArgs {
     uint32_t* part_done;              // per tile: parts of a split tile finished (reset by the last part)
     uint32_t packet_lanes;            // frame-less mode: 8 (AVX variant) or 4 (SSE variant, 2x2 footprint)
     uint32_t queues;                  // persistent trace: tile queues in use (one per XCD, power of 2 <= SF_QUEUES)
+    uint32_t* bin_cost;               // frame-less mode (NULL = off): per packet bin, cycles of the last wave starting in it
+    uint32_t bin_shift, bins_x;       // frame-less mode: the batch's packet bins (squares of 2^bin_shift pixels)
 };
 
 // Headless SSAO post-process (Shaders/post_ssao.glsl, post_ssao_blur.glsl,

@@ -393,9 +393,21 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     // divergent region; its VALU cost is per wave either way.
     const uint32_t bl = lane < 36u ? lane : lane - 36u;
     const uint32_t bi = bl % 9u, bc = bl / 9u;
-    // per-ray semantics only: in packet semantics a lane with tca < 0 can pass LOD through another
-    // lane's bounding hit (SIMD_AVX.h:254), which the reachability bound below does not cover
-    const bool lod_cull = !PACKET && (K_flags & SF_FLAG_NO_LOD_CULL) == 0u;
+    // The leaf-threshold skip bounds t from below for every ray. In packet semantics a lane with tca < 0
+    // can also pass LOD through another lane's bounding hit (negative t, SIMD_AVX.h:254), which that
+    // bound does not cover: there the skip additionally needs every sphere of the child's subtree in
+    // front of every lane (leaf_front below).
+    const bool lod_cull = (K_flags & SF_FLAG_NO_LOD_CULL) == 0u;
+    // Every sphere of a node's subtree lies inside its bounding sphere (radius 2r around its centre c).
+    // If c.d >= 2r for every lane's unit direction d, each such sphere (centre c', radius R') has
+    // c'.d - R' >= c.d - 2r >= 0, so its near root t >= 0 for every lane: no negative t, and the
+    // per-ray leaf threshold applies. Checked as tca >= 0 and tca^2 >= (2r)^2 (1 + 2^-6), the margin
+    // covering the rounding of tca, |d| and the threshold.
+    auto leaf_front = [&](const float4 pc, float R2b) -> bool {
+        if constexpr (!PACKET) return true;
+        const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
+        return wave_ballot(!(tca >= 0.0f && tca * tca >= R2b * (1.0f + 0x1p-6f))) == 0ull;
+    };
     float b[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) b[j] = K->child[bi][4u * bc + j];
@@ -603,7 +615,9 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         lds_fence();
         const float4 pc = *reinterpret_cast<const float4*>(L.root());
         self_test(pc, 0u, wave_ballot(ex0), 0u, depth_consts(K, 0u).y);
-        if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u))))) eN = expand(L.root(), L.root() + 4u, 4u, 0u, ex0, wave_ballot(ex0), pend);
+        if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u))) &&
+              leaf_front(pc, depth_consts(K, 0u).x)))
+            eN = expand(L.root(), L.root() + 4u, 4u, 0u, ex0, wave_ballot(ex0), pend);
         else SF_COUNT(4, 1);
     }
 
@@ -628,7 +642,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             self_test(pc, d + 1u, am, 9u * idxN + 1u + c, depth_consts(K, d + 1u).y);
             // A child none of whose children can pass LOD for any ray (sfhost::leaf_threshold) only needs its
             // own sphere: no push, no level, no child build.
-            if (lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, d + 1u)))) {
+            if (lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, d + 1u))) &&
+                leaf_front(pc, depth_consts(K, d + 1u).x)) {
                 SF_COUNT(4, 1);
                 SF_COUNT(8, 1);
                 SF_COUNT(9, __builtin_popcountll(am));
@@ -1154,8 +1169,10 @@ extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t
                                                                     uint32_t* __restrict__ chunk_cnt,
                                                                     const uint32_t* __restrict__ chunk_off,
                                                                     const uint32_t* __restrict__ order_meta,
-                                                                    uint32_t* __restrict__ order)
+                                                                    uint32_t* __restrict__ order,
+                                                                    uint32_t* __restrict__ rank_out)
 {
+    // (rank_out, when not NULL: rank_out[i] = item i's position, the inverse permutation; unsplit orders only)
     const uint32_t c = blockIdx.x, lane = threadIdx.x, i = c * 64u + lane;
     const uint32_t split_from = order_meta[1], parts = order_meta[2];
     const uint32_t first = parts == 4u ? SF_PART_QUARTER0 : SF_PART_HALF0;
@@ -1172,6 +1189,7 @@ extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t
                 for (uint32_t p = 0; p < parts; ++p) order[off + parts * rank + p] = i | ((first + p) << SF_UNIT_PART_SHIFT);
             } else {
                 order[off + rank] = i;
+                if (rank_out) rank_out[i] = off + rank;
             }
         }
         pending &= ~m;
@@ -1421,15 +1439,20 @@ extern "C" __global__ __launch_bounds__(256) void sf_packet_bin(FrameArgs a, con
     atomicAdd(bin_cnt + b, 1u);
 }
 
-extern "C" __global__ __launch_bounds__(1024) void sf_packet_scan(uint32_t* bin_cnt, uint32_t nbins)
+extern "C" __global__ __launch_bounds__(1024) void sf_packet_scan(uint32_t* bin_cnt, uint32_t nbins,
+                                                                  const uint32_t* __restrict__ rank)
 {
-    // Counts -> exclusive offsets in place (the place cursors). Staged through LDS so that global
-    // reads and writes are coalesced; thread t scans bins [t * per, (t + 1) * per) of the staged copy
-    // (index padded by 1 per 32 against bank conflicts).
+    // Counts -> exclusive offsets in place (the place cursors), the bins taken in the order rank[]
+    // (heaviest first, from the last batch's per-bin wave cycles) or in index order (rank NULL). Staged
+    // through LDS (at the bin's rank) so that global reads and writes are coalesced; thread t scans
+    // ranks [t * per, (t + 1) * per) of the staged copy (index padded by 1 per 32 against bank conflicts).
     __shared__ uint32_t cnt[SF_PROG_MAX_BINS + SF_PROG_MAX_BINS / 32u];
     __shared__ uint32_t part[16];
     const uint32_t t = threadIdx.x, per = (nbins + 1023u) / 1024u, b0 = t * per, b1 = min(nbins, b0 + per);
-    for (uint32_t i = t; i < nbins; i += 1024u) cnt[i + (i >> 5)] = bin_cnt[i];
+    for (uint32_t i = t; i < nbins; i += 1024u) {
+        const uint32_t r = rank ? rank[i] : i;
+        cnt[r + (r >> 5)] = bin_cnt[i];
+    }
     __syncthreads();
     uint32_t s_ = 0u;
     for (uint32_t b = b0; b < b1; ++b) s_ += cnt[b + (b >> 5)];
@@ -1459,7 +1482,26 @@ extern "C" __global__ __launch_bounds__(1024) void sf_packet_scan(uint32_t* bin_
         off += c;
     }
     __syncthreads();
-    for (uint32_t i = t; i < nbins; i += 1024u) bin_cnt[i] = cnt[i + (i >> 5)];
+    for (uint32_t i = t; i < nbins; i += 1024u) {
+        const uint32_t r = rank ? rank[i] : i;
+        bin_cnt[i] = cnt[r + (r >> 5)];
+    }
+}
+
+// Frame-less heavy-first order: per 64-bin chunk, the cost-bucket histogram of the bins' last recorded
+// wave cycles (input of sf_order_scan / sf_order_scatter, which then rank the bins heaviest first).
+extern "C" __global__ __launch_bounds__(64) void sf_bin_hist(const uint32_t* __restrict__ bin_cost, uint32_t nbins,
+                                                             uint32_t* __restrict__ chunk_cnt)
+{
+    const uint32_t c = blockIdx.x, lane = threadIdx.x, i = c * 64u + lane;
+    const uint32_t bk = i < nbins ? cost_bucket(bin_cost[i]) : SF_ORDER_BUCKETS;
+    uint32_t mine = 0u;
+#pragma unroll 1
+    for (uint32_t b = 0; b < SF_ORDER_BUCKETS; ++b) {
+        const uint32_t n = (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(bk == b));
+        mine = lane == b ? n : mine;
+    }
+    if (lane < SF_ORDER_BUCKETS) chunk_cnt[c * SF_ORDER_BUCKETS + lane] = mine;
 }
 
 extern "C" __global__ __launch_bounds__(256) void sf_packet_place(FrameArgs a, const uint32_t* draws, uint64_t counter0,
@@ -1485,6 +1527,8 @@ __device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t slot = wave * PPW + lane / PW;   // position in the (binned) trace order
     if (wave * PPW >= packets) return;   // wave-uniform
+    const uint64_t w_start = (a.flags & SF_FLAG_DIAG_UNITS) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const uint64_t c_start = a.bin_cost ? __builtin_amdgcn_s_memtime() : 0ull;
     const bool valid = slot < packets;
     const uint32_t packet = valid ? (perm ? perm[slot] : slot) : slot;
     const uint32_t q = lane % PW;
@@ -1518,7 +1562,7 @@ __device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint
     const bool inb = valid && pix < (uint64_t)a.W * a.H;
     out.pixel = inb ? (uint32_t)pix : 0xffffffffu;
     if (valid) lanes[(size_t)packet * PW + q] = out;
-    if (inb) atomicMax(owner + pix, (unsigned long long)(ticket0 + packet));
+    if (inb && !(a.flags & SF_FLAG_DIAG_NO_OWNER)) atomicMax(owner + pix, (unsigned long long)(ticket0 + packet));
 
     const float closest = wave_min(inb ? h.minT : FLT_MAX);
     const bool anyov = wave_ballot(overflowed) != 0ull;
@@ -1535,6 +1579,22 @@ __device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint
     if (anyov && ovf_list) {
         const uint32_t k = wave_fetch_add(ovf_cnt, 1u);
         ovf_list[k] = wave;   // uniform value and address
+    }
+    if (a.bin_cost && perm) {
+        // scheduling hint for the next batch (sf_bin_hist): this wave's cycles, for the bin of its first
+        // packet (uniform value and address; bins with several waves keep the last one's)
+        const uint64_t cyc = __builtin_amdgcn_s_memtime() - c_start;
+        const uint32_t p0 = __builtin_amdgcn_readfirstlane(perm[wave * PPW]);
+        const uint32_t b = __builtin_amdgcn_readfirstlane(
+            packet_bin<PW>(a, K, draws, counter0, p0, a.bin_shift, a.bins_x));
+        // quantised to a power of 4: cost classes two octaves wide, so that bins of one class keep their
+        // index (screen) order and a wave straddling two bins still gets spatial neighbours
+        const uint32_t c32 = cyc > 0x7fffffffull ? 0x7fffffffu : ((uint32_t)cyc | 1u);
+        a.bin_cost[b] = 1u << ((31u - (uint32_t)__builtin_clz(c32)) & ~1u);
+    }
+    if ((a.flags & SF_FLAG_DIAG_UNITS) && a.tile_trace) {   // diagnostics: this wave's {start, end}
+        a.tile_trace[2u * wave] = w_start;
+        a.tile_trace[2u * wave + 1u] = __builtin_amdgcn_s_memrealtime();
     }
 }
 

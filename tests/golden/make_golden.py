@@ -150,6 +150,8 @@ PROGRESSIVE = {
     "p1": (64, 36, 0.25, 1, 3000),          # dense: every pixel overwritten many times
     "p2": (640, 360, 1.0, 12345, 100000),
     "p3": (1920, 1080, 0.25, 777, 200000),
+    "p4": (160, 90, 0.15, 4242, 6000),     # camera inside the root's bounding sphere: packets with t < 0
+    "p5": (320, 180, 0.2, 99, 20000),      # ... and deeper (LOD) levels
 }
 
 
@@ -182,6 +184,8 @@ SSE_CONFIGS = {
 SSE_PROGRESSIVE = {
     "ps1": (64, 36, 0.25, 1, 3000),
     "ps2": (640, 360, 1.0, 12345, 100000),
+    "ps3": (160, 90, 0.15, 4242, 6000),
+    "ps4": (320, 180, 0.2, 99, 20000),
 }
 
 

@@ -183,7 +183,7 @@ def test_gbuffer_initial_state_and_errors():
         assert e.value.code == sf.SF_EINVAL
 
 
-@pytest.mark.parametrize("name", ["p1", "p2", "p3"])
+@pytest.mark.parametrize("name", ["p1", "p2", "p3", "p4", "p5"])
 def test_progressive_matches_reference_worker(name):
     """Frame-less mode (Sphereflake.cpp:86-214): one reference worker's packet stream from mt19937(seed)
     -- Sobol pixel draws, 8-ray packets with packet-wide early-outs, sequential scatter."""
@@ -342,7 +342,7 @@ def test_sse_variant_config_frames_bit_exact(name):
     assert st.max_depth == fx["stats"]["max_depth"]
 
 
-@pytest.mark.parametrize("name", ["ps1", "ps2"])
+@pytest.mark.parametrize("name", ["ps1", "ps2", "ps3", "ps4"])
 def test_sse_variant_progressive_matches_reference_worker(name):
     """Frame-less mode of the SSE build: 4-ray packets on the 2x2 footprint (Sphereflake.cpp:115-138)."""
     fx = load_progressive(name)
