@@ -124,9 +124,10 @@ struct sf_ctx {
     uint32_t prog_cap = 0;             // packets the scratch buffers hold
     uint32_t* perm = nullptr;          // binned trace order of a batch (prog_cap)
     uint32_t* bin_cnt = nullptr;       // SF_PROG_MAX_BINS packet-bin counters / cursors
-    // frame-less heavy-first trace order (env SF_PROG_ORDER=0: bins in index order): per bin the cycles of
+    // frame-less heavy-first trace order (env SF_PROG_ORDER=1; default off: with the packet-mode leaf
+    // skip it measured 1-2 % slower, the longest waves no longer set the batch): per bin the cycles of
     // the last wave that started in it, its histogram per 64-bin chunk, and the bins' heavy-first rank
-    bool prog_order = true;
+    bool prog_order = false;
     uint32_t* bin_cost = nullptr;
     uint32_t* bin_rank = nullptr;
     uint32_t* bin_order = nullptr;

@@ -183,10 +183,12 @@ def test_gbuffer_initial_state_and_errors():
         assert e.value.code == sf.SF_EINVAL
 
 
-@pytest.mark.parametrize("name", ["p1", "p2", "p3", "p4", "p5"])
-def test_progressive_matches_reference_worker(name):
+@pytest.mark.parametrize("name,order", [("p1", "0"), ("p2", "0"), ("p3", "0"), ("p3", "1"), ("p4", "0"), ("p5", "0")])
+def test_progressive_matches_reference_worker(name, order, monkeypatch):
     """Frame-less mode (Sphereflake.cpp:86-214): one reference worker's packet stream from mt19937(seed)
-    -- Sobol pixel draws, 8-ray packets with packet-wide early-outs, sequential scatter."""
+    -- Sobol pixel draws, 8-ray packets with packet-wide early-outs, sequential scatter. p3 also with the
+    heavy-first bin order (SF_PROG_ORDER=1: its second, binned batch is ordered by the first's costs)."""
+    monkeypatch.setenv("SF_PROG_ORDER", order)
     fx = load_progressive(name)
     W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
     with sf.Sphereflake(W, H) as s:
