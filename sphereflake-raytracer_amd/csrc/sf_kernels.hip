@@ -1337,10 +1337,13 @@ extern "C" __global__ __launch_bounds__(256) void sf_trace_ray(FrameArgs a)
 // One workgroup; the twist runs in four dependency phases through LDS.
 extern "C" __global__ __launch_bounds__(1024) void sf_mt_draws(uint32_t* state, uint32_t* out, uint32_t n)
 {
-    __shared__ uint32_t s[624], t[624];
+    // Double-buffered twist in three dependency phases ([0, 227) from the old block; [227, 454) and
+    // [454, 623) + 623 from words just made: offsets 397 - 624 = -227 and 1 - 624): 3 barriers per
+    // 624 words, no copy-back. A tempered block is written while the next twist fills the other buffer.
+    __shared__ uint32_t buf[2][624];
     const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < 624u; i += blockDim.x) s[i] = state[i];
-    uint32_t pos = state[624];
+    for (uint32_t i = tid; i < 624u; i += blockDim.x) buf[0][i] = state[i];
+    uint32_t pos = state[624], cur = 0;
     __syncthreads();
     auto f = [](uint32_t a, uint32_t b, uint32_t c) {
         const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
@@ -1349,21 +1352,21 @@ extern "C" __global__ __launch_bounds__(1024) void sf_mt_draws(uint32_t* state, 
     uint32_t done = 0;
     while (done < n) {
         if (pos >= 624u) {
-            if (tid < 227u) t[tid] = f(s[tid], s[tid + 1], s[tid + 397]);
+            const uint32_t* sb = buf[cur];
+            uint32_t* tb = buf[cur ^ 1u];
+            if (tid < 227u) tb[tid] = f(sb[tid], sb[tid + 1u], sb[tid + 397u]);
             __syncthreads();
-            if (tid >= 227u && tid < 454u) t[tid] = f(s[tid], s[tid + 1], t[tid - 227]);
+            if (tid >= 227u && tid < 454u) tb[tid] = f(sb[tid], sb[tid + 1u], tb[tid - 227u]);
             __syncthreads();
-            if (tid >= 454u && tid < 623u) t[tid] = f(s[tid], s[tid + 1], t[tid - 227]);
+            if (tid >= 454u && tid < 623u) tb[tid] = f(sb[tid], sb[tid + 1u], tb[tid - 227u]);
+            else if (tid == 623u) tb[623] = f(sb[623], tb[0], tb[396]);
             __syncthreads();
-            if (tid == 623u) t[623] = f(s[623], t[0], t[396]);
-            __syncthreads();
-            if (tid < 624u) s[tid] = t[tid];
-            __syncthreads();
+            cur ^= 1u;
             pos = 0;
         }
         const uint32_t m = min(624u - pos, n - done);
         if (tid < m) {
-            uint32_t y = s[pos + tid];
+            uint32_t y = buf[cur][pos + tid];
             y ^= y >> 11;
             y ^= (y << 7) & 0x9d2c5680u;
             y ^= (y << 15) & 0xefc60000u;
@@ -1374,7 +1377,7 @@ extern "C" __global__ __launch_bounds__(1024) void sf_mt_draws(uint32_t* state, 
         done += m;
     }
     __syncthreads();
-    for (uint32_t i = tid; i < 624u; i += blockDim.x) state[i] = s[i];
+    for (uint32_t i = tid; i < 624u; i += blockDim.x) state[i] = buf[cur][i];
     if (tid == 0) state[624] = pos;
 }
 
