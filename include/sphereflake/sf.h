@@ -188,6 +188,23 @@ int sf_download_image(sf_ctx* ctx, uint8_t* rgba);
 /* The SSAO noise texture (SSAO.cpp:144-164): 64*64 RGBA32F texels into out[16384]. Host only. */
 int sf_ssao_noise(float* out);
 
+/* --- headless image dump ("a PPM/EXR dump for inspection") ------------ */
+/* The reference only shows its output in the GL window (main.cpp:306-330); a headless host (no GL)
+   inspects a frame through these files. Rows are written top row first (G-buffer row 0 = the top
+   edge, Sphereflake.cpp:186-196), so the picture reads the right way up in any viewer. */
+#define SF_DUMP_IMAGE         0   /* PPM (P6, 8-bit RGB) of the RGBA8 image of the last sf_post_process;
+                                     alpha dropped; SF_ESTATE before any post-process */
+#define SF_DUMP_NORMALS       1   /* PPM of the normal channel as clamp(0.5 n + 0.5) * 255, misses black */
+#define SF_DUMP_POSITIONS_PFM 2   /* PFM (little-endian float RGB, lossless) of the position channel (x, y, z) */
+#define SF_DUMP_NORMALS_PFM   3   /* PFM of the normal channel */
+/* Download the context's frame (synchronises) and write it to `path` as `what` (SF_DUMP_*). */
+int sf_save_image(sf_ctx* ctx, const char* path, int what);
+/* Host-only writers of the same formats: rgba = w*h*4 bytes; v4 = w*h float4 (w component dropped). */
+int sf_write_ppm(const char* path, uint32_t width, uint32_t height, const uint8_t* rgba);
+int sf_write_pfm(const char* path, uint32_t width, uint32_t height, const float* v4);
+/* Frame size of a context. */
+int sf_get_size(const sf_ctx* ctx, uint32_t* width, uint32_t* height);
+
 /* Device pointers of the context buffers (any out-pointer may be NULL). */
 int sf_device_buffers(sf_ctx* ctx, float** pos4, float** nrm4, float** min_t, uint32_t** hit_index);
 

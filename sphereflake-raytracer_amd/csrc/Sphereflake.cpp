@@ -59,6 +59,12 @@ void Sphereflake::Render(const sf_render_params* params)
     m_Stale = true;
 }
 
+void Sphereflake::SaveImage(const std::string& path, int what) const
+{
+    std::lock_guard<std::mutex> lk(m_Mutex);
+    Check(sf_save_image(m_Ctx, path.c_str(), what));
+}
+
 // Frame-less mode: like the reference's worker threads (seeded from time(NULL), Sphereflake.cpp:88-89),
 // a host thread keeps tracing batches of random packets into the persistent G-buffer.
 void Sphereflake::Initialize() { Initialize((uint32_t)time(NULL)); }
@@ -195,6 +201,8 @@ void SSAO::Render()
     }
     Check(sf_post_process(m_Flake.Context(), &m_Params, nullptr, nullptr, nullptr, nullptr));
 }
+
+void SSAO::SaveImage(const std::string& path) const { m_Flake.SaveImage(path, SF_DUMP_IMAGE); }
 
 const std::vector<uint8_t>& SSAO::GetImage() const
 {

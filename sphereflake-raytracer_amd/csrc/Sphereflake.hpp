@@ -77,6 +77,9 @@ public:
     void Render(const sf_render_params* params = nullptr);
 
     const GBuffer& GetGBuffer() const;
+    // Headless dump of the device frame (sf_save_image): SF_DUMP_NORMALS / _POSITIONS_PFM / _NORMALS_PFM,
+    // or SF_DUMP_IMAGE after an SSAO::Render(). The reference only shows its frame in the GL window.
+    void SaveImage(const std::string& path, int what = SF_DUMP_NORMALS) const;
 
     int GetMaxDepthReached() const;
     void ResetMaxDepthReached();
@@ -122,6 +125,7 @@ public:
 
     void Render();                                  // SSAO, blur x, blur y, final (asynchronous)
     const std::vector<uint8_t>& GetImage() const;   // D2H of the last Render's image
+    void SaveImage(const std::string& path) const;  // the last Render's image as a PPM
 
 private:
     Sphereflake& m_Flake;

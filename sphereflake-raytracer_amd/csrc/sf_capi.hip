@@ -349,6 +349,14 @@ const char* sf_strerror(int s)
 
 int sf_last_hip_error(const sf_ctx* ctx) { return ctx ? ctx->last_hip : 0; }
 
+int sf_get_size(const sf_ctx* ctx, uint32_t* width, uint32_t* height)
+{
+    if (!ctx) return SF_EINVAL;
+    if (width) *width = ctx->W;
+    if (height) *height = ctx->H;
+    return SF_OK;
+}
+
 int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
 {
     if (!out || width == 0 || height == 0) return SF_EINVAL;

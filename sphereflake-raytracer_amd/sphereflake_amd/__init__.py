@@ -70,6 +70,7 @@ SF_VARIANT_AVX = 0
 SF_VARIANT_SSE = 1
 SF_POST_GENERAL = 1
 SF_POST_UNIT_NORMALS = 2
+SF_DUMP_IMAGE, SF_DUMP_NORMALS, SF_DUMP_POSITIONS_PFM, SF_DUMP_NORMALS_PFM = 0, 1, 2, 3
 
 # exported symbol -> (restype, argtypes); checked against include/sphereflake/sf.h by the tests
 _F = ctypes.POINTER(ctypes.c_float)
@@ -96,6 +97,10 @@ SIGNATURES = {
                                        ctypes.c_void_p, ctypes.c_void_p]),
     "sf_download_image": (ctypes.c_int, [_CTX, ctypes.c_void_p]),
     "sf_ssao_noise": (ctypes.c_int, [_F]),
+    "sf_save_image": (ctypes.c_int, [_CTX, ctypes.c_char_p, ctypes.c_int]),
+    "sf_write_ppm": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
+    "sf_write_pfm": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
+    "sf_get_size": (ctypes.c_int, [_CTX, _U, _U]),
     "sf_host_register": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
     "sf_host_unregister": (ctypes.c_int, [ctypes.c_void_p]),
     "sf_device_buffers": (ctypes.c_int, [_CTX] + [ctypes.POINTER(ctypes.c_void_p)] * 4),
@@ -467,6 +472,12 @@ class Sphereflake:
         out = np.empty((64 * 64, 4), np.float32)
         _check(lib().sf_ssao_noise(_fp(out)), "sf_ssao_noise")
         return out
+
+    def save_image(self, path: str, what: int = SF_DUMP_NORMALS) -> None:
+        """Download this context's frame and write it as SF_DUMP_* (PPM of the post-processed image or
+        of the normals, PFM of positions / normals) through the C ABI's sf_save_image."""
+        with self._mutex:
+            _check(lib().sf_save_image(self._ctx, os.fsencode(path), int(what)), "sf_save_image", self._ctx)
 
     @staticmethod
     def save_ppm(path: str, rgb) -> None:

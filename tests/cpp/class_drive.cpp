@@ -15,6 +15,7 @@
 //   sf_progressive(seed, k * batch, batch) calls, which the test checks).
 #include <chrono>
 #include <cstdio>
+#include <string>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -107,6 +108,13 @@ int main(int argc, char** argv)
             if (!f) return 4;
             std::fwrite(img.data(), 1, img.size(), f);
             std::fclose(f);
+            if (argc > 18) {   // headless dumps (sf_save_image) under the prefix argv[18]
+                const std::string pre = argv[18];
+                ssao.SaveImage(pre + "_image.ppm");
+                flake.SaveImage(pre + "_normals.ppm");
+                flake.SaveImage(pre + "_pos.pfm", SF_DUMP_POSITIONS_PFM);
+                flake.SaveImage(pre + "_nrm.pfm", SF_DUMP_NORMALS_PFM);
+            }
         }
         flake.ResetRaysPerSecond();
         flake.ResetMaxDepthReached();

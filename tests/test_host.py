@@ -170,6 +170,28 @@ def test_save_ppm_layout(tmp_path):
     assert tuple(px[0, 0]) == (255, 128, 0) and tuple(px[1, 2]) == (255, 0, 64)
 
 
+def test_c_abi_ppm_pfm_writers(tmp_path):
+    """Host-only writers behind sf_save_image (sf.h image dump): P6 drops alpha and keeps rows top first;
+    PF writes little-endian float RGB rows bottom first; bad arguments are SF_EINVAL."""
+    L = sf.lib()
+    rgba = np.arange(2 * 3 * 4, dtype=np.uint8).reshape(2, 3, 4)
+    p = tmp_path / "a.ppm"
+    assert L.sf_write_ppm(str(p).encode(), 3, 2, rgba.ctypes.data) == 0
+    head = b"P6\n3 2\n255\n"
+    b = p.read_bytes()
+    assert b[:len(head)] == head and b[len(head):] == rgba[:, :, :3].tobytes()
+    v4 = np.random.default_rng(3).standard_normal((2, 3, 4)).astype(np.float32)
+    q = tmp_path / "a.pfm"
+    assert L.sf_write_pfm(str(q).encode(), 3, 2, v4.ctypes.data) == 0
+    head = b"PF\n3 2\n-1.0\n"
+    b = q.read_bytes()
+    assert b[:len(head)] == head
+    assert b[len(head):] == np.ascontiguousarray(v4[::-1, :, :3]).astype("<f4").tobytes()
+    assert L.sf_write_ppm(None, 3, 2, rgba.ctypes.data) == sf.SF_EINVAL
+    assert L.sf_write_pfm(str(q).encode(), 0, 2, v4.ctypes.data) == sf.SF_EINVAL
+    assert L.sf_save_image(None, str(q).encode(), sf.SF_DUMP_NORMALS) == sf.SF_EINVAL
+
+
 @pytest.mark.parametrize("c", [70.0, 60.0])
 def test_lod_threshold_exact_both_variants(c):
     """sqrtf(t/r) < C || t < 0  <=>  t < T for the AVX (70) and SSE (60, SIMD_SSE.h:21) constants."""
