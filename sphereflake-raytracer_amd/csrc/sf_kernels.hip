@@ -205,6 +205,8 @@ struct TraverseLds {
     }
 };
 
+template <bool B> struct BoolC { static constexpr bool value = B; };
+
 __device__ __forceinline__ void lds_fence()
 {
     __builtin_amdgcn_wave_barrier();
@@ -290,8 +292,11 @@ __device__ __forceinline__ void wave_atomic_add_u64(uint64_t* p, uint64_t v)
 __device__ __forceinline__ float4 depth_consts(const DeviceConsts* K, uint32_t d)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
+    // a 32-bit byte offset added to the table base: the scalar load takes it as its SGPR offset, with no
+    // 64-bit address arithmetic on the scalar unit per access
     typedef const __attribute__((address_space(4))) float4* ConstF4;
-    return ((ConstF4)(const void*)K->depth8)[2u * d];
+    typedef const __attribute__((address_space(4))) char* ConstC;
+    return *(ConstF4)((ConstC)(const void*)K->depth8 + (d << 5));
 #else
     return reinterpret_cast<const float4*>(K->depth8)[2u * d];   // host pass: never executed
 #endif
@@ -300,8 +305,9 @@ __device__ __forceinline__ float4 depth_consts(const DeviceConsts* K, uint32_t d
 __device__ __forceinline__ float depth_leaf(const DeviceConsts* K, uint32_t d)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
-    typedef const __attribute__((address_space(4))) float4* ConstF4;
-    return ((ConstF4)(const void*)K->depth8)[2u * d + 1u].x;
+    typedef const __attribute__((address_space(4))) float* ConstF;
+    typedef const __attribute__((address_space(4))) char* ConstC;
+    return *(ConstF)((ConstC)(const void*)K->depth8 + (d << 5) + 16u);
 #else
     return reinterpret_cast<const float4*>(K->depth8)[2u * d + 1u].x;
 #endif
@@ -418,21 +424,24 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
 
     uint32_t d = 0;                 // uniform: depth of the open (expanded) node
     uint32_t cN = 0;                // uniform: its index in the parent's table
-    uint32_t idxN = 0;              // uniform: its heap index mod 2^32 (root 0, child i of n: 9n+1+i)
+    uint32_t idxB = 1;              // uniform: 9 x its heap index + 1 mod 2^32 (root 0, child i of n: 9n+1+i),
+                                    // i.e. the heap index of its child 0
 
     // ---- the own sphere of a node (Sphereflake.h:174-224) with centre/|c|^2 `pc`, depth dd, heap index
     // idx, tested when the node opens. The reference tests it after the children (post-order) and
     // accepts strictly smaller t, so on an exact tie the earlier node in post-order wins. Pre-order
     // differs from post-order only for ancestor/descendant pairs, hence: a tie is accepted iff the
     // current best is an ancestor of this node (`anc`). Same result as the reference's order in every case.
-    // (actm: the lanes for which the node is visited)
-    auto self_test = [&](const float4 pc, uint32_t dd, uint64_t actm, uint32_t idx, float R2s) {
+    // (actm / actv: the lanes for which the node is visited, as a wave mask (packet semantics) and as a
+    // float, +inf on those lanes and -1 on the others (per-ray semantics: one v_min3 folds the visiting
+    // lanes into the hit compare, so the hit mask needs no scalar AND)
+    auto self_test = [&](const float4 pc, uint32_t dd, uint64_t actm, float actv, uint32_t idx, float R2s) {
         const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
         const float d2 = pc.w - tca * tca;
         const bool f0 = tca >= 0.0f, in = d2 <= R2s;
         uint64_t hsm;
         if constexpr (PACKET) hsm = actm & wave_ballot(group_any<PW>(f0) && group_any<PW>(in));
-        else hsm = actm & wave_ballot(f0) & wave_ballot(in);
+        else hsm = wave_ballot(__builtin_fminf(__builtin_fminf(tca, R2s - d2), actv) >= 0.0f);   // f0 && in (child loop)
         if (hsm) {
             const float ts = near_root(tca, d2, R2s);
             const uint64_t accm = hsm & (wave_ballot(ts < h.minT) | (wave_ballot(ts == h.minT) & ancm));
@@ -456,13 +465,17 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     // (the node's own sphere is tested by the caller when the node is entered, before this)
     // (act: the lanes visiting the node, as a per-lane bool for the packet semantics and as the wave mask actm)
     auto expand = [&](const float* node, const float* col, uint32_t cs, uint32_t d, bool act, uint64_t actm,
-                      uint32_t& pend) -> uint32_t {
+                      float actv, uint32_t& pend, uint32_t& leafm) -> uint32_t {
         d = __builtin_amdgcn_readfirstlane(d);   // wave-uniform: depth constants come by scalar loads
         lds_fence();
         const float4 pc = *reinterpret_cast<const float4*>(node);
         const float3 p0 = *reinterpret_cast<const float3*>(col);
         const float3 p1 = *reinterpret_cast<const float3*>(col + cs);
         const float3 p2 = *reinterpret_cast<const float3*>(col + 2u * cs);
+        // the wave's ray cone, read with the node (before this level's stores: the junk cc store below goes
+        // to the cone block, so a read after it would wait for a second LDS round trip)
+        const float4 cn = *reinterpret_cast<const float4*>(L.cone());
+        const float sinT = L.cone()[4];
         const float4 dtn = depth_consts(K, d);        // this node: (4/3) r
         const float4 dtc = depth_consts(K, d + 1u);   // children: (2r)^2, T
         // world = parent * child (SIMD_AVX.h:59-81), child translation scaled by (4/3) r (Sphereflake.h:162-172):
@@ -490,8 +503,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         // terms cover this test's own rounding (hardware sqrt). With beta < 45 deg and theta < 30 deg
         // every lane's phi stays in [beta, 180 - beta], which also covers the 8-lane packet tests.
         // Such a child changes nothing for any lane in the reference: skip it for the whole wave.
-        const float4 cn = *reinterpret_cast<const float4*>(L.cone());
-        const float ax = cn.x, ay = cn.y, az = cn.z, cosT = cn.w, sinT = L.cone()[4];
+        const float ax = cn.x, ay = cn.y, az = cn.z, cosT = cn.w;
         const float dl = w * 0x1p-18f;
         const float ca = (x * ax + y * ay) + z * az;
         const float qx = x - ca * ax, qy = y - ca * ay, qz = z - ca * az;
@@ -512,68 +524,87 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             // child i's {centre, cc}: a broadcast LDS read of plane 0 of the table just stored (one LDS
             // instruction instead of four v_readlane on the VALU); the deepest provisioned level keeps no
             // table, there the centre lanes are read back
-            const bool tab = d + 1u < levels;
-            const float* ctab = L.table(d);
-            while (M) {   // uniform loop over the children some lane can reach, in index order
-                const uint32_t i = __builtin_ctz(M);
-                M &= M - 1u;
-                SF_COUNT(1, 1);
-                float cx, cy, cz, cc;
-#ifndef SF_CHILD_READLANE
-                if (tab) {
-                    const float4 c4 = *reinterpret_cast<const float4*>(ctab + i * 4u);
-                    cx = c4.x, cy = c4.y, cz = c4.z, cc = c4.w;
-                } else
-#endif
-                {
-                    cx = readlane_f(x, 27u + i), cy = readlane_f(y, 27u + i);
-                    cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
-                }
-                const float tca = (cx * dx + cy * dy) + cz * dz;
-                const float d2 = cc - tca * tca;
-                const bool f0 = tca >= 0.0f, f1 = d2 <= R2b;
-                const uint64_t hbm = actm & wave_ballot(f0) & wave_ballot(f1);   // bounding (SIMD_AVX.h:247-258)
+            // (the loop is instantiated twice, for the LDS and the readlane centres, so the choice is not
+            // re-tested in every iteration)
+            // actv (+inf on the lanes visiting the node, -1 on the others): ONE v_min3 + compare gives the
+            // bounding mask already restricted to the visiting lanes, and the loop branches on it (VCC)
+            // without scalar mask algebra
+            auto child_loop = [&](auto tab) {
+                const float* ctab = L.table(d);
+                while (M) {   // uniform loop over the children some lane can reach, in index order
+                    const uint32_t i = __builtin_ctz(M);
+                    M &= ~(1u << i);
+                    SF_COUNT(1, 1);
+                    float cx, cy, cz, cc;
+                    if constexpr (decltype(tab)::value) {
+                        const float4 c4 = *reinterpret_cast<const float4*>(ctab + i * 4u);
+                        cx = c4.x, cy = c4.y, cz = c4.z, cc = c4.w;
+                    } else {
+                        cx = readlane_f(x, 27u + i), cy = readlane_f(y, 27u + i);
+                        cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
+                    }
+                    const float tca = (cx * dx + cy * dy) + cz * dz;
+                    const float d2 = cc - tca * tca;
+                    // bounding (SIMD_AVX.h:247-258): tca >= 0 && d2 <= R2b as ONE compare, min(tca, R2b - d2) >= 0:
+                    // with denormals kept, fl(R2b - d2) >= 0 exactly when d2 <= R2b (no NaN operands here)
+                    const float xs = R2b - d2;
+                    const uint64_t hbm = wave_ballot(__builtin_fminf(__builtin_fminf(tca, xs), actv) >= 0.0f);
 #ifdef SF_EXP_PAD   // experiment builds only: independent VALU filler per child iteration (issue-bound test)
-                {
-                    float pad = dx;
+                    {
+                        float pad = dx;
 #pragma unroll
-                    for (int k_ = 0; k_ < SF_EXP_PAD; ++k_) __asm__ volatile("v_mov_b32 %0, %0" : "+v"(pad));
-                }
+                        for (int k_ = 0; k_ < SF_EXP_PAD; ++k_) __asm__ volatile("v_mov_b32 %0, %0" : "+v"(pad));
+                    }
 #endif
-                SF_COUNT(5, __builtin_popcountll(actm));
-                SF_COUNT(6, __builtin_popcountll(hbm));
-                SF_COUNT(10, d >= 4u ? 1 : 0);
-                SF_COUNT(11, d >= 4u ? __builtin_popcountll(actm) : 0);
-                SF_COUNT(12, __builtin_popcountll(actm) <= 4 ? 1 : 0);
-                SF_COUNT(13, __builtin_popcountll(actm) <= 16 ? 1 : 0);
-                SF_COUNT(14, __builtin_popcountll(actm) <= 32 ? 1 : 0);
-                if (hbm == 0ull) {
-                    SF_COUNT(2, 1);
-                    continue;
+#ifdef SF_EXP_SPAD  // experiment builds only: SALU filler per child iteration (scalar-unit-bound test)
+                    {
+                        uint32_t spad = i;
+#pragma unroll
+                        for (int k_ = 0; k_ < SF_EXP_SPAD; ++k_) __asm__ volatile("s_add_u32 %0, %0, 1" : "+s"(spad)::"scc");
+                    }
+#endif
+                    SF_COUNT(5, __builtin_popcountll(actm));
+                    SF_COUNT(6, __builtin_popcountll(hbm));
+                    SF_COUNT(10, d >= 4u ? 1 : 0);
+                    SF_COUNT(11, d >= 4u ? __builtin_popcountll(actm) : 0);
+                    SF_COUNT(12, __builtin_popcountll(actm) <= 4 ? 1 : 0);
+                    SF_COUNT(13, __builtin_popcountll(actm) <= 16 ? 1 : 0);
+                    SF_COUNT(14, __builtin_popcountll(actm) <= 32 ? 1 : 0);
+                    if (hbm == 0ull) {
+                        SF_COUNT(2, 1);
+                        continue;
+                    }
+                    // LOD on t = fl(tca - sqrt_rn(R2b - d2)) (SIMD_AVX.h:260-267; t0 <= t1 picks t1 for
+                    // thc >= 0). Fast bracket: the hardware sqrt is within 2 ulp of sqrt_rn and t is
+                    // monotone in it, so t_lo = fl(tca - (s + 2ulp)) <= t <= t_hi = fl(tca - (s - 2ulp)):
+                    // t_hi < T decides "expands", t_lo >= T decides "does not"; the exact path runs only
+                    // for lanes in between (or with a tiny sqrt argument).
+                    const float sq = __builtin_amdgcn_sqrtf(xs);
+                    const float s_lo = __uint_as_float((uint32_t)max((int32_t)__float_as_uint(sq) - 2, 0));
+                    const float s_hi = __uint_as_float(__float_as_uint(sq) + 2u);
+                    const float t_hi = tca - s_lo;
+                    const float t_lo = tca - s_hi;
+                    const bool yes = t_hi < T, maybe = t_lo < T, tiny = xs < 0x1p-96f;
+                    const uint64_t tinym = wave_ballot(tiny);
+                    uint64_t exm = hbm & wave_ballot(yes) & ~tinym;
+                    const uint64_t undm = hbm & ((wave_ballot(maybe) & ~wave_ballot(yes)) | tinym);
+                    if (undm) {   // rare: exact IEEE root for the undecided lanes
+                        const float te = near_root_exact(tca, d2, R2b);
+                        exm = (exm & ~undm) | (undm & wave_ballot(te < T));
+                    }
+                    sel_in_place(e, e | (1u << i), exm);   // the lanes of exm get bit i
+                    if (exm != 0ull) pm |= 1u << i;
+                    SF_COUNT(3, exm != 0ull ? 1 : 0);
                 }
-                // LOD on t = fl(tca - sqrt_rn(R2b - d2)) (SIMD_AVX.h:260-267; t0 <= t1 picks t1 for
-                // thc >= 0). Fast bracket: the hardware sqrt is within 2 ulp of sqrt_rn and t is
-                // monotone in it, so t_lo = fl(tca - (s + 2ulp)) <= t <= t_hi = fl(tca - (s - 2ulp)):
-                // t_hi < T decides "expands", t_lo >= T decides "does not"; the exact path runs only
-                // for lanes in between (or with a tiny sqrt argument).
-                const float xs = R2b - d2;
-                const float sq = __builtin_amdgcn_sqrtf(xs);
-                const float s_lo = __uint_as_float((uint32_t)max((int32_t)__float_as_uint(sq) - 2, 0));
-                const float s_hi = __uint_as_float(__float_as_uint(sq) + 2u);
-                const float t_hi = tca - s_lo;
-                const float t_lo = tca - s_hi;
-                const bool yes = t_hi < T, maybe = t_lo < T, tiny = xs < 0x1p-96f;
-                const uint64_t tinym = wave_ballot(tiny);
-                uint64_t exm = hbm & wave_ballot(yes) & ~tinym;
-                const uint64_t undm = hbm & ((wave_ballot(maybe) & ~wave_ballot(yes)) | tinym);
-                if (undm) {   // rare: exact IEEE root for the undecided lanes
-                    const float te = near_root_exact(tca, d2, R2b);
-                    exm = (exm & ~undm) | (undm & wave_ballot(te < T));
+                // children of a node at the deepest provisioned level (no table) would need a level that does
+                // not exist: flag the tile for the deeper re-trace instead of entering them
+                if constexpr (!decltype(tab)::value) {
+                    if (pm != 0u) overflowed = true;
+                    pm = 0u;
                 }
-                sel_in_place(e, e | (1u << i), exm);   // the lanes of exm get bit i
-                if (exm != 0ull) pm |= 1u << i;
-                SF_COUNT(3, exm != 0ull ? 1 : 0);
-            }
+            };
+            if (d + 1u < levels) child_loop(BoolC<true>{});
+            else child_loop(BoolC<false>{});
         } else {
             // Packet semantics (frame-less mode): early-outs over the 8 lanes of a reference packet.
             while (M) {
@@ -600,8 +631,15 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                     pm |= (mi != 0ull ? 1u : 0u) << i;
                 }
             }
+            if (d + 1u >= levels) {   // (as in the per-ray loop without a table)
+                if (pm != 0u) overflowed = true;
+                pm = 0u;
+            }
         }
         pend = pm;
+        // children none of whose own children can pass LOD for any ray (sfhost::leaf_threshold of their depth;
+        // |c|^2 of child i is w on lane 27 + i): entered as inline leaves
+        leafm = lod_cull ? (uint32_t)(wave_ballot(w > depth_leaf(K, d + 1u)) >> 27) & 0x1ffu : 0u;
         return e;
     };
 
@@ -609,41 +647,42 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     // Lane selects: no LDS traffic and no lane-0-only region in the loop.
     uint32_t stk_pc = 0u, stk_ix = 0u;
     uint32_t pend = 0u, eN = 0u;
+    uint32_t leafN = 0u;            // uniform: the open node's children that are inline leaves (bit i: child i)
     {
         // the root: its own sphere, then -- unless no child of it can pass LOD for any ray
         // (sfhost::leaf_threshold; per-ray semantics only) -- its children
         lds_fence();
         const float4 pc = *reinterpret_cast<const float4*>(L.root());
-        self_test(pc, 0u, wave_ballot(ex0), 0u, depth_consts(K, 0u).y);
+        const float av0 = ex0 ? __builtin_inff() : -1.0f;
+        self_test(pc, 0u, wave_ballot(ex0), av0, 0u, depth_consts(K, 0u).y);
         if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u))) &&
               leaf_front(pc, depth_consts(K, 0u).x)))
-            eN = expand(L.root(), L.root() + 4u, 4u, 0u, ex0, wave_ballot(ex0), pend);
+            eN = expand(L.root(), L.root() + 4u, 4u, 0u, ex0, wave_ballot(ex0), av0, pend, leafN);
         else SF_COUNT(4, 1);
     }
 
     for (;;) {
         d = __builtin_amdgcn_readfirstlane(d);
-        pend = __builtin_amdgcn_readfirstlane(pend);
         SF_STAMP(0);
         if (pend) {
             const uint32_t c = __builtin_ctz(pend);
-            pend &= pend - 1u;
-            if (d + 1u >= levels) {        // needs a deeper stack than provisioned: flag the tile
-                overflowed = true;
-                continue;
-            }
-            const bool a = ((eN >> c) & 1u) != 0u;
+            const uint32_t cbit = 1u << c;
+            pend &= ~cbit;
+            // (d + 1 < levels here: expand never leaves children pending at the deepest provisioned level)
+            const bool a = (eN & cbit) != 0u;
             const uint64_t am = wave_ballot(a);
+            const float av = a ? __builtin_inff() : -1.0f;
             const float* node = L.table(d) + c * 4u;
             // enter child c: its own sphere first (pre-order, see self_test), in one place for every child
             lds_fence();
             const float4 pc = *reinterpret_cast<const float4*>(node);
+            const float4 dc1 = depth_consts(K, d + 1u);
             maxd = (int32_t)d + 1 > maxd ? (int32_t)d + 1 : maxd;   // Sphereflake.h:157-160
-            self_test(pc, d + 1u, am, 9u * idxN + 1u + c, depth_consts(K, d + 1u).y);
+            self_test(pc, d + 1u, am, av, idxB + c, dc1.y);
             // A child none of whose children can pass LOD for any ray (sfhost::leaf_threshold) only needs its
-            // own sphere: no push, no level, no child build.
-            if (lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, d + 1u))) &&
-                leaf_front(pc, depth_consts(K, d + 1u).x)) {
+            // own sphere: no push, no level, no child build. (leafN: decided for all 9 children when the parent
+            // expanded)
+            if ((leafN & cbit) != 0u && leaf_front(pc, dc1.x)) {
                 SF_COUNT(4, 1);
                 SF_COUNT(8, 1);
                 SF_COUNT(9, __builtin_popcountll(am));
@@ -651,14 +690,14 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 continue;
             }
             // save the open node's state, enter child c
-            stk_pc = writelane_u(pend | (cN << 16), d, stk_pc);
-            stk_ix = writelane_u(idxN, d, stk_ix);
+            stk_pc = writelane_u(pend | (cN << 16) | (leafN << 20), d, stk_pc);
+            stk_ix = writelane_u(idxB, d, stk_ix);
             L.E(d)[lane] = (uint16_t)eN;
-            idxN = 9u * idxN + 1u + c;
+            idxB = 9u * (idxB + c) + 1u;
             cN = c;
             d += 1u;
             SF_STAMP(1);
-            eN = expand(node, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, a, am, pend);
+            eN = expand(node, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, a, am, av, pend, leafN);
             SF_STAMP(2);
             continue;
         }
@@ -672,8 +711,9 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         {
             const uint32_t pc = __builtin_amdgcn_readlane(stk_pc, d);
             pend = pc & 0xffffu;
-            cN = pc >> 16;
-            idxN = (uint32_t)__builtin_amdgcn_readlane(stk_ix, d);
+            cN = (pc >> 16) & 0xfu;
+            leafN = pc >> 20;
+            idxB = (uint32_t)__builtin_amdgcn_readlane(stk_ix, d);
         }
         eN = L.E(d)[lane];
         (void)__builtin_amdgcn_readfirstlane(eN);   // (stamp builds: close the pop segment after its reads)
