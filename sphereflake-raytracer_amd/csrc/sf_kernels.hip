@@ -133,6 +133,14 @@ __device__ __forceinline__ float wave_min(float v)
 // Wave64 ballot straight on the compare mask (no bool -> int -> compare round trip).
 __device__ __forceinline__ uint64_t wave_ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
+// (lane in m) ? b : a -- one v_cndmask on an SGPR lane mask (a wave ballot), no per-lane bool
+__device__ __forceinline__ float sel_mask(float a, float b, uint64_t m)
+{
+    float r;
+    __asm__("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+
 // dst = (lane in m) ? src : dst, in dst's own register (tied operand): one v_cndmask on an SGPR lane
 // mask, no per-lane bool materialised and no copy between a pre- and a post-update register
 __device__ __forceinline__ void sel_in_place(float& dst, float src, uint64_t m)
@@ -548,7 +556,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                     // bounding (SIMD_AVX.h:247-258): tca >= 0 && d2 <= R2b as ONE compare, min(tca, R2b - d2) >= 0:
                     // with denormals kept, fl(R2b - d2) >= 0 exactly when d2 <= R2b (no NaN operands here)
                     const float xs = R2b - d2;
-                    const uint64_t hbm = wave_ballot(__builtin_fminf(__builtin_fminf(tca, xs), actv) >= 0.0f);
+                    const bool hb = __builtin_fminf(__builtin_fminf(tca, xs), actv) >= 0.0f;
+                    const uint64_t hbm = wave_ballot(hb);
 #ifdef SF_EXP_PAD   // experiment builds only: independent VALU filler per child iteration (issue-bound test)
                     {
                         float pad = dx;
@@ -584,13 +593,21 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                     const float s_hi = __uint_as_float(__float_as_uint(sq) + 2u);
                     const float t_hi = tca - s_lo;
                     const float t_lo = tca - s_hi;
-                    const bool yes = t_hi < T, maybe = t_lo < T, tiny = xs < 0x1p-96f;
-                    const uint64_t tinym = wave_ballot(tiny);
-                    uint64_t exm = hbm & wave_ballot(yes) & ~tinym;
-                    const uint64_t undm = hbm & ((wave_ballot(maybe) & ~wave_ballot(yes)) | tinym);
-                    if (undm) {   // rare: exact IEEE root for the undecided lanes
+                    // The decision as per-lane values instead of scalar mask algebra: th / tl are t_hi / t_lo on
+                    // the lanes with a bounding hit and +inf elsewhere; a tiny sqrt argument makes the bracket
+                    // (-inf, +inf), i.e. undecided. expands: th < T; undecided: tl < T <= th.
+                    const uint64_t tinym = wave_ballot(xs < 0x1p-96f);
+                    // (the tiny select is opaque asm, so the hb select below stays one v_cndmask on the VCC of the
+                    // bounding compare instead of being merged into scalar mask algebra)
+                    const float thx = sel_mask(t_hi, __builtin_inff(), tinym);
+                    const float tlx = sel_mask(t_lo, -__builtin_inff(), tinym);
+                    const float th = hb ? thx : __builtin_inff();
+                    const float tl = hb ? tlx : __builtin_inff();
+                    uint64_t exm = wave_ballot(th < T);
+                    const uint64_t undm = wave_ballot(sel_mask(tl, __builtin_inff(), exm) < T);
+                    if (undm) {   // rare: exact IEEE root for the undecided lanes (disjoint from exm)
                         const float te = near_root_exact(tca, d2, R2b);
-                        exm = (exm & ~undm) | (undm & wave_ballot(te < T));
+                        exm |= undm & wave_ballot(te < T);
                     }
                     sel_in_place(e, e | (1u << i), exm);   // the lanes of exm get bit i
                     if (exm != 0ull) pm |= 1u << i;
