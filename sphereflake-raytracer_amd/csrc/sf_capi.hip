@@ -185,6 +185,8 @@ struct sf_ctx {
     hipStream_t last_stream = nullptr; // stream of the latest enqueued work (nullptr: the context stream)
     hipEvent_t join_ev = nullptr;      // recorded on last_stream when a call switches streams
     bool use_order = true;             // env SF_ORDER=0: row-major order always
+    uint32_t order_every = 1;          // env SF_ORDER_EVERY = k: rebuild the order after every k-th render only
+    uint32_t order_phase = 0;          // renders since the last rebuild
     // Measurement: HIP events around the main trace kernel of each render (sf_set_kernel_timing)
     static constexpr int kTimed = 64;
     hipEvent_t ev[kTimed][2] = {};
@@ -385,6 +387,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     }
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_ORDER")) c->use_order = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_ORDER_EVERY")) c->order_every = std::atoi(ev) > 1 ? (uint32_t)std::atoi(ev) : 1u;
     if (const char* ev = std::getenv("SF_PROG_BIN")) c->prog_bin = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_PREFETCH")) c->prog_prefetch = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_ADAPT")) c->prog_adapt = std::atoi(ev) != 0;
@@ -621,9 +624,13 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             if (nblk > need) nblk = need;
             if (c->max_blocks && nblk > c->max_blocks) nblk = c->max_blocks;
             const dim3 grid(nblk);
+            // the order is rebuilt after every order_every-th render (and whenever none exists for this frame
+            // size); the renders in between keep the last order and record their tile costs only
+            const bool rebuild = c->use_order && (c->order_n != ntiles || c->order_phase + 1u >= c->order_every);
+            if (c->use_order) c->order_phase = rebuild ? 0u : c->order_phase + 1u;
             if (c->use_order) {
                 a.tile_cost = c->tile_cost;
-                a.chunk_cnt = c->chunk_cnt;
+                a.chunk_cnt = rebuild ? c->chunk_cnt : nullptr;
                 a.part_cost = c->part_cost;
                 a.part_done = c->part_done;
                 a.tile_order = c->order_n == ntiles ? c->tile_order : nullptr;   // ordered by ctx_join
@@ -641,7 +648,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 c->ev_next = (c->ev_next + 1u) % sf_ctx::kTimed;
                 c->ev_count = c->ev_count < (uint32_t)sf_ctx::kTimed ? c->ev_count + 1u : c->ev_count;
             }
-            if (c->use_order) {   // the next render's tile order, from this render's tile costs
+            if (rebuild) {   // the next render's tile order, from this render's tile costs
                 const uint32_t nc = (ntiles + 63u) / 64u;
                 const uint32_t waves = nblk * wpb;   // resident waves of the persistent grid
                 const uint32_t spare = waves > ntiles ? waves - ntiles : 0u;

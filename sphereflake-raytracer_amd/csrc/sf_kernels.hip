@@ -933,8 +933,10 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
         }
         if (last) {
             a.tile_cost[tile] = cost;
-            const uint32_t slot = __builtin_amdgcn_readfirstlane((tile >> 6) * SF_ORDER_BUCKETS + cost_bucket(cost));
-            wave_atomic_inc_nowait(a.chunk_cnt + slot);
+            if (a.chunk_cnt) {   // (renders that rebuild the order: the histogram for sf_order_scan)
+                const uint32_t slot = __builtin_amdgcn_readfirstlane((tile >> 6) * SF_ORDER_BUCKETS + cost_bucket(cost));
+                wave_atomic_inc_nowait(a.chunk_cnt + slot);
+            }
         }
     }
     if (!FIXUP && overflowed) {
