@@ -431,7 +431,6 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     const uint32_t slot = bc == 3u ? bi * 4u : SF_LDS_PLANE + bc * SF_LDS_COLS + bi * 3u;
 
     uint32_t d = 0;                 // uniform: depth of the open (expanded) node
-    uint32_t cN = 0;                // uniform: its index in the parent's table
     uint32_t idxB = 1;              // uniform: 9 x its heap index + 1 mod 2^32 (root 0, child i of n: 9n+1+i),
                                     // i.e. the heap index of its child 0
 
@@ -486,6 +485,9 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         const float sinT = L.cone()[4];
         const float4 dtn = depth_consts(K, d);        // this node: (4/3) r
         const float4 dtc = depth_consts(K, d + 1u);   // children: (2r)^2, T
+        // children's leaf threshold (+inf: no inline leaves when the LOD cull is off), loaded with the others
+        const float leaf1 = depth_leaf(K, d + 1u);
+        const float leafc = lod_cull ? leaf1 : __builtin_inff();
         // world = parent * child (SIMD_AVX.h:59-81), child translation scaled by (4/3) r (Sphereflake.h:162-172):
         // column 3 lanes multiply b0..b2 by s, the others by 1 (exact)
         const float sm = bc == 3u ? dtn.z : 1.0f;
@@ -518,8 +520,10 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         const float sq = __builtin_amdgcn_sqrtf((qx * qx + qy * qy) + qz * qz);
         const float lhs = sq * cosT - ca * sinT;
         const float rhs = __builtin_amdgcn_sqrtf(R2b + dl) * (1.0f + 0x1p-18f) + (ca + sq) * 0x1p-18f;
-        const uint64_t skip = wave_ballot(ca > 0.0f) & wave_ballot(w > 2.0f * (R2b + dl)) & wave_ballot(lhs > rhs);
-        uint32_t M = (uint32_t)(~skip >> 27) & 0x1ffu;
+        // skip = ca > 0 && w > 2 (R2b + dl) && lhs > rhs, as ONE compare of a v_min3 (with denormals kept,
+        // a > b exactly when fl(a - b) > 0; every operand is finite): the kept children straight from a ballot
+        const float mk = __builtin_fminf(__builtin_fminf(ca, w - 2.0f * (R2b + dl)), lhs - rhs);
+        uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 27) & 0x1ffu;
         M = __builtin_amdgcn_readfirstlane(M);
         SF_STAMP(6);
         uint32_t e = 0, pm = 0;
@@ -656,7 +660,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         pend = pm;
         // children none of whose own children can pass LOD for any ray (sfhost::leaf_threshold of their depth;
         // |c|^2 of child i is w on lane 27 + i): entered as inline leaves
-        leafm = lod_cull ? (uint32_t)(wave_ballot(w > depth_leaf(K, d + 1u)) >> 27) & 0x1ffu : 0u;
+        leafm = (uint32_t)(wave_ballot(w > leafc) >> 27) & 0x1ffu;
         return e;
     };
 
@@ -707,11 +711,10 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 continue;
             }
             // save the open node's state, enter child c
-            stk_pc = writelane_u(pend | (cN << 16) | (leafN << 20), d, stk_pc);
+            stk_pc = writelane_u(pend | (leafN << 16), d, stk_pc);
             stk_ix = writelane_u(idxB, d, stk_ix);
             L.E(d)[lane] = (uint16_t)eN;
             idxB = 9u * (idxB + c) + 1u;
-            cN = c;
             d += 1u;
             SF_STAMP(1);
             eN = expand(node, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, a, am, av, pend, leafN);
@@ -728,8 +731,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         {
             const uint32_t pc = __builtin_amdgcn_readlane(stk_pc, d);
             pend = pc & 0xffffu;
-            cN = (pc >> 16) & 0xfu;
-            leafN = pc >> 20;
+            leafN = pc >> 16;
             idxB = (uint32_t)__builtin_amdgcn_readlane(stk_ix, d);
         }
         eN = L.E(d)[lane];
