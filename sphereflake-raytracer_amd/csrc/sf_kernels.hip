@@ -877,10 +877,17 @@ __device__ __forceinline__ uint32_t part_axis_lane(uint32_t part)
     return (2u + 4u * (q >> 1)) * 8u + 2u + 4u * (q & 1u);
 }
 
-template <bool FIXUP>
+struct NoPrefetch {
+    __device__ void operator()() const {}
+};
+
+// `pre` runs right after the traversal, before the tile's shading and stores: the persistent kernel takes
+// its next queue ticket there, so the atomic's round trip overlaps the shading instead of following the
+// G-buffer stores (whose completion a later wait would otherwise include: vmcnt counts in order).
+template <bool FIXUP, class Prefetch = NoPrefetch>
 __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __restrict__ L, uint32_t tile,
                                                 uint32_t levels, uint32_t* overflow_list, uint32_t* overflow_count,
-                                                uint32_t part = 0u)
+                                                uint32_t part = 0u, const Prefetch& pre = Prefetch())
 {
     const DeviceConsts* __restrict__ K = a.consts;
     const uint32_t lane = threadIdx.x & 63u;
@@ -897,6 +904,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     uint64_t tile_counts = 0;
     traverse<0>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed, a.flags,
                     FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
+    pre();
     if (!FIXUP && a.tile_trace) {
         // diagnostics only: never read by the kernel, never feeds an output value. Every lane stores
         // the same (uniform) words: no lane-0-only region.
@@ -1065,17 +1073,10 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 #else
         at = a;
 #endif
-        uint32_t g;                // position in the render's unit order
-        if (first != ~0u) {
-            g = first;
-            first = ~0u;
-            if (g >= nunits) break;   // (then the queues are empty too)
-        } else {
-            // (an agent-coherent load of the queue word before the atomic, to skip dry queues, made
-            // the frame 1.7x slower: it contends with the atomics on the line)
-            g = nwaves + wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u) * nq + k;   // uniform
-            if (g >= nunits) break;   // the XCD's queue is empty
-        }
+        // position in the render's unit order: the static first unit, then the ticket the previous tile
+        // took after its traversal (past the end: the XCD's queue is empty)
+        const uint32_t g = first;
+        if (g >= nunits) break;
         uint32_t t = g, part = 0u;
         if (at.tile_order) {      // heaviest tiles of the previous render first (scalar load)
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1101,7 +1102,14 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
             else __builtin_amdgcn_s_setprio(0);
         }
         const uint64_t u_start = (at.flags & SF_FLAG_DIAG_UNITS) ? __builtin_amdgcn_s_memrealtime() : 0ull;
-        const TileStats st = trace_tile<false>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity, part);
+        // the next unit's ticket, taken when this tile's traversal ends (see trace_tile)
+        // (an agent-coherent load of the queue word before the atomic, to skip dry queues, made the frame
+        // 1.7x slower: it contends with the atomics on the line)
+        auto ticket = [&]() {
+            first = nwaves + wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u) * nq + k;   // uniform
+        };
+        const TileStats st = trace_tile<false>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity, part,
+                                               ticket);
         if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace) {   // diagnostics only (uniform words)
             uint64_t* ut = at.tile_trace + 3u * (at.tiles_x * at.tile_rows) + SF_DIAG_SLOTS + 3u * g;
             ut[0] = u_start;
