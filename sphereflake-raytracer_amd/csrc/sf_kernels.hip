@@ -628,11 +628,21 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             else child_loop(BoolC<false>{});
         } else {
             // Packet semantics (frame-less mode): early-outs over the 8 lanes of a reference packet.
+            // (child centres from the LDS table by broadcast reads where the level has one, as in the per-ray
+            // loop; the loop is instantiated for both sources)
+            auto packet_loop = [&](auto tab) {
+            const float* ctab = L.table(d);
             while (M) {
                 const uint32_t i = __builtin_ctz(M);
                 M &= M - 1u;
-                const float cx = readlane_f(x, 27u + i), cy = readlane_f(y, 27u + i);
-                const float cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
+                float cx, cy, cz, cc;
+                if constexpr (decltype(tab)::value) {
+                    const float4 c4 = *reinterpret_cast<const float4*>(ctab + i * 4u);
+                    cx = c4.x, cy = c4.y, cz = c4.z, cc = c4.w;
+                } else {
+                    cx = readlane_f(x, 27u + i), cy = readlane_f(y, 27u + i);
+                    cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
+                }
                 const float tca = (cx * dx + cy * dy) + cz * dz;
                 const float d2 = cc - tca * tca;
                 const bool hb = act & group_any<PW>(tca >= 0.0f) & group_any<PW>(d2 <= R2b);
@@ -652,6 +662,9 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                     pm |= (mi != 0ull ? 1u : 0u) << i;
                 }
             }
+            };
+            if (d + 1u < levels) packet_loop(BoolC<true>{});
+            else packet_loop(BoolC<false>{});
             if (d + 1u >= levels) {   // (as in the per-ray loop without a table)
                 if (pm != 0u) overflowed = true;
                 pm = 0u;
