@@ -290,6 +290,32 @@ def test_repeat_renders_heavy_first_order_bit_exact():
     assert st.max_depth == fx["stats"]["max_depth"] and st.overflow_tiles == 0
 
 
+@pytest.mark.parametrize("every", ["2", "3"])
+def test_order_rebuilt_every_kth_render_bit_exact(monkeypatch, every):
+    """SF_ORDER_EVERY=k: renders between two order rebuilds record tile costs without the histogram and
+    keep the last order (sf_capi.hip `rebuild`). Every render still equals the golden c2 frame, the kept
+    order stays a valid permutation of the tiles, and a rebuild after skipped renders gives the order of
+    the costs it was built from (no histogram counts carried over from the skipped renders)."""
+    monkeypatch.setenv("SF_ORDER_EVERY", every)
+    fx = load_frame("c2")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    n = ((W + 7) // 8) * ((H + 7) // 8)
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for k in range(2 * int(every) + 2):
+            s.Render()
+            pos, nrm, _, _ = s.download()
+            assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == [], f"render {k}"
+            units, cost = s.tile_order()
+            tiles = units & ((1 << 29) - 1)
+            assert np.array_equal(np.unique(tiles), np.arange(n)), f"render {k}: order is not a permutation"
+            if k % int(every) == 0:   # a rebuild render (0, k, 2k, ...): the order of its own costs
+                assert len(units) == n   # (14 400 tiles > the persistent grid's waves: no splits)
+                assert np.array_equal(units, expected_units(cost, None, 0)[0]), f"render {k}"
+        st = s.stats()
+    assert st.max_depth == fx["stats"]["max_depth"]
+
+
 def test_camera_inside_bounding_ball_uses_fixup_levels():
     """K = 0.2 puts the camera inside the flake's bounding ball: no geometric level bound, so the
     adaptive levels and the overflow re-trace path carry the frame (c5's camera on a small frame)."""
