@@ -112,7 +112,8 @@ struct sf_ctx {
     bool persistent = true;                      // tuning knob: env SF_PERSISTENT=0 -> one workgroup per tile group
     uint32_t flags = 0;                          // SF_FLAG_* A/B switches: env SF_FLAGS
     int cus = 256;
-    uint32_t queues = SF_QUEUES;                 // persistent trace: tile queues, one per XCD (power of 2)
+    uint32_t queues = 8;                         // persistent trace: XCD queue groups, one per XCD (power of 2)
+    uint32_t queues_per_xcd = 1;                 // env SF_QUEUES_PER_XCD = 1 | 2 | 4: tile queues per XCD
     uint32_t prio_buckets = 6;                   // top cost buckets (3 octaves) traced at raised wave priority (env SF_PRIO_BUCKETS)
     int occ_key = -1, occ_blocks = 0;            // cached occupancy (waves per block, levels) -> blocks per CU
     uint32_t max_blocks = 0;                     // diagnostics: env SF_MAX_BLOCKS caps the persistent grid
@@ -378,11 +379,15 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     c->cus = prop.multiProcessorCount;
     {   // gfx950: 32 CUs per XCD; a compute partition of the chip exposes fewer XCDs (then fewer queues)
         uint32_t x = c->cus >= 32 ? (uint32_t)c->cus / 32u : 1u, q = 1u;
-        while (q * 2u <= x && q * 2u <= SF_QUEUES) q *= 2u;
+        while (q * 2u <= x && q * 2u <= 8u) q *= 2u;
         c->queues = q;
         if (const char* ev = std::getenv("SF_NQUEUES")) {
             const int v = std::atoi(ev);
             if (v == 1 || v == 2 || v == 4 || v == 8) c->queues = (uint32_t)v;
+        }
+        if (const char* ev = std::getenv("SF_QUEUES_PER_XCD")) {
+            const int v = std::atoi(ev);
+            if (v == 1 || v == 2 || v == 4) c->queues_per_xcd = (uint32_t)v;
         }
     }
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
@@ -518,7 +523,8 @@ static FrameArgs frame_args(const sf_ctx* c)
     a.consts = c->consts;
     a.stats = c->stats;
     a.flags = c->flags;
-    a.queues = c->queues;
+    a.xcds = c->queues;
+    a.queues = c->queues;   // (x queues per XCD once the persistent grid is known, launch())
     return a;
 }
 
@@ -624,6 +630,10 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             if (nblk > need) nblk = need;
             if (c->max_blocks && nblk > c->max_blocks) nblk = c->max_blocks;
             const dim3 grid(nblk);
+            // several queues per XCD split each XCD's tickets over as many counters (less contention on
+            // each); every queue needs waves of its own, so only with a full grid (>= 64 waves per queue)
+            if (c->queues_per_xcd > 1u && nblk * wpb >= 64u * c->queues * c->queues_per_xcd)
+                a.queues = c->queues * c->queues_per_xcd;
             // the order is rebuilt after every order_every-th render (and whenever none exists for this frame
             // size); the renders in between keep the last order and record their tile costs only
             const bool rebuild = c->use_order && (c->order_n != ntiles || c->order_phase + 1u >= c->order_every);

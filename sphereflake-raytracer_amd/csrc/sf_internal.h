@@ -35,7 +35,7 @@
 
 // Persistent-kernel tile queues: SF_QUEUES counters per render parity, one 128-byte line each, after
 // the two overflow counters (u32 words).
-#define SF_QUEUES 8u
+#define SF_QUEUES 32u                     // up to 8 XCDs x 4 queues per XCD
 #define SF_QUEUE_STRIDE 32u
 #define SF_QUEUE_WORD(parity, k) (SF_QUEUE_STRIDE + ((parity) * SF_QUEUES + (k)) * SF_QUEUE_STRIDE)
 #define SF_COUNTER_WORDS (SF_QUEUE_STRIDE + 2u * SF_QUEUES * SF_QUEUE_STRIDE)
@@ -113,7 +113,8 @@ struct FrameArgs {
     uint32_t* part_cost;              // per tile: max cycles over the parts of a split tile (reset by the last part)
     uint32_t* part_done;              // per tile: parts of a split tile finished (reset by the last part)
     uint32_t packet_lanes;            // frame-less mode: 8 (AVX variant) or 4 (SSE variant, 2x2 footprint)
-    uint32_t queues;                  // persistent trace: tile queues in use (one per XCD, power of 2 <= SF_QUEUES)
+    uint32_t queues;                  // persistent trace: tile queues in use (xcds x queues per XCD, <= SF_QUEUES)
+    uint32_t xcds;                    // persistent trace: XCD queue groups (power of 2); queue k serves XCD k % xcds
     uint32_t* bin_cost;               // frame-less mode (NULL = off): per packet bin, cycles of the last wave starting in it
     uint32_t bin_shift, bins_x;       // frame-less mode: the batch's packet bins (squares of 2^bin_shift pixels)
 };

@@ -1062,8 +1062,11 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
     // contended chip-wide at the end of the frame: the last wave exited ~60 us after the last tile
     // ended. Every queue still drains: its XCD's waves only leave when it is empty, and queue units exist
     // only when the grid is the full persistent grid, which spans every XCD.
-    const uint32_t nq = a.queues;
-    const uint32_t k = __builtin_amdgcn_readfirstlane(xcc) & (nq - 1u);
+    const uint32_t nq = a.queues, nx = a.xcds;
+    // queue k = XCD group (k % nx) + nx x sub-queue; an XCD's waves spread over its nq / nx sub-queues by
+    // their position in the grid (blocks go round-robin over the XCDs)
+    const uint32_t sub = ((blockIdx.x / nx) * WAVES + wv) & (nq / nx - 1u);
+    const uint32_t k = __builtin_amdgcn_readfirstlane((xcc & (nx - 1u)) + nx * sub);
     int32_t maxd = -1;
     float closest = FLT_MAX;   // per lane
     // The first unit of every wave is static: wave w (in dispatch order) takes unit w, so the head of the
