@@ -1178,7 +1178,13 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t*
     const uint32_t tid = threadIdx.x, b = tid % SF_ORDER_BUCKETS, k = tid / SF_ORDER_BUCKETS;
     const uint32_t per = (nc + 31u) / 32u, c0 = k * per, c1 = min(nc, c0 + per);
     uint32_t s_ = 0u;
-    for (uint32_t cb = c0; cb < c1; cb += SF_SCAN_BATCH) {
+    uint32_t v0[SF_SCAN_BATCH];   // the first batch stays in registers for the offsets pass below (frames of up
+                                  // to 32 x SF_SCAN_BATCH chunks, 1080p included, need no second read)
+#pragma unroll
+    for (int j = 0; j < SF_SCAN_BATCH; ++j) v0[j] = c0 + j < c1 ? chunk_cnt[(c0 + j) * SF_ORDER_BUCKETS + b] : 0u;
+#pragma unroll
+    for (int j = 0; j < SF_SCAN_BATCH; ++j) s_ += v0[j];
+    for (uint32_t cb = c0 + SF_SCAN_BATCH; cb < c1; cb += SF_SCAN_BATCH) {
         uint32_t v[SF_SCAN_BATCH];
 #pragma unroll
         for (int j = 0; j < SF_SCAN_BATCH; ++j) v[j] = cb + j < c1 ? chunk_cnt[(cb + j) * SF_ORDER_BUCKETS + b] : 0u;
@@ -1198,47 +1204,63 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t*
     }
     __syncthreads();
     __shared__ uint32_t split_from;
-    if (tid == 0) {
+    if (tid < 64u) {
+        // One wave, lane = bucket (lanes 32..63 hold 0): the split and priority decisions and the bucket
+        // offsets from suffix sums over the buckets (heaviest first), instead of serial loops on one thread.
         // Split tiles into `parts` units each, heaviest buckets first (bucket 0 never): automatically as
         // many whole buckets as fit into `spare` idle wave slots, or the top `split_buckets` occupied
-        // buckets (at most an eighth of the tiles). Then bucket totals (in units) -> exclusive offsets,
-        // heaviest first.
-        int bs = (int)SF_ORDER_BUCKETS;
-        uint32_t nsplit = 0u;
-        if (split_buckets == SF_SPLIT_AUTO) {
-            for (int bb = (int)SF_ORDER_BUCKETS - 1; bb >= 1 && (nsplit + tot[bb]) * (parts - 1u) <= spare; --bb) {
-                nsplit += tot[bb];
-                bs = bb;
-            }
-        } else if (split_buckets != 0u) {
-            int bmax = (int)SF_ORDER_BUCKETS - 1;
-            while (bmax > 0 && tot[bmax] == 0u) --bmax;
-            bs = bmax - (int)split_buckets + 1;
-            if (bs < 1) bs = 1;
-            for (int bb = bs; bb < (int)SF_ORDER_BUCKETS; ++bb) nsplit += tot[bb];
-            while (bs < (int)SF_ORDER_BUCKETS && 8u * nsplit > n_tiles) nsplit -= tot[bs++];
+        // buckets (at most an eighth of the tiles).
+        const uint32_t l = tid;
+        const uint32_t t = l < SF_ORDER_BUCKETS ? tot[l] : 0u;
+        uint32_t S = t;   // S(l) = sum of tot[bb] over bb >= l
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+            const uint32_t up = (uint32_t)__shfl_down((int)S, o, 64);
+            S += l + (uint32_t)o < SF_ORDER_BUCKETS ? up : 0u;
         }
-        split_from = (uint32_t)bs;
+        const uint64_t nz = __builtin_amdgcn_ballot_w64(t != 0u);
+        const int btop = nz ? 63 - __builtin_clzll(nz) : 0;   // highest occupied bucket (0 if none)
+        int bs = (int)SF_ORDER_BUCKETS;
+        if (split_buckets == SF_SPLIT_AUTO) {
+            // S is non-increasing in the bucket: the buckets that fit form a suffix
+            const uint64_t ok = __builtin_amdgcn_ballot_w64(l >= 1u && l < SF_ORDER_BUCKETS && S * (parts - 1u) <= spare);
+            if (ok >> (SF_ORDER_BUCKETS - 1u) & 1ull) bs = __builtin_ctzll(ok);
+        } else if (split_buckets != 0u) {
+            int b0 = btop - (int)split_buckets + 1;
+            if (b0 < 1) b0 = 1;
+            // then drop buckets from the bottom of the range while more than an eighth of the tiles split
+            const uint64_t ok = __builtin_amdgcn_ballot_w64((int)l >= b0 && l < SF_ORDER_BUCKETS && 8u * S <= n_tiles);
+            bs = ok ? __builtin_ctzll(ok) : (int)SF_ORDER_BUCKETS;
+        }
         // the top `prio_buckets` occupied cost buckets run at raised wave priority next render (their
         // serial DFS is the frame's critical path)
-        int btop = (int)SF_ORDER_BUCKETS - 1;
-        while (btop > 0 && tot[btop] == 0u) --btop;
         const int bp = btop - (int)prio_buckets + 1;
-        order_meta[3] = prio_buckets == 0u ? SF_ORDER_BUCKETS : (uint32_t)(bp < 0 ? 0 : bp);
-        uint32_t acc = 0u;
-        for (int bb = (int)SF_ORDER_BUCKETS - 1; bb >= 0; --bb) {
-            const uint32_t x = tot[bb] * (bb >= bs ? parts : 1u);
-            tot[bb] = acc;
-            acc += x;
+        // units per bucket -> exclusive offsets, heaviest first: X(l) = sum of units over bb > l
+        const uint32_t x = t * ((int)l >= bs ? parts : 1u);
+        uint32_t X = x;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+            const uint32_t up = (uint32_t)__shfl_down((int)X, o, 64);
+            X += l + (uint32_t)o < SF_ORDER_BUCKETS ? up : 0u;
         }
-        order_meta[0] = acc;            // units of the next render
-        order_meta[1] = (uint32_t)bs;   // first split bucket
-        order_meta[2] = parts;          // units per split tile
+        if (l < SF_ORDER_BUCKETS) tot[l] = X - x;
+        if (l == 0u) {
+            split_from = (uint32_t)bs;
+            order_meta[0] = X;              // units of the next render
+            order_meta[1] = (uint32_t)bs;   // first split bucket
+            order_meta[2] = parts;          // units per split tile
+            order_meta[3] = prio_buckets == 0u ? SF_ORDER_BUCKETS : (uint32_t)(bp < 0 ? 0 : bp);
+        }
     }
     __syncthreads();
     const uint32_t mult = b >= split_from ? parts : 1u;
     uint32_t off = tot[b] + part[k][b] * mult;
-    for (uint32_t cb = c0; cb < c1; cb += SF_SCAN_BATCH) {
+#pragma unroll
+    for (int j = 0; j < SF_SCAN_BATCH; ++j) {
+        if (c0 + j < c1) chunk_off[(c0 + j) * SF_ORDER_BUCKETS + b] = off;
+        off += v0[j] * mult;
+    }
+    for (uint32_t cb = c0 + SF_SCAN_BATCH; cb < c1; cb += SF_SCAN_BATCH) {
         uint32_t v[SF_SCAN_BATCH];
 #pragma unroll
         for (int j = 0; j < SF_SCAN_BATCH; ++j) v[j] = cb + j < c1 ? chunk_cnt[(cb + j) * SF_ORDER_BUCKETS + b] : 0u;
