@@ -769,7 +769,7 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
         uint64_t skip = 2 * counter0;
         while (skip > 0) {
             uint32_t n = (uint32_t)(skip < 2ull * c->prog_cap ? skip : 2ull * c->prog_cap);
-            hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(1024), 0, s, c->mt_state, c->draws, n);
+            hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(256), 0, s, c->mt_state, c->draws, n);
             SF_HIP(c, hipGetLastError());
             skip -= n;
         }
@@ -784,7 +784,7 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     a.packet_lanes = pl;
     if (c->flags & SF_FLAG_DIAG_UNITS) a.tile_trace = c->tile_trace;   // per-wave diagnostics (sf_set_tile_trace)
     if (!prefetched) {
-        hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(1024), 0, s, c->mt_state, c->draws, 2 * packets);
+        hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(256), 0, s, c->mt_state, c->draws, 2 * packets);
         SF_HIP(c, hipGetLastError());
     }
     // Prefetch the next batch's draws (a continuing stream of the same batch size) on pf_stream, into
@@ -802,7 +802,7 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
         SF_HIP(c, hipStreamWaitEvent(c->pf_stream, c->mt_ready, 0));
         if (c->traced_valid) SF_HIP(c, hipStreamWaitEvent(c->pf_stream, c->traced, 0));   // draws_pf free
         SF_HIP(c, hipMemcpyAsync(c->mt_saved, c->mt_state, 625 * 4, hipMemcpyDeviceToDevice, c->pf_stream));
-        hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(1024), 0, c->pf_stream, c->mt_state, c->draws_pf, 2 * packets);
+        hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(256), 0, c->pf_stream, c->mt_state, c->draws_pf, 2 * packets);
         SF_HIP(c, hipGetLastError());
         SF_HIP(c, hipEventRecord(c->pf_done, c->pf_stream));
         c->pf_packets = packets;

@@ -1439,52 +1439,77 @@ extern "C" __global__ __launch_bounds__(256) void sf_trace_ray(FrameArgs a)
 // Frame-less progressive mode (Sphereflake.cpp:86-214): random 8-ray packets.
 // ------------------------------------------------------------------------------------------
 
-// std::mt19937 continuation: state[0..623] + next index state[624]; writes n raw 32-bit outputs
+// std::mt19937 continuation: state[0..623] + next index state[624]; writes n tempered 32-bit outputs
 // (std::uniform_int_distribution<unsigned>(0) over the full range returns them unchanged).
-// One workgroup; the twist runs in four dependency phases through LDS.
-extern "C" __global__ __launch_bounds__(1024) void sf_mt_draws(uint32_t* state, uint32_t* out, uint32_t n)
+// One workgroup. The twist runs as 227 independent chains: thread j < 227 makes words j, j + 227 and
+// (j < 169) j + 454 of the new block, each from the old block and the chain's own previous word (the
+// offset 397 - 624 = -227), in registers -- no barrier inside a twist, one between blocks (there were 3).
+// Word 623 of a new block needs new words 0 and 396 (two chains): it is made lazily, in the next twist, by
+// the two threads that use it (226: offset 397; 168: offset 1), from the old block's word 623 that the
+// buffer being refilled still holds at index 623 (thread 226 writes it back for the twist after).
+#define SF_MT_THREADS 256
+extern "C" __global__ __launch_bounds__(SF_MT_THREADS) void sf_mt_draws(uint32_t* state, uint32_t* out, uint32_t n)
 {
-    // Double-buffered twist in three dependency phases ([0, 227) from the old block; [227, 454) and
-    // [454, 623) + 623 from words just made: offsets 397 - 624 = -227 and 1 - 624): 3 barriers per
-    // 624 words, no copy-back. A tempered block is written while the next twist fills the other buffer.
     __shared__ uint32_t buf[2][624];
     const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < 624u; i += blockDim.x) buf[0][i] = state[i];
-    uint32_t pos = state[624], cur = 0;
+    for (uint32_t i = tid; i < 624u; i += SF_MT_THREADS) buf[0][i] = state[i];
+    const uint32_t pos0 = min(state[624], 624u);
     __syncthreads();
     auto f = [](uint32_t a, uint32_t b, uint32_t c) {
         const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
         return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
     };
-    uint32_t done = 0;
+    auto temper = [](uint32_t y) {
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= y >> 18;
+        return y;
+    };
+    // the rest of the loaded (complete) block
+    const uint32_t m0 = min(624u - pos0, n);
+    for (uint32_t k = tid; k < m0; k += SF_MT_THREADS) out[k] = temper(buf[0][pos0 + k]);
+    uint32_t done = m0;    // outputs written (uniform)
+    uint32_t cur = 0;      // buffer of the newest block
+    bool full = true;      // the newest block's word 623 is in the buffer (only the loaded block's)
+    uint32_t pos = pos0 + m0;
     while (done < n) {
-        if (pos >= 624u) {
-            const uint32_t* sb = buf[cur];
-            uint32_t* tb = buf[cur ^ 1u];
-            if (tid < 227u) tb[tid] = f(sb[tid], sb[tid + 1u], sb[tid + 397u]);
-            __syncthreads();
-            if (tid >= 227u && tid < 454u) tb[tid] = f(sb[tid], sb[tid + 1u], tb[tid - 227u]);
-            __syncthreads();
-            if (tid >= 454u && tid < 623u) tb[tid] = f(sb[tid], sb[tid + 1u], tb[tid - 227u]);
-            else if (tid == 623u) tb[623] = f(sb[623], tb[0], tb[396]);
-            __syncthreads();
-            cur ^= 1u;
-            pos = 0;
+        const uint32_t* sb = buf[cur];
+        uint32_t* tb = buf[cur ^ 1u];
+        // output index of the new block's word 0: after the newest block's word 623 when that is still due
+        const uint32_t o = done + (full ? 0u : 1u);
+        if (tid < 227u) {
+            const uint32_t j = tid;
+            uint32_t x623 = 0u;   // the newest block's word 623 (threads 226 and 168)
+            if (j == 226u || j == 168u) {
+                x623 = full ? sb[623] : f(tb[623], sb[0], sb[396]);
+                if (j == 226u && !full) {
+                    buf[cur][623] = x623;                    // for the lazy word 623 of the block made now
+                    if (done < n) out[done] = temper(x623);   // its place in the stream
+                }
+            }
+            const uint32_t wa = f(sb[j], sb[j + 1u], j == 226u ? x623 : sb[j + 397u]);
+            tb[j] = wa;
+            if (o + j < n) out[o + j] = temper(wa);
+            const uint32_t wb = f(sb[j + 227u], sb[j + 228u], wa);
+            tb[j + 227u] = wb;
+            if (o + j + 227u < n) out[o + j + 227u] = temper(wb);
+            if (j < 168u || j == 168u) {
+                const uint32_t wc = f(sb[j + 454u], j == 168u ? x623 : sb[j + 455u], wb);
+                tb[j + 454u] = wc;
+                if (o + j + 454u < n) out[o + j + 454u] = temper(wc);
+            }
         }
-        const uint32_t m = min(624u - pos, n - done);
-        if (tid < m) {
-            uint32_t y = buf[cur][pos + tid];
-            y ^= y >> 11;
-            y ^= (y << 7) & 0x9d2c5680u;
-            y ^= (y << 15) & 0xefc60000u;
-            y ^= y >> 18;
-            out[done + tid] = y;
-        }
-        pos += m;
-        done += m;
+        __syncthreads();
+        done = min(n, o + 623u);   // words 0..622 of the new block (623 is due with the next twist)
+        pos = done - o;
+        cur ^= 1u;
+        full = false;
     }
+    // state: the newest block, its word 623 made now if it is lazy
+    if (!full && tid == 0u) buf[cur][623] = f(buf[cur ^ 1u][623], buf[cur][0], buf[cur][396]);
     __syncthreads();
-    for (uint32_t i = tid; i < 624u; i += blockDim.x) state[i] = buf[cur][i];
+    for (uint32_t i = tid; i < 624u; i += SF_MT_THREADS) state[i] = buf[cur][i];
     if (tid == 0) state[624] = pos;
 }
 
