@@ -1065,8 +1065,12 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
     const uint32_t nq = a.queues, nx = a.xcds;
     // queue k = XCD group (k % nx) + nx x sub-queue; an XCD's waves spread over its nq / nx sub-queues by
     // their position in the grid (blocks go round-robin over the XCDs)
-    const uint32_t sub = ((blockIdx.x / nx) * WAVES + wv) & (nq / nx - 1u);
-    const uint32_t k = __builtin_amdgcn_readfirstlane((xcc & (nx - 1u)) + nx * sub);
+    uint32_t k = __builtin_amdgcn_readfirstlane(xcc) & (nx - 1u);
+    if (nq > nx) {   // (powers of two: shifts, no division)
+        const uint32_t lx = __builtin_ctz(nx);
+        k += nx * (((blockIdx.x >> lx) * WAVES + wv) & ((nq >> lx) - 1u));
+        k = __builtin_amdgcn_readfirstlane(k);
+    }
     int32_t maxd = -1;
     float closest = FLT_MAX;   // per lane
     // The first unit of every wave is static: wave w (in dispatch order) takes unit w, so the head of the
