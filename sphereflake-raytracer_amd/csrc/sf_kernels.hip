@@ -152,9 +152,10 @@ __device__ __forceinline__ void sel_in_place(uint32_t& dst, uint32_t src, uint64
     __asm__("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(dst) : "v"(src), "s"(m));
 }
 
-// Exact near root, kept out of line so the compiler cannot if-convert the rare exact path of the
-// fast LOD bracket into every child test.
-__device__ __attribute__((noinline)) float near_root_exact(float tca, float d2, float R2)
+// Exact near root for the rare undecided lanes of the LOD bracket. Inlined: its uniform branch stays a
+// real branch (the structurizer leaves wave-uniform regions alone), and without a call no SGPRs are saved
+// around it (round 1 kept it out of line so it would not be if-converted into every child test).
+__device__ __forceinline__ float near_root_exact(float tca, float d2, float R2)
 {
     return near_root(tca, d2, R2);
 }
