@@ -23,6 +23,7 @@ extern "C" __global__ void sf_trace_wave4(FrameArgs a, uint32_t* overflow_list, 
 extern "C" __global__ void sf_trace_queue1(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2(FrameArgs a);
 extern "C" __global__ void sf_trace_queue4(FrameArgs a);
+extern "C" __global__ void sf_trace_queue2p(FrameArgs a);
 extern "C" __global__ void sf_order_scan(const uint32_t* chunk_cnt, uint32_t nc, uint32_t n_tiles,
                                          uint32_t split_buckets, uint32_t parts, uint32_t spare, uint32_t prio_buckets,
                                          uint32_t* chunk_off, uint32_t* order_meta);
@@ -114,6 +115,7 @@ struct sf_ctx {
     int cus = 256;
     uint32_t queues = 8;                         // persistent trace: XCD queue groups, one per XCD (power of 2)
     uint32_t queues_per_xcd = 1;                 // env SF_QUEUES_PER_XCD = 1 | 2 | 4: tile queues per XCD
+    int pipe = -1;                               // env SF_PIPE = 0 | 1: latency variant of the trace (-1: auto)
     uint32_t prio_buckets = 6;                   // top cost buckets (3 octaves) traced at raised wave priority (env SF_PRIO_BUCKETS)
     int occ_key = -1, occ_blocks = 0;            // cached occupancy (waves per block, levels) -> blocks per CU
     uint32_t max_blocks = 0;                     // diagnostics: env SF_MAX_BLOCKS caps the persistent grid
@@ -385,6 +387,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
             const int v = std::atoi(ev);
             if (v == 1 || v == 2 || v == 4 || v == 8) c->queues = (uint32_t)v;
         }
+        if (const char* ev = std::getenv("SF_PIPE")) c->pipe = std::atoi(ev) != 0 ? 1 : 0;
         if (const char* ev = std::getenv("SF_QUEUES_PER_XCD")) {
             const int v = std::atoi(ev);
             if (v == 1 || v == 2 || v == 4) c->queues_per_xcd = (uint32_t)v;
@@ -649,7 +652,12 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             const bool timed = c->timing && c->ev_phase == 0;
             if (c->timing) c->ev_phase = (c->ev_phase + 1u) % c->ev_period;
             if (timed) SF_HIP(c, hipEventRecord(c->ev[c->ev_next][0], s));
+            // small frames (tiles fill the persistent grid less than twice) are latency-bound: the heaviest
+            // tiles' serial DFS is the frame, and the pipelined child loop shortens it (640x360 -4 %); full
+            // grids are throughput-bound, where it costs more instructions than it hides (1080p +1.7 %)
+            const bool pipe = c->pipe >= 0 ? c->pipe == 1 : ntiles <= 2u * nblk * wpb;
             if (wpb == 1) hipLaunchKernelGGL(sf_trace_queue1, grid, block, lds, s, a);
+            else if (wpb == 2 && pipe) hipLaunchKernelGGL(sf_trace_queue2p, grid, block, 2 * lds, s, a);
             else if (wpb == 2) hipLaunchKernelGGL(sf_trace_queue2, grid, block, 2 * lds, s, a);
             else hipLaunchKernelGGL(sf_trace_queue4, grid, block, 4 * lds, s, a);
             SF_HIP(c, hipGetLastError());

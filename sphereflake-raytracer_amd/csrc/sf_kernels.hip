@@ -342,7 +342,9 @@ __device__ __forceinline__ void stage_root(float* __restrict__ Lbase, const floa
     }
 }
 
-template <int PW>   // packet width of the semantics: 0 per ray, 8 (AVX) or 4 (SSE) frame-less packets
+// PW: packet width of the semantics (0 per ray, 8 (AVX) or 4 (SSE) frame-less packets); PIPE: the latency
+// variant of the per-ray child loop (small frames, whose heaviest tiles' serial DFS is the frame)
+template <int PW, bool PIPE = false>
 __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ Lbase,
                                          uint32_t levels, float dx, float dy, float dz, bool valid, HitState& h,
                                          int32_t& maxd, bool& overflowed, uint32_t K_flags,
@@ -542,12 +544,102 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             // actv (+inf on the lanes visiting the node, -1 on the others): ONE v_min3 + compare gives the
             // bounding mask already restricted to the visiting lanes, and the loop branches on it (VCC)
             // without scalar mask algebra
+            // one child test: bounding + LOD of child i (centre c, |c|^2 cc) for every lane
+            auto test_child = [&](uint32_t i, float cx, float cy, float cz, float cc) {
+                SF_COUNT(1, 1);
+                const float tca = (cx * dx + cy * dy) + cz * dz;
+                const float d2 = cc - tca * tca;
+                // bounding (SIMD_AVX.h:247-258): tca >= 0 && d2 <= R2b as ONE compare, min(tca, R2b - d2) >= 0:
+                // with denormals kept, fl(R2b - d2) >= 0 exactly when d2 <= R2b (no NaN operands here)
+                const float xs = R2b - d2;
+                const bool hb = __builtin_fminf(__builtin_fminf(tca, xs), actv) >= 0.0f;
+                const uint64_t hbm = wave_ballot(hb);
+#ifdef SF_EXP_PAD   // experiment builds only: independent VALU filler per child iteration (issue-bound test)
+                {
+                    float pad = dx;
+#pragma unroll
+                    for (int k_ = 0; k_ < SF_EXP_PAD; ++k_) __asm__ volatile("v_mov_b32 %0, %0" : "+v"(pad));
+                }
+#endif
+#ifdef SF_EXP_SPAD  // experiment builds only: SALU filler per child iteration (scalar-unit-bound test)
+                {
+                    uint32_t spad = i;
+#pragma unroll
+                    for (int k_ = 0; k_ < SF_EXP_SPAD; ++k_) __asm__ volatile("s_add_u32 %0, %0, 1" : "+s"(spad)::"scc");
+                }
+#endif
+                SF_COUNT(5, __builtin_popcountll(actm));
+                SF_COUNT(6, __builtin_popcountll(hbm));
+                SF_COUNT(10, d >= 4u ? 1 : 0);
+                SF_COUNT(11, d >= 4u ? __builtin_popcountll(actm) : 0);
+                SF_COUNT(12, __builtin_popcountll(actm) <= 4 ? 1 : 0);
+                SF_COUNT(13, __builtin_popcountll(actm) <= 16 ? 1 : 0);
+                SF_COUNT(14, __builtin_popcountll(actm) <= 32 ? 1 : 0);
+                if (hbm == 0ull) {
+                    SF_COUNT(2, 1);
+                    return;
+                }
+                // LOD on t = fl(tca - sqrt_rn(R2b - d2)) (SIMD_AVX.h:260-267; t0 <= t1 picks t1 for
+                // thc >= 0). Fast bracket: the hardware sqrt is within 2 ulp of sqrt_rn and t is
+                // monotone in it, so t_lo = fl(tca - (s + 2ulp)) <= t <= t_hi = fl(tca - (s - 2ulp)):
+                // t_hi < T decides "expands", t_lo >= T decides "does not"; the exact path runs only
+                // for lanes in between (or with a tiny sqrt argument).
+                const float sq = __builtin_amdgcn_sqrtf(xs);
+                const float s_lo = __uint_as_float((uint32_t)max((int32_t)__float_as_uint(sq) - 2, 0));
+                const float s_hi = __uint_as_float(__float_as_uint(sq) + 2u);
+                const float t_hi = tca - s_lo;
+                const float t_lo = tca - s_hi;
+                // The decision as per-lane values instead of scalar mask algebra: th / tl are t_hi / t_lo on
+                // the lanes with a bounding hit and +inf elsewhere; a tiny sqrt argument makes the bracket
+                // (-inf, +inf), i.e. undecided. expands: th < T; undecided: tl < T <= th.
+                const uint64_t tinym = wave_ballot(xs < 0x1p-96f);
+                // (the tiny select is opaque asm, so the hb select below stays one v_cndmask on the VCC of the
+                // bounding compare instead of being merged into scalar mask algebra)
+                const float thx = sel_mask(t_hi, __builtin_inff(), tinym);
+                const float tlx = sel_mask(t_lo, -__builtin_inff(), tinym);
+                const float th = hb ? thx : __builtin_inff();
+                const float tl = hb ? tlx : __builtin_inff();
+                uint64_t exm = wave_ballot(th < T);
+                const uint64_t undm = wave_ballot(sel_mask(tl, __builtin_inff(), exm) < T);
+                if (undm) {   // rare: exact IEEE root for the undecided lanes (disjoint from exm)
+                    const float te = near_root_exact(tca, d2, R2b);
+                    exm |= undm & wave_ballot(te < T);
+                }
+                sel_in_place(e, e | (1u << i), exm);   // the lanes of exm get bit i
+                if (exm != 0ull) pm |= 1u << i;
+                SF_COUNT(3, exm != 0ull ? 1 : 0);
+            };
             auto child_loop = [&](auto tab) {
                 const float* ctab = L.table(d);
+                if constexpr (PIPE && decltype(tab)::value) {
+                    // latency variant (small frames): software-pipelined two ways -- the next child's {centre,
+                    // cc} is read into the other register set while this one is tested, so the LDS latency
+                    // overlaps the test. Scalar loads are drained first so the waits count LDS reads only.
+                    // Child 8 is read again past the last child: harmless.
+                    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+                    if (M) {
+                        uint32_t i = __builtin_ctz(M);
+                        float4 ca = *reinterpret_cast<const float4*>(ctab + i * 4u), cb;
+                        for (;;) {
+                            uint32_t ci = i;
+                            M &= ~(1u << ci);
+                            i = __builtin_ctz(M | 0x100u);
+                            cb = *reinterpret_cast<const float4*>(ctab + i * 4u);
+                            test_child(ci, ca.x, ca.y, ca.z, ca.w);
+                            if (!M) break;
+                            ci = i;
+                            M &= ~(1u << ci);
+                            i = __builtin_ctz(M | 0x100u);
+                            ca = *reinterpret_cast<const float4*>(ctab + i * 4u);
+                            test_child(ci, cb.x, cb.y, cb.z, cb.w);
+                            if (!M) break;
+                        }
+                    }
+                }
+                else
                 while (M) {   // uniform loop over the children some lane can reach, in index order
                     const uint32_t i = __builtin_ctz(M);
                     M &= ~(1u << i);
-                    SF_COUNT(1, 1);
                     float cx, cy, cz, cc;
                     if constexpr (decltype(tab)::value) {
                         const float4 c4 = *reinterpret_cast<const float4*>(ctab + i * 4u);
@@ -556,67 +648,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                         cx = readlane_f(x, 27u + i), cy = readlane_f(y, 27u + i);
                         cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
                     }
-                    const float tca = (cx * dx + cy * dy) + cz * dz;
-                    const float d2 = cc - tca * tca;
-                    // bounding (SIMD_AVX.h:247-258): tca >= 0 && d2 <= R2b as ONE compare, min(tca, R2b - d2) >= 0:
-                    // with denormals kept, fl(R2b - d2) >= 0 exactly when d2 <= R2b (no NaN operands here)
-                    const float xs = R2b - d2;
-                    const bool hb = __builtin_fminf(__builtin_fminf(tca, xs), actv) >= 0.0f;
-                    const uint64_t hbm = wave_ballot(hb);
-#ifdef SF_EXP_PAD   // experiment builds only: independent VALU filler per child iteration (issue-bound test)
-                    {
-                        float pad = dx;
-#pragma unroll
-                        for (int k_ = 0; k_ < SF_EXP_PAD; ++k_) __asm__ volatile("v_mov_b32 %0, %0" : "+v"(pad));
-                    }
-#endif
-#ifdef SF_EXP_SPAD  // experiment builds only: SALU filler per child iteration (scalar-unit-bound test)
-                    {
-                        uint32_t spad = i;
-#pragma unroll
-                        for (int k_ = 0; k_ < SF_EXP_SPAD; ++k_) __asm__ volatile("s_add_u32 %0, %0, 1" : "+s"(spad)::"scc");
-                    }
-#endif
-                    SF_COUNT(5, __builtin_popcountll(actm));
-                    SF_COUNT(6, __builtin_popcountll(hbm));
-                    SF_COUNT(10, d >= 4u ? 1 : 0);
-                    SF_COUNT(11, d >= 4u ? __builtin_popcountll(actm) : 0);
-                    SF_COUNT(12, __builtin_popcountll(actm) <= 4 ? 1 : 0);
-                    SF_COUNT(13, __builtin_popcountll(actm) <= 16 ? 1 : 0);
-                    SF_COUNT(14, __builtin_popcountll(actm) <= 32 ? 1 : 0);
-                    if (hbm == 0ull) {
-                        SF_COUNT(2, 1);
-                        continue;
-                    }
-                    // LOD on t = fl(tca - sqrt_rn(R2b - d2)) (SIMD_AVX.h:260-267; t0 <= t1 picks t1 for
-                    // thc >= 0). Fast bracket: the hardware sqrt is within 2 ulp of sqrt_rn and t is
-                    // monotone in it, so t_lo = fl(tca - (s + 2ulp)) <= t <= t_hi = fl(tca - (s - 2ulp)):
-                    // t_hi < T decides "expands", t_lo >= T decides "does not"; the exact path runs only
-                    // for lanes in between (or with a tiny sqrt argument).
-                    const float sq = __builtin_amdgcn_sqrtf(xs);
-                    const float s_lo = __uint_as_float((uint32_t)max((int32_t)__float_as_uint(sq) - 2, 0));
-                    const float s_hi = __uint_as_float(__float_as_uint(sq) + 2u);
-                    const float t_hi = tca - s_lo;
-                    const float t_lo = tca - s_hi;
-                    // The decision as per-lane values instead of scalar mask algebra: th / tl are t_hi / t_lo on
-                    // the lanes with a bounding hit and +inf elsewhere; a tiny sqrt argument makes the bracket
-                    // (-inf, +inf), i.e. undecided. expands: th < T; undecided: tl < T <= th.
-                    const uint64_t tinym = wave_ballot(xs < 0x1p-96f);
-                    // (the tiny select is opaque asm, so the hb select below stays one v_cndmask on the VCC of the
-                    // bounding compare instead of being merged into scalar mask algebra)
-                    const float thx = sel_mask(t_hi, __builtin_inff(), tinym);
-                    const float tlx = sel_mask(t_lo, -__builtin_inff(), tinym);
-                    const float th = hb ? thx : __builtin_inff();
-                    const float tl = hb ? tlx : __builtin_inff();
-                    uint64_t exm = wave_ballot(th < T);
-                    const uint64_t undm = wave_ballot(sel_mask(tl, __builtin_inff(), exm) < T);
-                    if (undm) {   // rare: exact IEEE root for the undecided lanes (disjoint from exm)
-                        const float te = near_root_exact(tca, d2, R2b);
-                        exm |= undm & wave_ballot(te < T);
-                    }
-                    sel_in_place(e, e | (1u << i), exm);   // the lanes of exm get bit i
-                    if (exm != 0ull) pm |= 1u << i;
-                    SF_COUNT(3, exm != 0ull ? 1 : 0);
+                    test_child(i, cx, cy, cz, cc);
                 }
                 // children of a node at the deepest provisioned level (no table) would need a level that does
                 // not exist: flag the tile for the deeper re-trace instead of entering them
@@ -898,7 +930,7 @@ struct NoPrefetch {
 // `pre` runs right after the traversal, before the tile's shading and stores: the persistent kernel takes
 // its next queue ticket there, so the atomic's round trip overlaps the shading instead of following the
 // G-buffer stores (whose completion a later wait would otherwise include: vmcnt counts in order).
-template <bool FIXUP, class Prefetch = NoPrefetch>
+template <bool FIXUP, bool PIPE = false, class Prefetch = NoPrefetch>
 __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __restrict__ L, uint32_t tile,
                                                 uint32_t levels, uint32_t* overflow_list, uint32_t* overflow_count,
                                                 uint32_t part = 0u, const Prefetch& pre = Prefetch())
@@ -916,7 +948,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     int32_t maxd = -1;
     bool overflowed = false;
     uint64_t tile_counts = 0;
-    traverse<0>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed, a.flags,
+    traverse<0, PIPE>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed, a.flags,
                     FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
     pre();
     if (!FIXUP && a.tile_trace) {
@@ -1029,7 +1061,7 @@ extern "C" __global__ __launch_bounds__(256) void sf_trace_wave4(FrameArgs a, ui
 // atomic queue until it runs dry. Dynamic balancing: tile costs vary ~100x (sky vs. deep flake),
 // and the in-order workgroup dispatcher otherwise idles CUs behind long tiles. counters: [0,1]
 // overflow counts, [2,3] tile queues, alternating per render (this render zeroes the next one's).
-template <int WAVES>
+template <int WAVES, bool PIPE = false>
 __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 {
     extern __shared__ float lds[];
@@ -1129,7 +1161,7 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
         auto ticket = [&]() {
             first = nwaves + wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u) * nq + k;   // uniform
         };
-        const TileStats st = trace_tile<false>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity, part,
+        const TileStats st = trace_tile<false, PIPE>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity, part,
                                                ticket);
         if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace) {   // diagnostics only (uniform words)
             uint64_t* ut = at.tile_trace + 3u * (at.tiles_x * at.tile_rows) + SF_DIAG_SLOTS + 3u * g;
@@ -1160,6 +1192,11 @@ extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue4(FrameArgs a)
 {
     trace_queue_body<4>(a);
+}
+// latency variant (pipelined child loop) for frames whose tiles do not fill the persistent grid twice
+extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue2p(FrameArgs a)
+{
+    trace_queue_body<2, true>(a);
 }
 
 // Tile order for the next render: tiles sorted by this render's cost, heaviest first (LPT list
