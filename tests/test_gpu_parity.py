@@ -290,6 +290,22 @@ def test_repeat_renders_heavy_first_order_bit_exact():
     assert st.max_depth == fx["stats"]["max_depth"] and st.overflow_tiles == 0
 
 
+@pytest.mark.parametrize("name,pipe", [("c1", "0"), ("c3", "1")])
+def test_trace_variants_forced_bit_exact(monkeypatch, name, pipe):
+    """The persistent trace has a latency variant (sf_trace_queue2p, pipelined child loop) that the host
+    picks for small frames; SF_PIPE forces either. Each variant on the other's frame size: golden frame."""
+    monkeypatch.setenv("SF_PIPE", pipe)
+    fx = load_frame(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for k in range(2):   # row-major first render, then the heavy-first order
+            s.Render(emit_aux=True)
+            pos, nrm, mint, idx = s.download(aux=True)
+            assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == [], f"render {k}"
+            assert bad_rows(fx["row_digest_aux"], aux_digests(mint, idx)) == [], f"render {k}"
+
+
 @pytest.mark.parametrize("every", ["2", "3"])
 def test_order_rebuilt_every_kth_render_bit_exact(monkeypatch, every):
     """SF_ORDER_EVERY=k: renders between two order rebuilds record tile costs without the histogram and
