@@ -188,7 +188,8 @@ struct sf_ctx {
     hipStream_t last_stream = nullptr; // stream of the latest enqueued work (nullptr: the context stream)
     hipEvent_t join_ev = nullptr;      // recorded on last_stream when a call switches streams
     bool use_order = true;             // env SF_ORDER=0: row-major order always
-    uint32_t order_every = 1;          // env SF_ORDER_EVERY = k: rebuild the order after every k-th render only
+    uint32_t order_every = 0;          // env SF_ORDER_EVERY = k: rebuild the order after every k-th render only
+                                       // (0 = auto: 3 for small frames, 1 otherwise)
     uint32_t order_phase = 0;          // renders since the last rebuild
     // Measurement: HIP events around the main trace kernel of each render (sf_set_kernel_timing)
     static constexpr int kTimed = 64;
@@ -395,7 +396,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     }
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_ORDER")) c->use_order = std::atoi(ev) != 0;
-    if (const char* ev = std::getenv("SF_ORDER_EVERY")) c->order_every = std::atoi(ev) > 1 ? (uint32_t)std::atoi(ev) : 1u;
+    if (const char* ev = std::getenv("SF_ORDER_EVERY")) c->order_every = std::atoi(ev) > 1 ? (uint32_t)std::atoi(ev) : 1u;   // (explicit)
     if (const char* ev = std::getenv("SF_PROG_BIN")) c->prog_bin = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_PREFETCH")) c->prog_prefetch = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_ADAPT")) c->prog_adapt = std::atoi(ev) != 0;
@@ -639,7 +640,13 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 a.queues = c->queues * c->queues_per_xcd;
             // the order is rebuilt after every order_every-th render (and whenever none exists for this frame
             // size); the renders in between keep the last order and record their tile costs only
-            const bool rebuild = c->use_order && (c->order_n != ntiles || c->order_phase + 1u >= c->order_every);
+            // Small frames (tiles fill the persistent grid less than twice) are latency-bound: there the stale
+            // order costs the trace nothing measurable while the two order kernels are ~5 us of a ~80 us
+            // frame, so by default they are rebuilt after every 3rd render (640x360 -6 %, 1280x720 -4 %);
+            // full grids are throughput-bound and a stale order costs more than the kernels (1080p).
+            const bool small = ntiles <= 2u * nblk * wpb;
+            const uint32_t every = c->order_every ? c->order_every : (small ? 3u : 1u);
+            const bool rebuild = c->use_order && (c->order_n != ntiles || c->order_phase + 1u >= every);
             if (c->use_order) c->order_phase = rebuild ? 0u : c->order_phase + 1u;
             if (c->use_order) {
                 a.tile_cost = c->tile_cost;
@@ -655,7 +662,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             // small frames (tiles fill the persistent grid less than twice) are latency-bound: the heaviest
             // tiles' serial DFS is the frame, and the pipelined child loop shortens it (640x360 -4 %); full
             // grids are throughput-bound, where it costs more instructions than it hides (1080p +1.7 %)
-            const bool pipe = c->pipe >= 0 ? c->pipe == 1 : ntiles <= 2u * nblk * wpb;
+            const bool pipe = c->pipe >= 0 ? c->pipe == 1 : small;
             if (wpb == 1) hipLaunchKernelGGL(sf_trace_queue1, grid, block, lds, s, a);
             else if (wpb == 2 && pipe) hipLaunchKernelGGL(sf_trace_queue2p, grid, block, 2 * lds, s, a);
             else if (wpb == 2) hipLaunchKernelGGL(sf_trace_queue2, grid, block, 2 * lds, s, a);
