@@ -290,6 +290,25 @@ def test_repeat_renders_heavy_first_order_bit_exact():
     assert st.max_depth == fx["stats"]["max_depth"] and st.overflow_tiles == 0
 
 
+@pytest.mark.parametrize("qpx", ["2", "4"])
+def test_several_queues_per_xcd_bit_exact(monkeypatch, qpx):
+    """SF_QUEUES_PER_XCD: each XCD's tickets split over several queue words (sub-queues served by disjoint
+    sets of that XCD's waves). Every unit must still be traced exactly once: the c3 frame stays golden over
+    repeated renders (row-major, then heavy-first)."""
+    monkeypatch.setenv("SF_QUEUES_PER_XCD", qpx)
+    fx = load_frame("c3")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for k in range(3):
+            s.Render(emit_aux=True)
+            pos, nrm, mint, idx = s.download(aux=True)
+            assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == [], f"render {k}"
+            assert bad_rows(fx["row_digest_aux"], aux_digests(mint, idx)) == [], f"render {k}"
+        st = s.stats()
+    assert st.rays == 3 * W * H and st.overflow_tiles == 0
+
+
 @pytest.mark.parametrize("name,pipe", [("c1", "0"), ("c3", "1")])
 def test_trace_variants_forced_bit_exact(monkeypatch, name, pipe):
     """The persistent trace has a latency variant (sf_trace_queue2p, pipelined child loop) that the host
