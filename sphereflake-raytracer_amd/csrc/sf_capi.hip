@@ -116,7 +116,7 @@ struct sf_ctx {
     uint32_t queues = 8;                         // persistent trace: XCD queue groups, one per XCD (power of 2)
     uint32_t queues_per_xcd = 1;                 // env SF_QUEUES_PER_XCD = 1 | 2 | 4: tile queues per XCD
     int pipe = -1;                               // env SF_PIPE = 0 | 1: latency variant of the trace (-1: auto)
-    uint32_t prio_buckets = 6;                   // top cost buckets (3 octaves) traced at raised wave priority (env SF_PRIO_BUCKETS)
+    uint32_t prio_buckets = 8;                   // top cost buckets (3 octaves) traced at raised wave priority (env SF_PRIO_BUCKETS)
     int occ_key = -1, occ_blocks = 0;            // cached occupancy (waves per block, levels) -> blocks per CU
     uint32_t max_blocks = 0;                     // diagnostics: env SF_MAX_BLOCKS caps the persistent grid
     int variant = SF_VARIANT_AVX;                // reference path reproduced (sf_set_variant)

@@ -55,6 +55,9 @@
 #define SF_FLAG_DIAG_UNITS 0x20u
 // diagnostics only, WRONG results: the frame-less trace skips its per-pixel owner atomics (cost study)
 #define SF_FLAG_DIAG_NO_OWNER 0x40u
+// flat wave priority (A/B): every raised-priority cost bucket at s_setprio 2 (default: graded, see
+// trace_queue_body)
+#define SF_FLAG_PRIO_FLAT 0x80u
 
 struct DepthTables {
     float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)
