@@ -21,6 +21,7 @@
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <limits>
 #include <mutex>
@@ -53,6 +54,32 @@ struct GBuffer {
     std::vector<sf_vec4> normals;
 };
 
+// FIFO (ticket) lock: callers are served in arrival order. The frame-less loop re-locks right after each
+// batch; with std::mutex (not fair) a caller's per-frame SetView / GetGBuffer could lose to it for many
+// batches in a row. Here a waiting caller is always served before the loop's next batch.
+class FairMutex {
+public:
+    void lock()
+    {
+        std::unique_lock<std::mutex> l(m_);
+        const uint64_t t = next_++;
+        cv_.wait(l, [&] { return serving_ == t; });
+    }
+    void unlock()
+    {
+        {
+            std::lock_guard<std::mutex> l(m_);
+            ++serving_;
+        }
+        cv_.notify_all();
+    }
+
+private:
+    std::mutex m_;
+    std::condition_variable cv_;
+    uint64_t next_ = 0, serving_ = 0;
+};
+
 class Sphereflake {
 public:
     Sphereflake(size_t width, size_t height, int device = 0);
@@ -70,6 +97,10 @@ public:
     void Deinitialize();
     // Packets the frame-less loop has traced so far (= its next Sobol counter).
     uint64_t GetPacketsTraced() const;
+    // The frame-less loop's packet counter when the last SetView took effect: batches from that counter on
+    // trace the new view (the device loop picks a view up between batches; the reference's workers read
+    // it mid-packet, unsynchronised, Sphereflake.cpp:76-84).
+    uint64_t GetViewChangePacket() const;
 
     void SetView(const sf_vec3& origin, const sf_vec3& topLeft, const sf_vec3& topRight, const sf_vec3& bottomLeft);
 
@@ -102,11 +133,12 @@ private:
     mutable GBuffer m_GBuffer;
     mutable bool m_Stale = true;
     bool m_Pinned = false;
-    mutable std::mutex m_Mutex;
+    mutable FairMutex m_Mutex;
     std::thread m_Worker;
     std::atomic<bool> m_Deinitialize{ false };
     mutable std::atomic<int> m_WorkerError{ SF_OK };   // first failure of the frame-less loop
     uint64_t m_SobolCounter = 0;
+    uint64_t m_ViewChange = 0;
     uint32_t m_Seed = 0;
 };
 

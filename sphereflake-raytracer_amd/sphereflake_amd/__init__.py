@@ -299,6 +299,30 @@ def render_params(band_rows=0, band_count=1, band_index=0, compact=False, kernel
                             max_depth, 0, stream)
 
 
+class _FifoLock:
+    """Ticket lock: waiters are served in arrival order (the C++ class's FairMutex, Sphereflake.hpp). The
+    frame-less loop re-locks right after each batch; with a plain Lock a caller's SetView / GetGBuffer
+    could lose to it for many batches in a row."""
+
+    def __init__(self):
+        self._c = threading.Condition(threading.Lock())
+        self._next = 0
+        self._serving = 0
+
+    def __enter__(self):
+        with self._c:
+            t = self._next
+            self._next += 1
+            while self._serving != t:
+                self._c.wait()
+        return self
+
+    def __exit__(self, *exc):
+        with self._c:
+            self._serving += 1
+            self._c.notify_all()
+
+
 class Sphereflake:
     """Drop-in for the reference class. Owns a device context (G-buffer in HBM)."""
 
@@ -310,9 +334,10 @@ class Sphereflake:
         self._ctx = h
         self._worker = None
         self._stop = threading.Event()
-        self._mutex = threading.Lock()
+        self._mutex = _FifoLock()
         self._seed = 0
         self._counter = 0
+        self._view_change = 0
         self._worker_error = None
 
     # lifetime --------------------------------------------------------------
@@ -345,7 +370,15 @@ class Sphereflake:
     # view ------------------------------------------------------------------
     def SetView(self, origin, topLeft, topRight, bottomLeft):
         o, tl, tr, bl = (_f32(v, 3) for v in (origin, topLeft, topRight, bottomLeft))
-        _check(lib().sf_set_view(self._ctx, _fp(o), _fp(tl), _fp(tr), _fp(bl)), "SetView", self._ctx)
+        with self._mutex:   # (the frame-less loop's batches read the view)
+            _check(lib().sf_set_view(self._ctx, _fp(o), _fp(tl), _fp(tr), _fp(bl)), "SetView", self._ctx)
+            self._view_change = self._counter
+
+    def GetViewChangePacket(self) -> int:
+        """The frame-less loop's packet counter when the last SetView took effect (batches from it on trace
+        the new view)."""
+        with self._mutex:
+            return self._view_change
 
     def SetCamera(self, cam: Camera):
         o, tl, tr, bl = cam.corners()

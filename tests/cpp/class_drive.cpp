@@ -8,6 +8,13 @@
 //   also runs the headless SSAO chain as main.cpp:312-330 does (radius from GetClosestSphereDistance,
 //   camera = origin) and writes the RGBA8 image.
 //
+// usage: class_drive --initialize-moving W H views.bin out.bin seed batch ms period_us log.txt
+//   the frame-less loop under a moving view (main.cpp:304 calls SetView every frame while the workers
+//   trace): views.bin holds V views (12 float32 each: origin, TL, TR, BL); view 0 is set before
+//   Initialize, then view j % V every period_us. Each SetView's latency is measured; log.txt gets one line
+//   "view packet" per call (the loop's counter when it took effect). Prints
+//   "packets max_depth rays calls max_latency_us elapsed_us".
+//
 // usage: class_drive --initialize W H corners(12) out.bin seed batch ms
 //   the frame-less mode as main.cpp:120-121 starts it: SetView, Initialize(seed, batch), let the loop run
 //   `ms` milliseconds (reading GetGBuffer meanwhile, as the render loop does), Deinitialize; writes the
@@ -20,6 +27,7 @@
 #include <cstring>
 #include <exception>
 #include <thread>
+#include <vector>
 
 #include "Sphereflake.hpp"
 
@@ -62,8 +70,73 @@ static int initialize_mode(int argc, char** argv)
     return 0;
 }
 
+static int moving_mode(int argc, char** argv)
+{
+    if (argc < 11) return 2;
+    const size_t W = std::strtoul(argv[2], nullptr, 10), H = std::strtoul(argv[3], nullptr, 10);
+    std::vector<float> views;
+    {
+        FILE* f = std::fopen(argv[4], "rb");
+        if (!f) return 4;
+        float v[12];
+        while (std::fread(v, sizeof v, 1, f) == 1) views.insert(views.end(), v, v + 12);
+        std::fclose(f);
+    }
+    const size_t V = views.size() / 12;
+    if (V == 0) return 2;
+    const uint32_t seed = (uint32_t)std::strtoul(argv[6], nullptr, 0);
+    const uint32_t batch = (uint32_t)std::strtoul(argv[7], nullptr, 0);
+    const int ms = std::atoi(argv[8]);
+    const int period_us = std::atoi(argv[9]);
+    auto set_view = [&](Sphereflake& fl, size_t j) {
+        const float* v = &views[12 * j];
+        fl.SetView(sf_vec3(v[0], v[1], v[2]), sf_vec3(v[3], v[4], v[5]), sf_vec3(v[6], v[7], v[8]),
+                   sf_vec3(v[9], v[10], v[11]));
+    };
+    Sphereflake flake(W, H);
+    set_view(flake, 0);
+    FILE* log = std::fopen(argv[10], "w");
+    if (!log) return 4;
+    std::fprintf(log, "0 0\n");
+    flake.Initialize(seed, batch);
+    const auto t0 = std::chrono::steady_clock::now();
+    double max_lat = 0.0;
+    size_t calls = 0;
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(ms)) {
+        std::this_thread::sleep_for(std::chrono::microseconds(period_us));
+        const size_t j = (calls + 1) % V;
+        const auto c0 = std::chrono::steady_clock::now();
+        set_view(flake, j);
+        const double lat = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c0).count();
+        max_lat = lat > max_lat ? lat : max_lat;
+        std::fprintf(log, "%zu %llu\n", j, (unsigned long long)flake.GetViewChangePacket());
+        ++calls;
+    }
+    flake.Deinitialize();
+    const double elapsed = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    std::fclose(log);
+    const uint64_t packets = flake.GetPacketsTraced();
+    const GBuffer& g = flake.GetGBuffer();
+    FILE* out = std::fopen(argv[5], "wb");
+    if (!out) return 4;
+    std::fwrite(g.positions.data(), sizeof(sf_vec4), g.positions.size(), out);
+    std::fwrite(g.normals.data(), sizeof(sf_vec4), g.normals.size(), out);
+    std::fclose(out);
+    std::printf("%llu %d %lld %zu %.1f %.1f\n", (unsigned long long)packets, flake.GetMaxDepthReached(),
+                flake.GetRaysPerSecond(), calls, max_lat, elapsed);
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
+    if (argc > 1 && std::strcmp(argv[1], "--initialize-moving") == 0) {
+        try {
+            return moving_mode(argc, argv);
+        } catch (const std::exception& e) {
+            std::fprintf(stderr, "%s\n", e.what());
+            return 1;
+        }
+    }
     if (argc > 1 && std::strncmp(argv[1], "--initialize", 12) == 0) {
         try {
             return initialize_mode(argc, argv);

@@ -106,3 +106,87 @@ def test_python_initialize_error_surfaces():
         time.sleep(0.1)
         with pytest.raises(RuntimeError, match="frame-less loop failed"):
             s.Deinitialize()
+
+
+# ---- the loop under a moving view (main.cpp:304 calls SetView every frame while the workers trace,
+# Sphereflake.cpp:76-84): SetView is served within a batch, and the frame equals sequential batches
+# with the views switched at the packet counters the loop recorded
+WM, HM, BATCH_M = 640, 360, 1 << 16
+
+
+def moving_views(n=6):
+    out = []
+    for j in range(n):
+        cam = sf.config_camera(WM, HM, K)
+        cam.SetYaw(np.float32(sf.DEFAULT_YAW + 0.02 * (j - n // 2)))
+        out.append(cam.corners())
+    return out
+
+
+def replay_moving(views, log, packets):
+    """Sequential sf_progressive batches with view j from the first batch whose counter >= its packet."""
+    assert packets % BATCH_M == 0
+    with sf.Sphereflake(WM, HM) as s:
+        cur = None
+        for k in range(packets // BATCH_M):
+            j = [v for v, c in log if c <= k * BATCH_M][-1]
+            if j != cur:
+                s.SetView(*views[j])
+                cur = j
+            s.Progressive(SEED, BATCH_M, k * BATCH_M)
+        pos, nrm, _, _ = s.download()
+    return pos, nrm
+
+
+def test_cpp_initialize_moving_view(tmp_path):
+    views = moving_views()
+    vf = tmp_path / "views.bin"
+    np.asarray([np.concatenate(v) for v in views], np.float32).tofile(vf)
+    out, logf = tmp_path / "mv.bin", tmp_path / "log.txt"
+    r = subprocess.run([DRIVE, "--initialize-moving", str(WM), str(HM), str(vf), str(out), str(SEED),
+                        str(BATCH_M), "250", "2000", str(logf)], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr
+    f = r.stdout.split()
+    packets, rays, calls = int(f[0]), int(f[2]), int(f[3])
+    max_lat_us, elapsed_us = float(f[4]), float(f[5])
+    batches = packets // BATCH_M
+    assert batches >= 4 and calls >= 20, r.stdout
+    assert rays == 8 * packets
+    batch_us = elapsed_us / batches
+    # a SetView waits for at most the batch in flight (FIFO lock), plus host scheduling slack
+    assert max_lat_us <= 2.0 * batch_us + 2000.0, (max_lat_us, batch_us)
+    log = [tuple(int(x) for x in line.split()) for line in logf.read_text().split("\n") if line]
+    assert len(log) == calls + 1
+    assert len({c for _, c in log}) >= 4   # the view really changed between batches
+    g = np.fromfile(out, np.float32).reshape(2, HM, WM, 4)
+    pos, nrm = replay_moving(views, log, packets)
+    assert np.array_equal(g[0].view(np.uint32), pos.view(np.uint32))
+    assert np.array_equal(g[1].view(np.uint32), nrm.view(np.uint32))
+
+
+def test_python_initialize_moving_view():
+    views = moving_views()
+    log = [(0, 0)]
+    lat = []
+    with sf.Sphereflake(WM, HM) as s:
+        s.SetView(*views[0])
+        s.Initialize(SEED, batch=BATCH_M)
+        t0 = time.time()
+        j = 0
+        while time.time() - t0 < 0.25:
+            time.sleep(0.002)
+            j = (j + 1) % len(views)
+            c0 = time.perf_counter()
+            s.SetView(*views[j])
+            lat.append(time.perf_counter() - c0)
+            log.append((j, s.GetViewChangePacket()))
+        s.Deinitialize()
+        elapsed = time.time() - t0
+        packets = s.GetPacketsTraced()
+        pos, nrm, _, _ = s.download()
+    batches = packets // BATCH_M
+    assert batches >= 4 and len({c for _, c in log}) >= 4
+    assert max(lat) <= 2.0 * elapsed / batches + 0.005, (max(lat), elapsed / batches)
+    p2, n2 = replay_moving(views, log, packets)
+    assert np.array_equal(pos.view(np.uint32), p2.view(np.uint32))
+    assert np.array_equal(nrm.view(np.uint32), n2.view(np.uint32))
