@@ -275,6 +275,10 @@ int sf_set_kernel_timing(sf_ctx* ctx, int enable);
 /* Durations (ms) of the main trace kernel of the last min(n, 64) timed renders, oldest first;
    returns how many were written (>= 0) or a negative SF_E*. Synchronises. */
 int sf_kernel_times(sf_ctx* ctx, float* ms, uint32_t n);
+/* Live shader clock (MHz) of the same timed renders, oldest first: per render the median over the first
+   wave of 8 workgroups of delta s_memtime / delta s_memrealtime x 100 MHz across that wave's life in the
+   trace kernel (it runs for nearly the whole kernel). Returns how many were written; synchronises. */
+int sf_kernel_clocks(sf_ctx* ctx, float* mhz, uint32_t n);
 
 /* --- multi-GPU ------------------------------------------ */
 /* One process, n member devices (the reference's host thread pool, Sphereflake.cpp:67-74, becomes n
@@ -309,6 +313,8 @@ void* sf_context_stream(sf_ctx* ctx);
 const char* sf_strerror(int status);
 int sf_last_hip_error(const sf_ctx* ctx);
 int sf_abi_version(void);
+/* Hash of the sources this library was built from (scripts/source_hash.py): ties a measurement to a build. */
+const char* sf_build_id(void);
 int sf_device_count(void);
 
 #ifdef __cplusplus

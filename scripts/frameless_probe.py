@@ -27,9 +27,8 @@ with sf.Sphereflake(W, H) as s:
         s.Progressive(12345, B)
         s.Synchronize()
         s.tile_trace()
-        raw = s.raw_trace.astype(np.int64)
         waves = B // 8
-        wr = raw[:2 * waves].reshape(waves, 2)
+        wr = s.wave_trace[:waves].astype(np.int64)
         t0 = wr[:, 0].min()
         st, en = (wr[:, 0] - t0) / 100.0, (wr[:, 1] - t0) / 100.0
         du = en - st

@@ -50,16 +50,14 @@ with _Ctx(W, H) as s:
     print(f"  last traced render: heaviest tiles us {np.round(dur[top], 1)} starting at {np.round(st[top], 2)}; "
           f"tiles still starting after 20 us: {(st > 20).sum()}; mean tile {dur.mean():.2f} us")
     if os.environ.get("SF_FLAGS"):   # SF_FLAGS=0x20: per-wave {start, end} records
-        raw = s.raw_trace.astype(np.int64)
-        nw = int(os.environ.get("SF_PROBE_WAVES", "7168"))
-        wr = raw[len(raw) - 2 * nw:].reshape(nw, 2)
+        wr = s.wave_trace.astype(np.int64)
         wr = wr[wr[:, 0] > 0]
         t0 = tr[:, 0].min()
         print(f"  waves {len(wr)}: first wave start {(wr[:, 0].min() - t0) / 100:.2f} us, last wave start "
               f"{(wr[:, 0].max() - t0) / 100:.2f}, last wave end {(wr[:, 1].max() - t0) / 100:.2f} (tile times from first tile start)")
     if order is not None:   # where the last traced render's heaviest tiles sat in the order it used
         pos = np.full(len(dur), -1)
-        u = order[0] & ((1 << 29) - 1)
+        u = order[0] & ((1 << 27) - 1)
         pos[u[::-1]] = np.arange(len(u))[::-1]
         print(f"  order positions of the 5 heaviest tiles: {pos[top]} (moving camera: {MOVING})")
     ends = np.sort((tr[:, 1] - tr[:, 0].min()) / 100.0)

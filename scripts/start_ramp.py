@@ -24,7 +24,7 @@ with sf.Sphereflake(W, H) as s:
 t0 = tr[:, 0].min()
 start = (tr[:, 0] - t0) / 100.0
 end = (tr[:, 1] - t0) / 100.0
-tiles = units & ((1 << 29) - 1)
+tiles = units & ((1 << 27) - 1)
 st = start[tiles]
 for a, b in ((0, 8), (8, 64), (64, 256), (256, 1024), (1024, 4096), (4096, 7168), (7168, 8192)):
     print(f"order [{a:5d},{b:5d}): start us min {st[a:b].min():6.2f} median {np.median(st[a:b]):6.2f} max {st[a:b].max():6.2f}")

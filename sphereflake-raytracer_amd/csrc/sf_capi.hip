@@ -14,6 +14,7 @@
 #include <new>
 #include <utility>
 
+#include "sf_build_id.h"   // SF_SOURCE_HASH (generated: build/, scripts/source_hash.py)
 #include "sf_internal.h"
 #include "sphereflake/sf.h"
 
@@ -194,6 +195,7 @@ struct sf_ctx {
     // Measurement: HIP events around the main trace kernel of each render (sf_set_kernel_timing)
     static constexpr int kTimed = 64;
     hipEvent_t ev[kTimed][2] = {};
+    uint64_t* clock_buf = nullptr;     // per timed render slot: SF_CLOCK_WAVES x {memtime, realtime} at start / end
     bool timing = false;
     uint32_t ev_next = 0, ev_count = 0;
     uint32_t ev_period = 1, ev_phase = 0;   // time every ev_period-th render
@@ -291,6 +293,7 @@ static void free_ctx(sf_ctx* c)
     for (int i = 0; i < sf_ctx::kTimed; ++i)
         for (int j = 0; j < 2; ++j)
             if (c->ev[i][j]) (void)hipEventDestroy(c->ev[i][j]);
+    (void)hipFree(c->clock_buf);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -330,6 +333,8 @@ static int reset_stats_dev(sf_ctx* c, int which)
 extern "C" {
 
 int sf_abi_version(void) { return SF_ABI_VERSION; }
+
+const char* sf_build_id(void) { return SF_SOURCE_HASH; }
 
 int sf_device_count(void)
 {
@@ -417,6 +422,10 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     DevGuard g(device);
     const size_t npx = (size_t)width * height;
     const size_t ntiles = (size_t)((width + 7) / 8) * ((height + 7) / 8);
+    if (ntiles > (size_t)SF_UNIT_TILE_MASK + 1u) {   // a work unit holds the tile index in 27 bits
+        delete c;
+        return SF_EINVAL;
+    }
     auto fail = [&](hipError_t e) {
         c->last_hip = (int)e;
         free_ctx(c);
@@ -634,10 +643,14 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             if (nblk > need) nblk = need;
             if (c->max_blocks && nblk > c->max_blocks) nblk = c->max_blocks;
             const dim3 grid(nblk);
+            // every queue group needs blocks of its own (the group is blockIdx mod xcds): fewer queues for a
+            // grid of fewer blocks than groups
+            while (a.xcds > 1u && a.xcds > nblk) a.xcds >>= 1;
+            a.queues = a.xcds;
             // several queues per XCD split each XCD's tickets over as many counters (less contention on
             // each); every queue needs waves of its own, so only with a full grid (>= 64 waves per queue)
-            if (c->queues_per_xcd > 1u && nblk * wpb >= 64u * c->queues * c->queues_per_xcd)
-                a.queues = c->queues * c->queues_per_xcd;
+            if (c->queues_per_xcd > 1u && nblk * wpb >= 64u * a.xcds * c->queues_per_xcd)
+                a.queues = a.xcds * c->queues_per_xcd;
             // the order is rebuilt after every order_every-th render (and whenever none exists for this frame
             // size); the renders in between keep the last order and record their tile costs only
             // Small frames (tiles fill the persistent grid less than twice) are latency-bound: there the stale
@@ -658,7 +671,10 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             }
             const bool timed = c->timing && c->ev_phase == 0;
             if (c->timing) c->ev_phase = (c->ev_phase + 1u) % c->ev_period;
-            if (timed) SF_HIP(c, hipEventRecord(c->ev[c->ev_next][0], s));
+            if (timed) {
+                SF_HIP(c, hipEventRecord(c->ev[c->ev_next][0], s));
+                a.clock_probe = c->clock_buf + (size_t)c->ev_next * SF_CLOCK_WAVES * 4u;
+            }
             // small frames (tiles fill the persistent grid less than twice) are latency-bound: the heaviest
             // tiles' serial DFS is the frame, and the pipelined child loop shortens it (640x360 -4 %); full
             // grids are throughput-bound, where it costs more instructions than it hides (1080p +1.7 %)
@@ -1119,9 +1135,10 @@ int sf_set_tile_trace(sf_ctx* c, int enable)
     }
     if (!c->tile_trace) {
         const size_t ntiles = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8);
-        // per tile {start, end, id}, the diagnostic slots, per work unit {start, end, unit} (<= 4 per tile)
-        SF_HIP(c, hipMalloc(&c->tile_trace, (ntiles * 15 + SF_DIAG_SLOTS) * 8));
-        SF_HIP(c, hipMemset(c->tile_trace, 0, (ntiles * 15 + SF_DIAG_SLOTS) * 8));
+        // per tile {start, end, id}, the diagnostic slots, per work unit {start, end, unit} (<= 4 per tile),
+        // per wave {start, end}
+        SF_HIP(c, hipMalloc(&c->tile_trace, SF_TRACE_WORDS(ntiles) * 8));
+        SF_HIP(c, hipMemset(c->tile_trace, 0, SF_TRACE_WORDS(ntiles) * 8));
     }
     return SF_OK;
 }
@@ -1134,8 +1151,8 @@ int sf_get_tile_trace(sf_ctx* c, uint64_t* out, size_t n)
     if (n < ntiles * 3) return SF_EINVAL;
     if (int rc_ = ctx_drain(c)) return rc_;
     // n >= 3 * tiles + SF_DIAG_SLOTS also returns the segment sums / event counts of the diagnostic
-    // builds (zeros otherwise)
-    const size_t full = ntiles * 15 + SF_DIAG_SLOTS;
+    // builds (zeros otherwise); n >= SF_TRACE_WORDS(tiles) the per-unit and per-wave records too
+    const size_t full = SF_TRACE_WORDS(ntiles);
     SF_HIP(c, hipMemcpy(out, c->tile_trace, (n >= full ? full : n >= ntiles * 3 + SF_DIAG_SLOTS ? ntiles * 3 + SF_DIAG_SLOTS : ntiles * 3) * 8,
                         hipMemcpyDeviceToHost));
     return SF_OK;
@@ -1176,6 +1193,9 @@ int sf_set_kernel_timing(sf_ctx* c, int enable)
     if (enable && !c->ev[0][0]) {
         for (int i = 0; i < sf_ctx::kTimed; ++i)
             for (int j = 0; j < 2; ++j) SF_HIP(c, hipEventCreate(&c->ev[i][j]));
+        const size_t cb = (size_t)sf_ctx::kTimed * SF_CLOCK_WAVES * 4u * 8u;
+        SF_HIP(c, hipMalloc(&c->clock_buf, cb));
+        SF_HIP(c, hipMemset(c->clock_buf, 0, cb));
     }
     if (enable < 0) return SF_EINVAL;
     c->timing = enable != 0;
@@ -1194,6 +1214,31 @@ int sf_kernel_times(sf_ctx* c, float* ms, uint32_t n)
         const uint32_t slot = (c->ev_next + sf_ctx::kTimed - k + i) % sf_ctx::kTimed;
         SF_HIP(c, hipEventSynchronize(c->ev[slot][1]));
         SF_HIP(c, hipEventElapsedTime(&ms[i], c->ev[slot][0], c->ev[slot][1]));
+    }
+    return (int)k;
+}
+
+int sf_kernel_clocks(sf_ctx* c, float* mhz, uint32_t n)
+{
+    if (!c || !mhz) return SF_EINVAL;
+    DevGuard g(c->device);
+    if (int rc_ = ctx_drain(c)) return rc_;
+    const uint32_t k = n < c->ev_count ? n : c->ev_count;
+    if (k == 0 || !c->clock_buf) return 0;
+    static_assert(SF_CLOCK_WAVES == 8u, "median below assumes 8 records");
+    uint64_t rec[SF_CLOCK_WAVES * 4];
+    for (uint32_t i = 0; i < k; ++i) {   // the k most recent timed renders, oldest first (as sf_kernel_times)
+        const uint32_t slot = (c->ev_next + sf_ctx::kTimed - k + i) % sf_ctx::kTimed;
+        SF_HIP(c, hipMemcpy(rec, c->clock_buf + (size_t)slot * SF_CLOCK_WAVES * 4u, sizeof rec, hipMemcpyDeviceToHost));
+        float v[SF_CLOCK_WAVES];
+        uint32_t m = 0;
+        for (uint32_t w = 0; w < SF_CLOCK_WAVES; ++w) {
+            const uint64_t* r = rec + 4u * w;
+            if (r[3] > r[1] && r[2] > r[0]) v[m++] = (float)((double)(r[2] - r[0]) / (double)(r[3] - r[1]) * 100.0);
+        }
+        for (uint32_t a = 1; a < m; ++a)   // (insertion sort of <= 8 values)
+            for (uint32_t b = a; b > 0 && v[b - 1] > v[b]; --b) std::swap(v[b - 1], v[b]);
+        mhz[i] = m ? (m & 1u ? v[m / 2] : 0.5f * (v[m / 2 - 1] + v[m / 2])) : 0.0f;
     }
     return (int)k;
 }

@@ -42,6 +42,12 @@
 
 // 64-bit diagnostic slots after the per-tile trace (segment sums of PHASES=1, event counts of COUNTS=1)
 #define SF_DIAG_SLOTS 16
+// per-wave {start, end} records (SF_FLAG_DIAG_UNITS) after the per-tile and per-unit records: waves past
+// this many are not recorded
+#define SF_DIAG_WAVES 65536u
+// tile trace buffer (u64): per tile {start, end, id}, the diagnostic slots, per work unit {start, end,
+// unit} (<= 4 units per tile), per wave {start, end}
+#define SF_TRACE_WORDS(ntiles) ((size_t)(ntiles) * 15u + SF_DIAG_SLOTS + 2u * SF_DIAG_WAVES)
 
 #define SF_FLAG_NO_LOD_CULL 1u    // disable the leaf-threshold skip (A/B only; results identical)
 #define SF_FLAG_NO_CONE_CULL 2u   // disable the per-child ray-cone cull (A/B only; results identical)
@@ -120,7 +126,10 @@ struct FrameArgs {
     uint32_t xcds;                    // persistent trace: XCD queue groups (power of 2); queue k serves XCD k % xcds
     uint32_t* bin_cost;               // frame-less mode (NULL = off): per packet bin, cycles of the last wave starting in it
     uint32_t bin_shift, bins_x;       // frame-less mode: the batch's packet bins (squares of 2^bin_shift pixels)
+    uint64_t* clock_probe;            // measurement (NULL = off): the first wave of blocks 0..SF_CLOCK_WAVES-1
+                                      // writes {s_memtime, s_memrealtime} at its start and at its end
 };
+#define SF_CLOCK_WAVES 8u             // live shader clock samples per timed render (one per XCD group)
 
 // Headless SSAO post-process (Shaders/post_ssao.glsl, post_ssao_blur.glsl,
 // post_final.glsl, SSAO.cpp:106-142). Textures are modelled, not emulated: NEAREST/LINEAR filtering
@@ -152,12 +161,16 @@ struct PostArgs {
 #define SF_PROG_BIN_MIN 65536u         // frame-less batches below this many packets trace in draw order
                                        // (binning pays once the batch is several waves per slot)
 #define SF_ORDER_BUCKETS 32u           // log-spaced cost buckets of sf_tile_order (2 per octave from 2^8 cycles)
-// A work unit of the tile order: tile index | part << SF_UNIT_PART_SHIFT. Part 0 = the whole 8x8 tile;
+// A work unit of the tile order: tile index | prio << SF_UNIT_PRIO_SHIFT | part << SF_UNIT_PART_SHIFT.
+// prio (written by sf_order_scatter from the unit's cost bucket, so the trace reads no cost table the same
+// launch rewrites): 0 normal, 1 raised (the lowest 3 of the top order_meta[3].. buckets, s_setprio 2),
+// 2 raised high (the buckets above, s_setprio 3). Part 0 = the whole 8x8 tile;
 // 1, 2 = its pixel rows 0-3 / 4-7 (halves); 3..6 = its 4x4 quarters (q = part - 3: rows 4 (q >> 1).., columns
 // 4 (q & 1)..). The heaviest tiles are traced as 2 or 4 part units by as many waves: a tile's serial DFS
 // otherwise bounds the frame.
 #define SF_UNIT_PART_SHIFT 29u
-#define SF_UNIT_TILE_MASK ((1u << SF_UNIT_PART_SHIFT) - 1u)
+#define SF_UNIT_PRIO_SHIFT 27u
+#define SF_UNIT_TILE_MASK ((1u << SF_UNIT_PRIO_SHIFT) - 1u)   // frames of up to 2^27 8x8 tiles
 #define SF_PART_HALF0 1u
 #define SF_PART_QUARTER0 3u
 // Which tiles are split: env SF_SPLIT_BUCKETS = k splits the top k occupied cost buckets (at most an

@@ -1067,6 +1067,14 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
     extern __shared__ float lds[];
     const uint64_t w_start = __builtin_amdgcn_s_memrealtime();
     const uint32_t wv = threadIdx.x >> 6;
+    // measurement: the live shader clock, delta s_memtime / delta s_memrealtime x 100 MHz over this wave's
+    // life (the start pair stored now, so nothing stays live across the tile loop; uniform values and
+    // addresses; read by sf_kernel_clocks, never by a kernel)
+    if (a.clock_probe && wv == 0u && blockIdx.x < SF_CLOCK_WAVES) {
+        uint64_t* cp = a.clock_probe + 4u * blockIdx.x;
+        cp[0] = __builtin_amdgcn_s_memtime();
+        cp[1] = w_start;
+    }
     // a.queues (<= SF_QUEUES) tile queues per render, one cache line each: queue k hands out the units
     // after the static first ones with index = k mod a.queues
     // A wave starts on its own XCD's queue and moves on to the next one when it runs dry. One queue
@@ -1088,17 +1096,17 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 #endif
     }
     stage_root(L, a.root);
-    uint32_t xcc;
-    __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    // One queue per XCD (a.queues of them); a wave drains its own XCD's queue and then exits. Stealing
+    // One queue per XCD (a.queues of them); a wave drains its own group's queue and then exits. Stealing
     // from the other queues once the own one ran dry cost every wave up to 7 more atomics on queue words
     // contended chip-wide at the end of the frame: the last wave exited ~60 us after the last tile
-    // ended. Every queue still drains: its XCD's waves only leave when it is empty, and queue units exist
-    // only when the grid is the full persistent grid, which spans every XCD.
+    // ended. Every queue still drains: its group's waves only leave when it is empty.
     const uint32_t nq = a.queues, nx = a.xcds;
-    // queue k = XCD group (k % nx) + nx x sub-queue; an XCD's waves spread over its nq / nx sub-queues by
-    // their position in the grid (blocks go round-robin over the XCDs)
-    uint32_t k = __builtin_amdgcn_readfirstlane(xcc) & (nx - 1u);
+    // queue k = block group (k % nx) + nx x sub-queue; a group's waves spread over its nq / nx sub-queues by
+    // their position in the grid. The group is blockIdx mod nx, not the XCD id: blocks are observed to be
+    // dealt round-robin over the XCDs, so a group is one XCD's blocks (its queue word stays in that XCD's
+    // traffic), but every group has waves whatever the placement (a CU-masked stream, a partitioned chip):
+    // the host keeps nx <= the grid's blocks, so every queue drains.
+    uint32_t k = blockIdx.x & (nx - 1u);
     if (nq > nx) {   // (powers of two: shifts, no division)
         const uint32_t lx = __builtin_ctz(nx);
         k += nx * (((blockIdx.x >> lx) * WAVES + wv) & ((nq >> lx) - 1u));
@@ -1140,23 +1148,14 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 #endif
             t = u & SF_UNIT_TILE_MASK;
             part = u >> SF_UNIT_PART_SHIFT;
-        }
-        if (at.tile_order) {
             // critical-path tiles (top cost buckets of the last render, order_meta[3]) at raised priority:
-            // the SIMD's issue arbitration serves them first, the cheap tiles absorb the wait
-#if defined(__HIP_DEVICE_COMPILE__)
-            typedef const __attribute__((address_space(4))) uint32_t* ConstU32;
-            const uint32_t pb = ((ConstU32)(const void*)at.order_meta)[3];
-            const uint32_t prev = ((ConstU32)(const void*)at.tile_cost)[t];
-#else
-            const uint32_t pb = at.order_meta[3], prev = at.tile_cost[t];
-#endif
-            // graded: the raised buckets' lowest 3 (1.5 octaves) at 2, the ones above at 3, so the very
-            // heaviest tiles also win the arbitration against the merely heavy (8 buckets: 0.1607 -> 0.1578
-            // ms/frame against all raised buckets at one level)
-            const uint32_t cb = cost_bucket(prev);
-            if (!(at.flags & SF_FLAG_PRIO_FLAT) && cb >= pb + 3u) __builtin_amdgcn_s_setprio(3);
-            else if (cb >= pb) __builtin_amdgcn_s_setprio(2);
+            // the SIMD's issue arbitration serves them first, the cheap tiles absorb the wait. Graded: the
+            // raised buckets' lowest 3 (1.5 octaves) at 2, the ones above at 3, so the very heaviest tiles
+            // also win the arbitration against the merely heavy (8 buckets: 0.1607 -> 0.1578 ms/frame against
+            // all raised buckets at one level). The level comes with the unit (sf_order_scatter).
+            const uint32_t pr = (u >> SF_UNIT_PRIO_SHIFT) & 3u;
+            if (pr == 2u && !(at.flags & SF_FLAG_PRIO_FLAT)) __builtin_amdgcn_s_setprio(3);
+            else if (pr != 0u) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(0);
         }
         const uint64_t u_start = (at.flags & SF_FLAG_DIAG_UNITS) ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -1177,12 +1176,32 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
         maxd = st.maxd > maxd ? st.maxd : maxd;
         closest = fminf(closest, st.closest);
     }
-    publish_stats(a, maxd, closest, 0u);
-    if ((a.flags & SF_FLAG_DIAG_UNITS) && a.tile_trace) {   // diagnostics: this wave's {start, end}, at the buffer's end
-        uint64_t* wt = a.tile_trace + 15u * (a.tiles_x * a.tile_rows) + SF_DIAG_SLOTS - 2u * nwaves
-                       + 2u * __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + wv);
-        wt[0] = w_start;
-        wt[1] = __builtin_amdgcn_s_memrealtime();
+    // the launch arguments again from the kernarg segment, so that none of them is held in a register
+    // across the tile loop for the code below
+    FrameArgs e;
+#if defined(__HIP_DEVICE_COMPILE__)
+    {
+        typedef const __attribute__((address_space(4))) FrameArgs* KernargArgs;
+        KernargArgs pa = (KernargArgs)__builtin_amdgcn_kernarg_segment_ptr();
+        __asm__ volatile("" : "+s"(pa));
+        __builtin_memcpy(&e, (const FrameArgs*)pa, sizeof(FrameArgs));
+    }
+#else
+    e = a;
+#endif
+    publish_stats(e, maxd, closest, 0u);
+    if (e.clock_probe && wv == 0u && blockIdx.x < SF_CLOCK_WAVES) {   // measurement: the end pair (see above)
+        uint64_t* cp = e.clock_probe + 4u * blockIdx.x;
+        cp[2] = __builtin_amdgcn_s_memtime();
+        cp[3] = __builtin_amdgcn_s_memrealtime();
+    }
+    if ((e.flags & SF_FLAG_DIAG_UNITS) && e.tile_trace) {   // diagnostics: this wave's {start, end}
+        const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + wv);
+        if (w < SF_DIAG_WAVES) {
+            uint64_t* wt = e.tile_trace + (SF_TRACE_WORDS(e.tiles_x * e.tile_rows) - 2u * SF_DIAG_WAVES) + 2u * w;
+            wt[0] = w_start;
+            wt[1] = __builtin_amdgcn_s_memrealtime();
+        }
     }
 }
 
@@ -1328,7 +1347,7 @@ extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t
 {
     // (rank_out, when not NULL: rank_out[i] = item i's position, the inverse permutation; unsplit orders only)
     const uint32_t c = blockIdx.x, lane = threadIdx.x, i = c * 64u + lane;
-    const uint32_t split_from = order_meta[1], parts = order_meta[2];
+    const uint32_t split_from = order_meta[1], parts = order_meta[2], pb = order_meta[3];
     const uint32_t first = parts == 4u ? SF_PART_QUARTER0 : SF_PART_HALF0;
     const uint32_t bk = i < n ? cost_bucket(cost[i]) : SF_ORDER_BUCKETS;   // sentinel: no tile
     const uint32_t offs = chunk_off[c * SF_ORDER_BUCKETS + (lane & (SF_ORDER_BUCKETS - 1u))];   // lane b: bucket b
@@ -1339,10 +1358,12 @@ extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t
         const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)offs, (int)b);
         if (bk == b) {
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            // the unit's wave priority next render (see SF_UNIT_PRIO_SHIFT)
+            const uint32_t u = i | ((b >= pb + 3u ? 2u : b >= pb ? 1u : 0u) << SF_UNIT_PRIO_SHIFT);
             if (b >= split_from) {   // `parts` part units, adjacent
-                for (uint32_t p = 0; p < parts; ++p) order[off + parts * rank + p] = i | ((first + p) << SF_UNIT_PART_SHIFT);
+                for (uint32_t p = 0; p < parts; ++p) order[off + parts * rank + p] = u | ((first + p) << SF_UNIT_PART_SHIFT);
             } else {
-                order[off + rank] = i;
+                order[off + rank] = u;
                 if (rank_out) rank_out[i] = off + rank;
             }
         }
@@ -1774,9 +1795,11 @@ __device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint
         const uint32_t c32 = cyc > 0x7fffffffull ? 0x7fffffffu : ((uint32_t)cyc | 1u);
         a.bin_cost[b] = 1u << ((31u - (uint32_t)__builtin_clz(c32)) & ~1u);
     }
-    if ((a.flags & SF_FLAG_DIAG_UNITS) && a.tile_trace) {   // diagnostics: this wave's {start, end}
-        a.tile_trace[2u * wave] = w_start;
-        a.tile_trace[2u * wave + 1u] = __builtin_amdgcn_s_memrealtime();
+    if ((a.flags & SF_FLAG_DIAG_UNITS) && a.tile_trace && wave < SF_DIAG_WAVES) {   // diagnostics: this wave's
+        // {start, end}, in the per-wave records of the context's trace buffer (sf_set_tile_trace)
+        uint64_t* wt = a.tile_trace + (SF_TRACE_WORDS((uint64_t)((a.W + 7u) / 8u) * ((a.H + 7u) / 8u)) - 2u * SF_DIAG_WAVES);
+        wt[2u * wave] = w_start;
+        wt[2u * wave + 1u] = __builtin_amdgcn_s_memrealtime();
     }
 }
 

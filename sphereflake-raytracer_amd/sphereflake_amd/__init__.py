@@ -37,6 +37,7 @@ FLT_MAX = float(np.finfo(np.float32).max)
 DEFAULT_CAMERA_POSITION = (-5.4098, -7.2139, 1.19006)
 DEFAULT_PITCH = -1.371
 DEFAULT_YAW = 0.921999
+SF_DIAG_WAVES = 65536            # per-wave diagnostic records (sf_internal.h)
 
 
 class SphereflakeError(RuntimeError):
@@ -122,9 +123,11 @@ SIGNATURES = {
                                          ctypes.c_size_t]),
     "sf_set_kernel_timing": (ctypes.c_int, [_CTX, ctypes.c_int]),
     "sf_kernel_times": (ctypes.c_int, [_CTX, _F, ctypes.c_uint32]),
+    "sf_kernel_clocks": (ctypes.c_int, [_CTX, _F, ctypes.c_uint32]),
     "sf_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "sf_last_hip_error": (ctypes.c_int, [_CTX]),
     "sf_abi_version": (ctypes.c_int, []),
+    "sf_build_id": (ctypes.c_char_p, []),
     "sf_device_count": (ctypes.c_int, []),
     "sf_context_stream": (ctypes.c_void_p, [_CTX]),
     "sf_group_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
@@ -174,6 +177,25 @@ def lib() -> ctypes.CDLL:
                 fn.argtypes = args
             _lib = L
     return _lib
+
+
+def build_info() -> dict:
+    """Which build is loaded: the source hash the library embeds (sf_build_id), the hash of the sources in
+    this tree (scripts/source_hash.py), whether they agree, and the SHA-256 of the library file itself."""
+    import hashlib
+    import importlib.util
+    with open(LIB_PATH, "rb") as f:
+        lib_sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    embedded = lib().sf_build_id().decode()
+    tree = None
+    sh = os.path.join(os.path.dirname(ROOT_DIR), "scripts", "source_hash.py")
+    if os.path.exists(sh):
+        spec = importlib.util.spec_from_file_location("_sf_source_hash", sh)
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        tree = m.source_hash()
+    return {"source_sha256": embedded, "tree_source_sha256": tree, "lib_matches_tree": embedded == tree,
+            "lib_sha256": lib_sha}
 
 
 def _strerror(code: int) -> str:
@@ -528,12 +550,13 @@ class Sphereflake:
             _check(lib().sf_set_tile_trace(self._ctx, int(bool(enable))), "sf_set_tile_trace", self._ctx)
             return None
         n = ((self.width + 7) // 8) * ((self.height + 7) // 8)
-        out = np.zeros(15 * n + 16, np.uint64)   # tiles, SF_DIAG_SLOTS, units (SF_FLAG_DIAG_UNITS)
+        # tiles, SF_DIAG_SLOTS, units and waves (SF_FLAG_DIAG_UNITS): SF_TRACE_WORDS (sf_internal.h)
+        out = np.zeros(15 * n + 16 + 2 * SF_DIAG_WAVES, np.uint64)
         _check(lib().sf_get_tile_trace(self._ctx, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), out.size),
                "sf_get_tile_trace", self._ctx)
         self.phase_sums = out[3 * n:3 * n + 16]   # segment cycle sums / event counts of diagnostic builds
-        self.unit_trace = out[3 * n + 16:].reshape(4 * n, 3)   # per order position (SF_FLAG_DIAG_UNITS)
-        self.raw_trace = out   # (SF_FLAG_DIAG_UNITS: per persistent wave {start, end} at the end of the buffer)
+        self.unit_trace = out[3 * n + 16:15 * n + 16].reshape(4 * n, 3)   # per order position (SF_FLAG_DIAG_UNITS)
+        self.wave_trace = out[15 * n + 16:].reshape(SF_DIAG_WAVES, 2)   # per wave {start, end} (SF_FLAG_DIAG_UNITS)
         return out[:3 * n].reshape(n, 3)
 
     def tile_order(self):
@@ -560,6 +583,14 @@ class Sphereflake:
         k = lib().sf_kernel_times(self._ctx, out.ctypes.data_as(_F), n)
         if k < 0:
             _check(k, "sf_kernel_times", self._ctx)
+        return out[:k]
+
+    def kernel_clocks(self, n: int = 64):
+        """Live shader clock (MHz) of the last n timed renders' trace kernels, oldest first (sf_kernel_clocks)."""
+        out = np.zeros(n, np.float32)
+        k = lib().sf_kernel_clocks(self._ctx, out.ctypes.data_as(_F), n)
+        if k < 0:
+            _check(k, "sf_kernel_clocks", self._ctx)
         return out[:k]
 
     # stats (Sphereflake.h:30-58) --------------------------------------------

@@ -342,7 +342,7 @@ def test_order_rebuilt_every_kth_render_bit_exact(monkeypatch, every):
             pos, nrm, _, _ = s.download()
             assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == [], f"render {k}"
             units, cost = s.tile_order()
-            tiles = units & ((1 << 29) - 1)
+            tiles = units & ((1 << 27) - 1)
             assert np.array_equal(np.unique(tiles), np.arange(n)), f"render {k}: order is not a permutation"
             if k % int(every) == 0:   # a rebuild render (0, k, 2k, ...): the order of its own costs
                 assert len(units) == n   # (14 400 tiles > the persistent grid's waves: no splits)
@@ -432,15 +432,20 @@ def cost_bucket(c):
     return np.where((b >= 0) & (b < 32), b, np.where(k < (135 << 1), 0, 31))
 
 
-def expected_units(cost, split_buckets, spare=0, parts=2):
+def expected_units(cost, split_buckets, spare=0, parts=2, prio_buckets=8):
     """Host restatement of sf_order_scan + sf_order_scatter: tiles stably sorted by cost bucket, heaviest
     first; split tiles become `parts` adjacent part units (halves tile | 1 << 29, tile | 2 << 29; quarters
     tile | 3..6 << 29). split_buckets None (auto): whole buckets from the heaviest while the extra units
     fit `spare` idle waves; k: the top k occupied buckets, at most an eighth of the tiles. Bucket 0 is
-    never split."""
+    never split. Every unit carries its wave priority at bit 27 (SF_UNIT_PRIO_SHIFT): of the top
+    `prio_buckets` buckets from the highest occupied one down, the lowest 3 get 1 and the ones above 2."""
     n = len(cost)
     bk = cost_bucket(cost)
     cnt = np.bincount(bk, minlength=32)
+    occ = np.nonzero(cnt)[0]
+    btop = int(occ[-1]) if len(occ) else 0
+    pb = 32 if prio_buckets == 0 else max(0, btop - prio_buckets + 1)
+    prio = lambda b: (2 if b >= pb + 3 else 1 if b >= pb else 0) << 27
     bs, nsplit = 32, 0
     if split_buckets is None:
         for b in range(31, 0, -1):
@@ -459,10 +464,11 @@ def expected_units(cost, split_buckets, spare=0, parts=2):
     first = 3 if parts == 4 else 1
     units = []
     for t in np.lexsort((np.arange(n), -bk)):
+        u = int(t) | prio(bk[t])
         if bk[t] >= bs:
-            units += [t | ((first + p) << 29) for p in range(parts)]
+            units += [u | ((first + p) << 29) for p in range(parts)]
         else:
-            units.append(t)
+            units.append(u)
     return np.array(units, np.uint32), nsplit
 
 
@@ -489,7 +495,7 @@ def test_tile_order_is_stable_heavy_first_schedule(W, H, split, parts, monkeypat
         exp, nsplit = expected_units(cost, split, parts=parts)
     assert np.array_equal(units, exp)
     assert len(units) == n + nsplit * (parts - 1)
-    tiles, part = units & ((1 << 29) - 1), units >> 29
+    tiles, part = units & ((1 << 27) - 1), units >> 29
     first = 3 if parts == 4 else 1
     assert np.array_equal(np.sort(tiles[(part == 0) | (part == first)]), np.arange(n, dtype=np.uint32))
     for p in range(1, parts):
@@ -612,3 +618,32 @@ def test_raised_priority_tiles_bit_exact(prio, monkeypatch):
             s.Render()
             pos, nrm, _, _ = s.download()
             assert frame_digest(pos, nrm) == fx["frame_digest"], prio
+        units, cost = s.tile_order()
+    lv = (units >> 27) & 3
+    assert np.array_equal(units, expected_units(cost, None, len(units) - len(cost), 4, int(prio))[0])
+    if prio == "0":
+        assert lv.max() == 0
+    elif prio == "32":
+        assert lv.min() >= 1 and lv.max() == 2
+    else:
+        assert 0 < np.count_nonzero(lv) < len(units)
+
+
+@pytest.mark.parametrize("blocks,nq", [("4", "8"), ("3", "8"), ("1", "8"), ("6", "4")])
+def test_tiny_grid_many_queues_bit_exact(blocks, nq, monkeypatch):
+    """A persistent grid of fewer blocks than tile queues (SF_MAX_BLOCKS below SF_NQUEUES, as a CU-masked
+    stream or a partitioned chip can give): the host drops to as many queue groups as the grid has blocks,
+    so every queue has waves and every unit is traced -- golden frames, first and heavy-first renders."""
+    monkeypatch.setenv("SF_MAX_BLOCKS", blocks)
+    monkeypatch.setenv("SF_NQUEUES", nq)
+    fx = load_frame("t3")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    exp = load_npz("t3")
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for _ in range(2):
+            s.Render(emit_aux=True)
+            pos, nrm, mint, idx = s.download(aux=True)
+            for k, got in (("pos4", pos), ("nrm4", nrm), ("minT", mint), ("index", idx)):
+                assert np.array_equal(np.ascontiguousarray(got).view(np.uint8),
+                                      np.ascontiguousarray(exp[k]).view(np.uint8)), (k, blocks, nq)
