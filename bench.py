@@ -86,8 +86,15 @@ def frame_camera(width, height, k, frame):
     return cam
 
 
-KTIMING_PERIOD = 10                  # HIP events on every 10th timed render
+KTIMING_PERIOD = 10                  # HIP events on every 10th timed render (fewer steps: denser, see ktiming_period)
+KTIMING_MIN_SAMPLES = 8              # at least this many kernel-timing samples per timed loop
 CPU_REPS = 40                        # ~1.2 s wall x 16 threads: ~20 s of CPU work
+
+
+def ktiming_period(steps):
+    """Every k-th timed render carries the kernel-timing events: k = 10 (an event pair costs ~7 us of stream
+    time per frame, so it is sampled), or less when that would give fewer than KTIMING_MIN_SAMPLES samples."""
+    return max(1, min(KTIMING_PERIOD, steps // KTIMING_MIN_SAMPLES))
 
 
 BASELINE_CONFIGS = {(640, 360, 1.0): "configs[0]", (1280, 720, 0.8): "configs[1]", (1920, 1080, 0.25): "configs[2]",
@@ -99,14 +106,17 @@ def pmc_config_key(width, height, k, camera):
     return f"{width}x{height} K={k:g} {camera}"
 
 
-def load_pmc(kernel, config_key):
+def load_pmc(kernel, config_key, build):
     """Per-dispatch PMC means of `kernel` from profiles/pmc_traffic.json -- only when that summary was
-    profiled on this very configuration (None otherwise: counters are never replayed onto another config)."""
+    profiled on this very configuration AND this very library build (its `build.lib_sha256`); None otherwise:
+    counters are never replayed onto another config or another build."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             j = json.load(f)
         if j.get("config") != config_key:
+            return None, None
+        if (j.get("build") or {}).get("lib_sha256") != build.get("lib_sha256"):
             return None, None
         return j["kernels"][kernel], j.get("source", path)
     except (OSError, KeyError, ValueError):
@@ -332,7 +342,7 @@ def run_rows(args, torch, dist, dist_on, rank, n, kernel):
         for i in range(args.warmup):
             g.SetView(*views[i])
             g.Render(band)
-        g.member_kernel_timing(0, True, period=KTIMING_PERIOD)
+        g.member_kernel_timing(0, True, period=ktiming_period(args.steps))
         g.Synchronize()
         g.reset_stats()
     if dist_on:
@@ -351,7 +361,7 @@ def run_rows(args, torch, dist, dist_on, rank, n, kernel):
     st = g.stats()
     if st.overflow_tiles:
         raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
-    tk = g.member_kernel_timing(0, n=min(-(-args.steps // KTIMING_PERIOD), 64))
+    tk = g.member_kernel_timing(0, n=min(-(-args.steps // ktiming_period(args.steps)), 64))
     trace_ms = float(np.mean(tk)) if len(tk) else dt / args.steps * 1e3
     rays0 = sf.lib().sf_slab_rows(height, band, n, 0) * width   # member 0's rays per launch
     t_step = dt / args.steps
@@ -461,6 +471,7 @@ def main():
     # HIP events around the dominant (trace) kernel of every KTIMING_PERIOD-th render: an event pair
     # costs ~7 us of stream time per frame, so it is sampled (SF_BENCH_KTIMING=0: off, for A/B)
     ktiming = os.environ.get("SF_BENCH_KTIMING", "1") != "0"
+    kp = ktiming_period(args.steps)
 
     ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -468,7 +479,7 @@ def main():
     # whole-render events (kernel_ms) on the same sampled steps as the trace-kernel events: every
     # event record on the stream costs GPU time between kernels (measured ~7 us per pair per frame)
     def run_step(i, timed, view=None):
-        timed = timed and ktiming and i % KTIMING_PERIOD == 0
+        timed = timed and ktiming and i % kp == 0
         with torch.cuda.stream(stream):
             if timed:
                 ev_s[i].record(stream)
@@ -494,7 +505,7 @@ def main():
     moving = args.mode == "frames"
     for i in range(args.warmup):
         run_step(i, False, views[i] if moving else None)
-    ctx.kernel_timing(ktiming, period=KTIMING_PERIOD)   # samples timed renders 0, 10, 20, ...
+    ctx.kernel_timing(ktiming, period=kp)   # samples timed renders 0, kp, 2 kp, ...
     torch.cuda.synchronize(dev)
     if dist_on:
         dist.barrier()
@@ -510,9 +521,11 @@ def main():
     st = ctx.stats()
     if st.overflow_tiles:
         raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
-    kern_ms = (float(np.mean([ev_s[i].elapsed_time(ev_e[i]) for i in range(0, args.steps, KTIMING_PERIOD)]))
+    kern_ms = (float(np.mean([ev_s[i].elapsed_time(ev_e[i]) for i in range(0, args.steps, kp)]))
                if ktiming else dt / args.steps * 1e3)   # whole render, sampled
-    tk = ctx.kernel_timing(n=min(-(-args.steps // KTIMING_PERIOD), 64)) if ktiming else []   # the trace kernel alone, last timed renders
+    nks = min(-(-args.steps // kp), 64)
+    tk = ctx.kernel_timing(n=nks) if ktiming else []   # the trace kernel alone, last timed renders
+    clk = ctx.kernel_clocks(n=nks) if ktiming else []  # live shader clock of the same renders
     trace_ms = float(np.mean(tk)) if len(tk) else kern_ms
 
     # the same loop on one unchanging view (the config camera, frame 0 of the path): extra key, never `value`
@@ -578,7 +591,8 @@ def main():
         per_launch_bytes = BYTES_PER_RAY * rays_per_step_rank
         achieved = per_launch_bytes / (trace_ms * 1e-3) / 1e9
         camera = "moving" if moving else "fixed"
-        pmc, _ = load_pmc(TRACE_KERNEL, pmc_config_key(width, height, args.K, camera))
+        build = sf.build_info()
+        pmc, _ = load_pmc(TRACE_KERNEL, pmc_config_key(width, height, args.K, camera), build)
         traffic = pmc_traffic(pmc)
         cfg_name = BASELINE_CONFIGS.get((width, height, round(args.K, 4)))
         out = {
@@ -613,12 +627,14 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": round(traffic) if traffic else None,
-                         "kernel": TRACE_KERNEL, "kernel_ms": round(trace_ms, 4),
+                         "kernel": TRACE_KERNEL, "kernel_ms": round(trace_ms, 4), "kernel_samples": len(tk),
+                         "clock_mhz_live": round(float(np.median(clk)), 1) if len(clk) else None,
                          "note": "path is VALU/latency-bound (SURVEY.md §8(d), see `valu`); achieved = 32 B/ray x "
                                  "rays per launch / mean duration of the trace kernel (HIP events around it on its "
                                  "launch stream); traffic = PMC WRITE_SIZE + 2 x FETCH_SIZE per launch "
                                  "(profiles/pmc_traffic.json, only when profiled on this config, else null)"},
             "valu": pmc_valu(pmc),
+            "build": build,
         }
         if check is not None:
             out["check_rows_bit_exact"] = check

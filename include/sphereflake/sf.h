@@ -42,7 +42,8 @@ enum sf_status {
     SF_ENODEV = -4,      /* no such device / not a gfx950 device */
     SF_ENOVIEW = -5,     /* sf_render before sf_set_view */
     SF_EDEPTH = -6,      /* traversal exceeded SF_MAX_DEPTH_LIMIT levels */
-    SF_ESTATE = -7       /* call not valid in the current state (e.g. progressive mode running) */
+    SF_ESTATE = -7,      /* call not valid in the current state (e.g. progressive mode running) */
+    SF_ECOMM = -8        /* RCCL error (see sf_dist_last_error) */
 };
 
 /* Traversal kernels. */
@@ -71,7 +72,9 @@ typedef struct sf_render_params {
     uint32_t emit_aux;        /* 1: also write minT (float) and hit index (uint32) channels */
     uint32_t max_depth;       /* traversal stack levels to provision (0 = auto: 12, retried at
                                  SF_MAX_DEPTH_LIMIT if a tile needs more) */
-    uint32_t reserved;
+    uint32_t packed;          /* 1: write ONE float4 (nx, ny, nz, minT) per pixel into pos4 (nrm4 unused): a
+                                 band slab for the multi-GPU gather at 16 B/pixel instead of 32; the position is
+                                 dir * minT, recomputed bit for bit by sf_unpack_bands (wave kernel only) */
     void* stream;             /* hipStream_t to launch on; NULL = the context stream */
 } sf_render_params;
 
@@ -123,6 +126,14 @@ int sf_render_to(sf_ctx* ctx, const sf_render_params* params, float* pos4, float
 
 /* Rows of the slab a (band_rows, band_count, band_index) shard owns (compact layout). */
 uint32_t sf_slab_rows(uint32_t height, uint32_t band_rows, uint32_t band_count, uint32_t band_index);
+
+/* The receiving end of a banded frame: `stage4` (device) holds the packed slabs (params.packed = 1,
+   compact = 1) of members first_member .. first_member + members - 1 of a (band_rows, band_count) split, each
+   stage_rows x W float4; every pixel is written to the context's G-buffer at its frame position in the
+   reference layout, bit for bit what an unbanded render writes (positions recomputed from the context's
+   current view: call it with the view the slabs were traced with). Asynchronous on `stream`. */
+int sf_unpack_bands(sf_ctx* ctx, const float* stage4, uint32_t stage_rows, uint32_t band_rows, uint32_t band_count,
+                    uint32_t first_member, uint32_t members, void* stream);
 
 /* Replaces GetGBuffer() + the GL PBO upload source (Sphereflake.h:25-28,
    GLPixelBufferObject.h:24-29): synchronous D2H copy of the context G-buffer into host
@@ -304,6 +315,39 @@ int sf_group_download(sf_group* group, float* pos4, float* nrm4);   /* synchrono
 int sf_group_get_stats(sf_group* group, sf_stats* out);             /* synchronises */
 int sf_group_reset_stats(sf_group* group);                          /* all three counters, every member */
 int sf_group_last_hip_error(const sf_group* group);
+
+/* --- multi-GPU, one process per GPU ------------------------------------------------------
+   The reference's worker pool (Sphereflake.cpp:67-74) as nranks processes, one GPU each (the torch.distributed /
+   MPI model): every rank traces the interleaved bands b = rank (mod nranks) of each frame; ranks k > 0 trace
+   theirs as packed slabs (16 B/pixel, sf_render_params.packed) and send them to rank 0 with RCCL over xGMI
+   (grouped ncclSend / ncclRecv on the frame's stream); rank 0 traces its own bands in place and unpacks the
+   others' (sf_unpack_bands) into its G-buffer, bit for bit the single-GPU frame.
+   `slots` frames may be in flight: frame i runs on slot i % slots (its own context, stream, communicator and
+   buffers), so a frame's trace fills the GPU while the previous frame's heaviest tiles and gather finish.
+   With nranks = 1 there is no communicator (frames in flight on one GPU). Every rank must issue the same calls
+   in the same order (set_view, render, get_stats) with the same views. */
+#define SF_DIST_ID_BYTES 128   /* ncclUniqueId */
+#define SF_DIST_MAX_SLOTS 8
+typedef struct sf_dist sf_dist;
+/* Rank 0 makes one id per slot and hands them to every rank (any channel: MPI, a torch.distributed broadcast). */
+int sf_dist_unique_id(uint8_t id[SF_DIST_ID_BYTES]);
+/* Collective over the ranks (RCCL communicator init per slot). ids: slots x SF_DIST_ID_BYTES (may be NULL when
+   nranks = 1: no communicator at all; with ids a one-rank communicator is made).
+   band_rows: a multiple of 8 (8 = one tile row). */
+int sf_dist_create(int device, uint32_t width, uint32_t height, uint32_t band_rows, int rank, int nranks, int slots,
+                   const uint8_t* ids, sf_dist** out);
+void sf_dist_destroy(sf_dist* dist);
+int sf_dist_slots(const sf_dist* dist);
+sf_ctx* sf_dist_context(sf_dist* dist, int slot);     /* slot's context; on rank 0 it holds that slot's frames */
+int sf_dist_last_slot(const sf_dist* dist);           /* slot of the last frame issued (SF_ESTATE before any) */
+int sf_dist_set_view(sf_dist* dist, const float origin[3], const float top_left[3], const float top_right[3],
+                     const float bottom_left[3]);     /* the view of the next frames */
+int sf_dist_render(sf_dist* dist);                    /* one frame, asynchronous (this rank's share + gather) */
+int sf_dist_synchronize(sf_dist* dist);               /* every slot of this rank done */
+int sf_dist_download(sf_dist* dist, float* pos4, float* nrm4);   /* rank 0: D2H of the last frame (synchronises) */
+int sf_dist_get_stats(sf_dist* dist, sf_stats* out);  /* collective: over slots and ranks (synchronises) */
+int sf_dist_reset_stats(sf_dist* dist);
+int sf_dist_last_error(const sf_dist* dist, int* hip_error, int* rccl_error);
 
 /* The context's own stream (hipStream_t) -- where calls with a NULL stream are queued. */
 void* sf_context_stream(sf_ctx* ctx);

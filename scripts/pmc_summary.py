@@ -40,7 +40,11 @@ for k, cs in acc.items():
     for c in sorted(cs):
         print(f"   {c:28s} {means[k][c]:16.1f}")
 if out_json:
+    # the library build the passes profiled (bench.py uses the counters only for that same build)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "sphereflake-raytracer_amd"))
+    import sphereflake_amd as sf  # noqa: E402
     with open(out_json, "w") as f:
         rel = sorted({os.path.relpath(d, os.getcwd()) for d in args})
         json.dump({"source": "rocprofv3 --pmc passes of scripts/prof_pmc.sh (" + ", ".join(rel) + "); "
-                             "FETCH_SIZE/WRITE_SIZE in KB per dispatch", "config": config, "kernels": means}, f, indent=1)
+                             "FETCH_SIZE/WRITE_SIZE in KB per dispatch", "config": config, "build": sf.build_info(),
+                   "kernels": means}, f, indent=1)

@@ -34,6 +34,8 @@ extern "C" __global__ void sf_order_scatter(const uint32_t* cost, uint32_t n, ui
 extern "C" __global__ void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list, uint32_t* counters,
                                          uint32_t parity);
 extern "C" __global__ void sf_trace_ray(FrameArgs a);
+extern "C" __global__ void sf_band_unpack(FrameArgs a, const float4* stage, uint32_t stage_rows, uint32_t band_rows,
+                                           uint32_t n, uint32_t first, uint32_t members, uint32_t row0);
 extern "C" __global__ void sf_post_ssao(PostArgs a);
 extern "C" __global__ void sf_post_blur(PostArgs a, uint32_t dir);
 extern "C" __global__ void sf_post_final(PostArgs a);
@@ -354,6 +356,7 @@ const char* sf_strerror(int s)
     case SF_ENOVIEW: return "render before SetView";
     case SF_EDEPTH: return "traversal deeper than SF_MAX_DEPTH_LIMIT";
     case SF_ESTATE: return "invalid state";
+    case SF_ECOMM: return "RCCL error";
     default: return "unknown error";
     }
 }
@@ -573,6 +576,8 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
     a.band_count = band_count;
     a.band_index = p.band_index;
     a.compact = p.compact ? 1u : 0u;
+    a.packed = p.packed ? 1u : 0u;
+    if (a.packed && p.kernel == SF_KERNEL_PER_RAY) return SF_EINVAL;   // (the per-ray kernel writes the plain layout)
     a.emit_aux = p.emit_aux ? 1u : 0u;
     a.pos = pos;
     a.nrm = nrm;
@@ -738,7 +743,32 @@ int sf_render(sf_ctx* c, const sf_render_params* p)
 
 int sf_render_to(sf_ctx* c, const sf_render_params* p, float* pos4, float* nrm4, float* min_t, uint32_t* hidx)
 {
+    if (p && p->packed && !nrm4) nrm4 = pos4;   // (packed slabs write pos4 only)
     return launch(c, p, pos4, nrm4, min_t, hidx);
+}
+
+int sf_unpack_bands(sf_ctx* c, const float* stage4, uint32_t stage_rows, uint32_t band_rows, uint32_t band_count,
+                    uint32_t first_member, uint32_t members, void* stream)
+{
+    if (!c || !stage4 || band_rows == 0 || band_rows % 8 != 0 || band_count == 0 ||
+        first_member + members > band_count)
+        return SF_EINVAL;
+    if (!c->has_view) return SF_ENOVIEW;
+    if (members == 0 || stage_rows == 0) return SF_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    DevGuard g(c->device);
+    if (int rc = ctx_join(c, s)) return rc;
+    FrameArgs a = frame_args(c);
+    a.pos = c->pos;
+    a.nrm = c->nrm;
+    for (uint32_t r0 = 0; r0 < stage_rows; r0 += 65535u) {
+        const uint32_t rows = stage_rows - r0 < 65535u ? stage_rows - r0 : 65535u;
+        hipLaunchKernelGGL(sf_band_unpack, dim3((c->W + 255u) / 256u, rows, members), dim3(256), 0, s, a,
+                           reinterpret_cast<const float4*>(stage4), stage_rows, band_rows, band_count, first_member,
+                           members, r0);
+        SF_HIP(c, hipGetLastError());
+    }
+    return SF_OK;
 }
 
 // Frame-less progressive mode (Sphereflake.cpp:67-74, 86-214). The device MT stream is kept in the

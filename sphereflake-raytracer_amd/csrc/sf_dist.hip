@@ -1,0 +1,297 @@
+// sf_dist.hip -- one process per GPU: a frame's rows split over the ranks, gathered to rank 0 with RCCL
+// over xGMI (north star: "row-tiles across 8 x MI355X with RCCL gather").
+//
+// The reference's only parallelism is its host thread pool (Sphereflake.cpp:67-74). Here every rank owns a
+// context on its own GPU and traces the interleaved 8-row bands b = rank (mod nranks) of each frame: flake rows
+// cost ~150 nodes per ray and sky rows ~1, so interleaving balances the ranks without any cost exchange.
+//   rank 0   traces its bands straight into its context's G-buffer at frame positions, then receives every
+//            other rank's slab and unpacks it into the same G-buffer (sf_unpack_bands);
+//   rank k   traces its bands as a PACKED compact slab -- one float4 (nx, ny, nz, minT) per pixel, half the
+//            G-buffer's 32 B: the position is dir * minT, which rank 0 recomputes bit for bit -- and sends it.
+// The gather is grouped ncclSend / ncclRecv on the slot's stream, right behind the trace (it is a gather to one
+// rank, each peer's slab over its own xGMI link: no ring collective).
+//
+// Frames in flight: `slots` independent pipelines (context + stream + communicator + slab), frame i on slot
+// i % slots. A frame's persistent trace grid then fills the wave slots the previous frame's heaviest tiles
+// leave idle, and its trace overlaps the previous frame's gather. Every slot has its own communicator, so
+// operations of different slots never share one; all ranks issue frames in the same order.
+// With nranks = 1 there is no communicator unless ids are given: the slots alone (frames in flight on one GPU).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "sf_internal.h"
+#include "sphereflake/sf.h"
+
+struct sf_dist {
+    int device = 0, rank = 0, nranks = 1;
+    uint32_t W = 0, H = 0, band_rows = 8;
+    struct Slot {
+        sf_ctx* ctx = nullptr;
+        ncclComm_t comm = nullptr;
+        float* slab = nullptr;       // rank > 0: this rank's packed slab (slab_rows x W float4)
+        float* stage = nullptr;      // rank 0: the other ranks' packed slabs (nranks - 1) x stage_rows x W float4
+    };
+    std::vector<Slot> slot;
+    uint32_t slab_rows = 0, stage_rows = 0;
+    uint64_t frames = 0;             // frames issued
+    int last_hip = 0;
+    int last_nccl = 0;
+    int64_t* red = nullptr;          // device scratch of sf_dist_get_stats (4 x int64)
+};
+
+namespace {
+
+struct Dev {
+    int prev = -1;
+    explicit Dev(int d)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != d) (void)hipSetDevice(d);
+    }
+    ~Dev()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+#define SFD_HIP(d, expr)                        \
+    do {                                        \
+        hipError_t e_ = (expr);                 \
+        if (e_ != hipSuccess) {                 \
+            (d)->last_hip = (int)e_;            \
+            return SF_EHIP;                     \
+        }                                       \
+    } while (0)
+#define SFD_NCCL(d, expr)                       \
+    do {                                        \
+        ncclResult_t r_ = (expr);               \
+        if (r_ != ncclSuccess) {                \
+            (d)->last_nccl = (int)r_;           \
+            return SF_ECOMM;                    \
+        }                                       \
+    } while (0)
+
+void free_dist(sf_dist* d)
+{
+    Dev g(d->device);
+    for (auto& s : d->slot)
+        if (s.ctx) (void)sf_synchronize(s.ctx);
+    for (auto& s : d->slot) {
+        if (s.comm) (void)ncclCommDestroy(s.comm);
+        (void)hipFree(s.slab);
+        (void)hipFree(s.stage);
+        if (s.ctx) sf_destroy(s.ctx);
+    }
+    (void)hipFree(d->red);
+    delete d;
+}
+
+}  // namespace
+
+extern "C" int sf_dist_unique_id(uint8_t id[SF_DIST_ID_BYTES])
+{
+    static_assert(SF_DIST_ID_BYTES == sizeof(ncclUniqueId), "RCCL unique id size");
+    if (!id) return SF_EINVAL;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return SF_ECOMM;
+    std::memcpy(id, &u, sizeof u);
+    return SF_OK;
+}
+
+extern "C" int sf_dist_create(int device, uint32_t width, uint32_t height, uint32_t band_rows, int rank, int nranks,
+                              int slots, const uint8_t* ids, sf_dist** out)
+{
+    if (!out || width == 0 || height == 0 || nranks < 1 || rank < 0 || rank >= nranks || slots < 1 ||
+        slots > SF_DIST_MAX_SLOTS || band_rows == 0 || band_rows % 8 != 0 || (nranks > 1 && !ids))
+        return SF_EINVAL;
+    *out = nullptr;
+    sf_dist* d = new (std::nothrow) sf_dist();
+    if (!d) return SF_ENOMEM;
+    d->device = device;
+    d->rank = rank;
+    d->nranks = nranks;
+    d->W = width;
+    d->H = height;
+    d->band_rows = band_rows;
+    d->slot.resize(slots);
+    const uint32_t n = (uint32_t)nranks;
+    d->slab_rows = sf_slab_rows(height, band_rows, n, (uint32_t)rank);
+    for (uint32_t k = 1; k < n; ++k) d->stage_rows = std::max(d->stage_rows, sf_slab_rows(height, band_rows, n, k));
+    auto fail = [&](int rc) {
+        free_dist(d);
+        return rc;
+    };
+    for (auto& s : d->slot)
+        if (int rc = sf_create(device, width, height, &s.ctx)) return fail(rc);
+    Dev g(device);
+    for (int k = 0; k < slots; ++k) {
+        auto& s = d->slot[k];
+        if (ids) {   // (one rank with ids: a communicator of one, which exercises the RCCL path)
+            ncclUniqueId u;
+            std::memcpy(&u, ids + (size_t)k * SF_DIST_ID_BYTES, sizeof u);
+            const ncclResult_t r = ncclCommInitRank(&s.comm, nranks, u, rank);
+            if (r != ncclSuccess) {
+                d->last_nccl = (int)r;
+                s.comm = nullptr;
+                return fail(SF_ECOMM);
+            }
+        }
+        hipError_t e = hipSuccess;
+        if (rank > 0 && d->slab_rows) e = hipMalloc(&s.slab, (size_t)d->slab_rows * width * 16);
+        if (e == hipSuccess && rank == 0 && nranks > 1 && d->stage_rows)
+            e = hipMalloc(&s.stage, (size_t)(nranks - 1) * d->stage_rows * width * 16);
+        if (e != hipSuccess) {
+            d->last_hip = (int)e;
+            return fail(e == hipErrorOutOfMemory ? SF_ENOMEM : SF_EHIP);
+        }
+    }
+    if (hipMalloc(&d->red, 4 * sizeof(int64_t)) != hipSuccess) return fail(SF_ENOMEM);
+    *out = d;
+    return SF_OK;
+}
+
+extern "C" void sf_dist_destroy(sf_dist* d)
+{
+    if (d) free_dist(d);
+}
+
+extern "C" int sf_dist_slots(const sf_dist* d) { return d ? (int)d->slot.size() : SF_EINVAL; }
+
+extern "C" sf_ctx* sf_dist_context(sf_dist* d, int slot)
+{
+    return (d && slot >= 0 && slot < (int)d->slot.size()) ? d->slot[slot].ctx : nullptr;
+}
+
+extern "C" int sf_dist_last_slot(const sf_dist* d)
+{
+    if (!d) return SF_EINVAL;
+    if (d->frames == 0) return SF_ESTATE;
+    return (int)((d->frames - 1) % d->slot.size());
+}
+
+extern "C" int sf_dist_set_view(sf_dist* d, const float origin[3], const float top_left[3], const float top_right[3],
+                                const float bottom_left[3])
+{
+    if (!d) return SF_EINVAL;
+    for (auto& s : d->slot)
+        if (int rc = sf_set_view(s.ctx, origin, top_left, top_right, bottom_left)) return rc;
+    return SF_OK;
+}
+
+extern "C" int sf_dist_render(sf_dist* d)
+{
+    if (!d) return SF_EINVAL;
+    const uint32_t n = (uint32_t)d->nranks, W = d->W;
+    auto& s = d->slot[d->frames % d->slot.size()];
+    hipStream_t st = (hipStream_t)sf_context_stream(s.ctx);
+    sf_render_params p;
+    std::memset(&p, 0, sizeof p);
+    p.band_rows = d->band_rows;
+    p.band_count = n;
+    p.band_index = (uint32_t)d->rank;
+    if (d->rank == 0) {
+        // rank 0: its bands in place; then the other ranks' slabs in, unpacked beside them
+        if (int rc = sf_render(s.ctx, &p)) return rc;
+        if (n > 1 && d->stage_rows) {
+            Dev g(d->device);
+            const size_t cnt = (size_t)d->stage_rows * W * 4;   // floats per peer slot of the stage
+            SFD_NCCL(d, ncclGroupStart());
+            for (uint32_t k = 1; k < n; ++k) {
+                const size_t rows = sf_slab_rows(d->H, d->band_rows, n, k);
+                if (!rows) continue;
+                SFD_NCCL(d, ncclRecv(s.stage + (k - 1) * cnt, rows * W * 4, ncclFloat32, (int)k, s.comm, st));
+            }
+            SFD_NCCL(d, ncclGroupEnd());
+            if (int rc = sf_unpack_bands(s.ctx, s.stage, d->stage_rows, d->band_rows, n, 1, n - 1, nullptr)) return rc;
+        }
+    } else {
+        p.compact = 1;
+        p.packed = 1;
+        if (d->slab_rows) {
+            if (int rc = sf_render_to(s.ctx, &p, s.slab, nullptr, nullptr, nullptr)) return rc;
+            Dev g(d->device);
+            SFD_NCCL(d, ncclSend(s.slab, (size_t)d->slab_rows * W * 4, ncclFloat32, 0, s.comm, st));
+        }
+    }
+    ++d->frames;
+    return SF_OK;
+}
+
+extern "C" int sf_dist_synchronize(sf_dist* d)
+{
+    if (!d) return SF_EINVAL;
+    int first = SF_OK;
+    for (auto& s : d->slot) {
+        const int rc = sf_synchronize(s.ctx);
+        if (rc != SF_OK && first == SF_OK) first = rc;
+    }
+    return first;
+}
+
+extern "C" int sf_dist_download(sf_dist* d, float* pos4, float* nrm4)
+{
+    if (!d) return SF_EINVAL;
+    if (d->rank != 0 || d->frames == 0) return SF_ESTATE;
+    if (int rc = sf_dist_synchronize(d)) return rc;
+    return sf_download(d->slot[(d->frames - 1) % d->slot.size()].ctx, pos4, nrm4, nullptr, nullptr);
+}
+
+// Collective: every rank calls it. Stats of this rank's slots combined, then over the ranks on the device
+// (max depth max, closest min, rays and overflow tiles summed: Sphereflake.h:30-58 over the whole frame).
+extern "C" int sf_dist_get_stats(sf_dist* d, sf_stats* out)
+{
+    if (!d || !out) return SF_EINVAL;
+    sf_stats t;
+    std::memset(&t, 0, sizeof t);
+    t.closest = FLT_MAX;
+    for (auto& s : d->slot) {
+        sf_stats x;
+        if (int rc = sf_get_stats(s.ctx, &x)) return rc;
+        t.max_depth = std::max(t.max_depth, x.max_depth);
+        t.closest = std::min(t.closest, x.closest);
+        t.rays += x.rays;
+        t.overflow_tiles += x.overflow_tiles;
+    }
+    if (d->slot[0].comm) {
+        Dev g(d->device);
+        hipStream_t st = (hipStream_t)sf_context_stream(d->slot[0].ctx);
+        // max of {max depth, -closest key}, sum of {rays, overflow tiles}
+        int64_t h[4] = { t.max_depth, -(int64_t)sf_float_key(t.closest), t.rays, t.overflow_tiles };
+        SFD_HIP(d, hipMemcpyAsync(d->red, h, sizeof h, hipMemcpyHostToDevice, st));
+        SFD_NCCL(d, ncclAllReduce(d->red, d->red, 2, ncclInt64, ncclMax, d->slot[0].comm, st));
+        SFD_NCCL(d, ncclAllReduce(d->red + 2, d->red + 2, 2, ncclInt64, ncclSum, d->slot[0].comm, st));
+        SFD_HIP(d, hipMemcpyAsync(h, d->red, sizeof h, hipMemcpyDeviceToHost, st));
+        SFD_HIP(d, hipStreamSynchronize(st));
+        t.max_depth = (int32_t)h[0];
+        t.closest = sf_key_float((int32_t)(-h[1]));
+        t.rays = h[2];
+        t.overflow_tiles = h[3];
+    }
+    *out = t;
+    return SF_OK;
+}
+
+extern "C" int sf_dist_reset_stats(sf_dist* d)
+{
+    if (!d) return SF_EINVAL;
+    for (auto& s : d->slot) {
+        if (int rc = sf_reset_max_depth(s.ctx)) return rc;
+        if (int rc = sf_reset_closest(s.ctx)) return rc;
+        if (int rc = sf_reset_rays(s.ctx)) return rc;
+    }
+    return SF_OK;
+}
+
+extern "C" int sf_dist_last_error(const sf_dist* d, int* hip_error, int* rccl_error)
+{
+    if (!d) return SF_EINVAL;
+    if (hip_error) *hip_error = d->last_hip;
+    if (rccl_error) *rccl_error = d->last_nccl;
+    return SF_OK;
+}

@@ -101,6 +101,7 @@ struct FrameArgs {
     uint32_t tiles_per_band;          // band_rows / 8
     uint32_t band_count, band_index;
     uint32_t compact;                 // write rows packed into the shard's slab
+    uint32_t packed;                  // write one float4 (nx, ny, nz, minT) per pixel to pos only (sf_render_params.packed)
     uint32_t max_depth;               // traversal levels provisioned (<= SF_MAX_DEPTH_LIMIT)
     uint32_t emit_aux;
     uint32_t flags;                   // SF_FLAG_* (A/B switches for diagnostics; 0 = product default)

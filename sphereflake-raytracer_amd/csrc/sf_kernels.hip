@@ -826,12 +826,18 @@ __device__ __forceinline__ Tile tile_of(const FrameArgs& a, uint32_t tile, uint3
 }
 
 // G-buffer write (Sphereflake.cpp:186-196): (pos, 1), (nrm, 1); a miss writes (0,0,0,1).
+// Packed slabs (multi-GPU bands, a.packed): one float4 (nx, ny, nz, minT) -- the position is dir * minT, which
+// the receiving side recomputes bit for bit (sf_unpack_bands), so a band ships 16 B per pixel instead of 32.
 __device__ __forceinline__ void write_pixel(const FrameArgs& a, const Tile& t, float dx, float dy, float dz,
                                             const HitState& h, const uint32_t* __restrict__ lut)
 {
     float px, py, pz, nx, ny, nz;
     shade(dx, dy, dz, h, lut, px, py, pz, nx, ny, nz);
     const size_t o = (size_t)t.orow * a.W + t.x;
+    if (a.packed) {   // (uniform)
+        reinterpret_cast<float4*>(a.pos)[o] = make_float4(nx, ny, nz, h.minT);
+        return;
+    }
     reinterpret_cast<float4*>(a.pos)[o] = make_float4(px, py, pz, 1.0f);
     reinterpret_cast<float4*>(a.nrm)[o] = make_float4(nx, ny, nz, 1.0f);
     if (a.emit_aux) {
@@ -1370,6 +1376,32 @@ extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t
         pending &= ~m;
     }
     if (lane < SF_ORDER_BUCKETS) chunk_cnt[c * SF_ORDER_BUCKETS + lane] = 0u;   // for the next render
+}
+
+// Packed band slabs -> the frame G-buffer (multi-GPU gather). `stage` holds `members` slabs
+// of members first .. first + members - 1 of a (band_rows, n) band split, each stage_rows x W float4
+// (nx, ny, nz, minT) in the compact row order of sf_render_params.compact (member k's bands k, k + n, ...).
+// Every pixel is rewritten at its frame position exactly as write_pixel would have: pos = (dir * t, 1) with
+// dir recomputed by ray_dir from the same view (t < FLT_MAX: a hit; a miss leaves minT = FLT_MAX) or
+// (0, 0, 0, 1), nrm = (n, 1). One thread per staged pixel, consecutive threads along a row: coalesced.
+extern "C" __global__ __launch_bounds__(256) void sf_band_unpack(FrameArgs a, const float4* __restrict__ stage,
+                                                                  uint32_t stage_rows, uint32_t band_rows, uint32_t n,
+                                                                  uint32_t first, uint32_t members, uint32_t row0)
+{
+    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t sr = row0 + blockIdx.y;            // slab row (launches of <= 65535 rows)
+    const uint32_t m = blockIdx.z;                    // member first + m
+    if (x >= a.W || m >= members) return;
+    const uint32_t k = first + m, i = sr / band_rows, r = sr % band_rows;
+    const uint32_t y = (i * n + k) * band_rows + r;   // frame row
+    if (y >= a.H) return;                             // (rows past this member's slab)
+    const float4 v = stage[((size_t)m * stage_rows + sr) * a.W + x];
+    float dx, dy, dz;
+    ray_dir(a, (float)x, (float)y, dx, dy, dz, a.consts->lut);
+    const bool hit = v.w < FLT_MAX;
+    const size_t o = (size_t)y * a.W + x;
+    reinterpret_cast<float4*>(a.pos)[o] = hit ? make_float4(dx * v.w, dy * v.w, dz * v.w, 1.0f) : make_float4(0.f, 0.f, 0.f, 1.0f);
+    reinterpret_cast<float4*>(a.nrm)[o] = make_float4(v.x, v.y, v.z, 1.0f);
 }
 
 // Re-traces flagged tiles with SF_MAX_LEVELS levels. Grid-stride over the list; reads this

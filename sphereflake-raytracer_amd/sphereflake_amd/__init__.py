@@ -51,7 +51,7 @@ class sf_render_params(ctypes.Structure):
     _fields_ = [("band_rows", ctypes.c_uint32), ("band_count", ctypes.c_uint32),
                 ("band_index", ctypes.c_uint32), ("compact", ctypes.c_uint32),
                 ("kernel", ctypes.c_uint32), ("emit_aux", ctypes.c_uint32),
-                ("max_depth", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("max_depth", ctypes.c_uint32), ("packed", ctypes.c_uint32),
                 ("stream", ctypes.c_void_p)]
 
 
@@ -87,6 +87,7 @@ SIGNATURES = {
     "sf_render_to": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_render_params), ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_void_p]),
     "sf_slab_rows": (ctypes.c_uint32, [ctypes.c_uint32] * 4),
+    "sf_unpack_bands": (ctypes.c_int, [_CTX, ctypes.c_void_p] + [ctypes.c_uint32] * 5 + [ctypes.c_void_p]),
     "sf_download": (ctypes.c_int, [_CTX, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "sf_download_async": (ctypes.c_int, [_CTX, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
@@ -143,7 +144,23 @@ SIGNATURES = {
     "sf_group_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(sf_stats)]),
     "sf_group_last_hip_error": (ctypes.c_int, [ctypes.c_void_p]),
     "sf_group_reset_stats": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_dist_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_dist_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "sf_dist_destroy": (None, [ctypes.c_void_p]),
+    "sf_dist_slots": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_dist_context": (ctypes.c_void_p, [ctypes.c_void_p, ctypes.c_int]),
+    "sf_dist_last_slot": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_dist_set_view": (ctypes.c_int, [ctypes.c_void_p, _F, _F, _F, _F]),
+    "sf_dist_render": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_dist_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_dist_download": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "sf_dist_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(sf_stats)]),
+    "sf_dist_reset_stats": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_dist_last_error": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
 }
+SF_ECOMM = -8
+SF_DIST_ID_BYTES = 128
 
 _lib = None
 _lock = threading.Lock()
@@ -316,9 +333,9 @@ class GBuffer:
 
 
 def render_params(band_rows=0, band_count=1, band_index=0, compact=False, kernel=SF_KERNEL_WAVE,
-                  emit_aux=False, max_depth=0, stream=None) -> sf_render_params:
+                  emit_aux=False, max_depth=0, stream=None, packed=False) -> sf_render_params:
     return sf_render_params(band_rows, band_count, band_index, int(bool(compact)), kernel, int(bool(emit_aux)),
-                            max_depth, 0, stream)
+                            max_depth, int(bool(packed)), stream)
 
 
 class _FifoLock:
@@ -431,6 +448,13 @@ class Sphereflake:
 
     def Synchronize(self):
         _check(lib().sf_synchronize(self._ctx), "sf_synchronize", self._ctx)
+
+    def unpack_bands(self, stage_ptr: int, stage_rows: int, band_rows: int, band_count: int, first_member: int,
+                     members: int, stream=None):
+        """Packed band slabs on the device (render_to(..., packed=True, compact=True) of members first_member..)
+        -> this context's G-buffer at frame positions (sf_unpack_bands), with the current view."""
+        _check(lib().sf_unpack_bands(self._ctx, ctypes.c_void_p(stage_ptr), stage_rows, band_rows, band_count,
+                                     first_member, members, stream), "sf_unpack_bands", self._ctx)
 
     def device_buffers(self):
         ptrs = [ctypes.c_void_p() for _ in range(4)]
@@ -763,3 +787,109 @@ class SphereflakeGroup:
         s = sf_stats()
         self._check(lib().sf_group_get_stats(self._g, ctypes.byref(s)), "sf_group_get_stats")
         return s
+
+
+def dist_unique_id() -> bytes:
+    """A fresh RCCL unique id (sf_dist_unique_id): rank 0 makes one per slot and hands them to every rank."""
+    buf = (ctypes.c_uint8 * SF_DIST_ID_BYTES)()
+    _check(lib().sf_dist_unique_id(buf), "sf_dist_unique_id")
+    return bytes(buf)
+
+
+class SphereflakeDist:
+    """One process per GPU (sf_dist_*): this rank's share of every frame (interleaved
+    `band_rows`-row bands), gathered to rank 0 over RCCL as packed slabs; `slots` frames in flight. `ids`:
+    slots x 128 bytes of dist_unique_id() from rank 0 (None when nranks = 1)."""
+
+    def __init__(self, device: int, width: int, height: int, rank: int = 0, nranks: int = 1, slots: int = 2,
+                 ids: bytes | None = None, band_rows: int = 8):
+        self.width, self.height, self.rank, self.nranks = int(width), int(height), int(rank), int(nranks)
+        h = ctypes.c_void_p()
+        idb = None
+        if ids is not None:
+            if len(ids) != slots * SF_DIST_ID_BYTES:
+                raise ValueError("ids must hold slots x 128 bytes")
+            idb = ctypes.create_string_buffer(bytes(ids), len(ids))
+        _check(lib().sf_dist_create(int(device), self.width, self.height, int(band_rows), self.rank, self.nranks,
+                                    int(slots), idb, ctypes.byref(h)), "sf_dist_create")
+        self._d = h
+
+    def close(self):
+        if getattr(self, "_d", None):
+            lib().sf_dist_destroy(self._d)
+            self._d = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc != SF_OK:
+            err = SphereflakeError(rc, what)
+            hip, nccl = ctypes.c_int(), ctypes.c_int()
+            lib().sf_dist_last_error(self._d, ctypes.byref(hip), ctypes.byref(nccl))
+            err.hip_error, err.rccl_error = hip.value, nccl.value
+            raise err
+
+    @property
+    def slots(self) -> int:
+        return lib().sf_dist_slots(self._d)
+
+    def context(self, slot: int):
+        return lib().sf_dist_context(self._d, int(slot))
+
+    def last_slot(self) -> int:
+        return lib().sf_dist_last_slot(self._d)
+
+    def SetView(self, origin, topLeft, topRight, bottomLeft):
+        o, tl, tr, bl = (_f32(v, 3) for v in (origin, topLeft, topRight, bottomLeft))
+        self._check(lib().sf_dist_set_view(self._d, _fp(o), _fp(tl), _fp(tr), _fp(bl)), "sf_dist_set_view")
+
+    def SetCamera(self, cam: Camera):
+        self.SetView(*cam.corners())
+
+    def Render(self):
+        self._check(lib().sf_dist_render(self._d), "sf_dist_render")
+
+    def Synchronize(self):
+        self._check(lib().sf_dist_synchronize(self._d), "sf_dist_synchronize")
+
+    def download(self):
+        """Rank 0: the last frame's G-buffer (synchronises)."""
+        H, W = self.height, self.width
+        pos = np.empty((H, W, 4), np.float32)
+        nrm = np.empty((H, W, 4), np.float32)
+        self._check(lib().sf_dist_download(self._d, pos.ctypes.data_as(ctypes.c_void_p),
+                                           nrm.ctypes.data_as(ctypes.c_void_p)), "sf_dist_download")
+        return pos, nrm
+
+    def stats(self) -> sf_stats:
+        """Collective over the ranks."""
+        s = sf_stats()
+        self._check(lib().sf_dist_get_stats(self._d, ctypes.byref(s)), "sf_dist_get_stats")
+        return s
+
+    def reset_stats(self):
+        self._check(lib().sf_dist_reset_stats(self._d), "sf_dist_reset_stats")
+
+    def kernel_timing(self, slot: int, enable: bool | None = None, n: int = 64, period: int = 1):
+        """Trace-kernel events of one slot's context (Sphereflake.kernel_timing)."""
+        ctx = self.context(slot)
+        if enable is not None:
+            _check(lib().sf_set_kernel_timing(ctx, max(1, int(period)) if enable else 0), "sf_set_kernel_timing", ctx)
+            return None
+        out = np.zeros(n, np.float32)
+        got = lib().sf_kernel_times(ctx, out.ctypes.data_as(_F), n)
+        if got < 0:
+            _check(got, "sf_kernel_times", ctx)
+        return out[:got]
+
+    def kernel_clocks(self, slot: int, n: int = 64):
+        ctx = self.context(slot)
+        out = np.zeros(n, np.float32)
+        got = lib().sf_kernel_clocks(ctx, out.ctypes.data_as(_F), n)
+        if got < 0:
+            _check(got, "sf_kernel_clocks", ctx)
+        return out[:got]

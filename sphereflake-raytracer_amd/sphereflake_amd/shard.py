@@ -83,3 +83,22 @@ def reduce_stats(max_depth: int, closest: float, rays: int, group=None, device=N
     dist.all_reduce(cl, op=dist.ReduceOp.MIN, group=group)
     dist.all_reduce(ry, op=dist.ReduceOp.SUM, group=group)
     return int(md.item()), float(cl.item()), int(ry.item())
+
+
+def dist_ids(slots: int, group=None, src: int = 0) -> bytes:
+    """RCCL unique ids for sf_dist_create (one per slot): made on rank `src` (sf_dist_unique_id), broadcast
+    to every rank over torch.distributed (any backend), so all ranks initialise the same communicators."""
+    import torch
+    import torch.distributed as dist
+    from . import SF_DIST_ID_BYTES, dist_unique_id
+    n = slots * SF_DIST_ID_BYTES
+    if dist.get_rank(group) == src:
+        raw = b"".join(dist_unique_id() for _ in range(slots))
+        t = torch.tensor(list(raw), dtype=torch.uint8)
+    else:
+        t = torch.zeros(n, dtype=torch.uint8)
+    backend = dist.get_backend(group)
+    if backend == "nccl":
+        t = t.cuda()
+    dist.broadcast(t, src=src, group=group)
+    return bytes(t.cpu().tolist())

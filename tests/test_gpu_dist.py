@@ -1,0 +1,105 @@
+"""GPU tests of the multi-GPU gather path (reference worker pool Sphereflake.cpp:67-74):
+- packed band slabs (sf_render_params.packed: one float4 (nx, ny, nz, minT) per pixel) unpacked into the frame
+  (sf_unpack_bands) give the golden frame bit for bit, for several band splits;
+- sf_dist_* (one process per GPU, RCCL gather) with one rank: frames in flight on slots, each frame equal to a
+  single-context render of the same view; with ids, a one-rank RCCL communicator (init, all-reduced stats).
+The multi-rank RCCL exchange itself needs one GPU per rank (RCCL refuses two ranks on one device); its host
+side (id exchange, band ownership) is tested over gloo in tests/test_multi.py."""
+import numpy as np
+import pytest
+
+from conftest import load_frame
+from sfcheck import bad_rows, frame_digest, row_digests
+
+pytestmark = pytest.mark.gpu
+
+import sphereflake_amd as sf  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    sf.build()
+    assert sf.device_count() >= 1, "no HIP device visible: GPU tests must run on an MI355X"
+
+
+@pytest.mark.parametrize("name,n,band", [("c2", 2, 8), ("c2", 3, 16), ("c3", 8, 8), ("c3", 3, 8), ("t3", 4, 8)])
+def test_packed_slabs_unpack_to_golden(name, n, band):
+    """Member 0's bands in place, members 1..n-1 as packed compact slabs unpacked beside them: the frame
+    equals the golden frame bit for bit (positions recomputed as dir * minT, misses (0,0,0,1))."""
+    import torch
+    fx = load_frame(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    rows = [sf.lib().sf_slab_rows(H, band, n, k) for k in range(n)]
+    stage_rows = max(rows[1:])
+    stage = torch.full((n - 1, stage_rows, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for rep in range(2):   # row-major, then the heavy-first unit order
+            s.Render(band_rows=band, band_count=n, band_index=0)
+            for k in range(1, n):
+                s.render_to(stage[k - 1].data_ptr(), 0, band_rows=band, band_count=n, band_index=k, compact=True,
+                            packed=True)
+            s.unpack_bands(stage.data_ptr(), stage_rows, band, n, 1, n - 1)
+            pos, nrm, _, _ = s.download()
+            assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == [], (name, n, band, rep)
+        st = s.stats()
+    assert st.max_depth == fx["stats"]["max_depth"]
+
+
+def test_packed_rejects_per_ray_kernel():
+    with sf.Sphereflake(64, 64) as s:
+        s.SetCamera(sf.config_camera(64, 64, 0.25))
+        import torch
+        buf = torch.empty((64, 64, 4), dtype=torch.float32, device="cuda")
+        with pytest.raises(sf.SphereflakeError):
+            s.render_to(buf.data_ptr(), 0, packed=True, kernel=sf.SF_KERNEL_PER_RAY)
+
+
+def path_views(W, H, K, n):
+    from bench import frame_camera
+    return [frame_camera(W, H, K, i).corners() for i in range(n)]
+
+
+@pytest.mark.parametrize("slots", [1, 2, 3])
+def test_dist_one_rank_slots_equal_single_context(slots):
+    """Frames of the bench's moving camera path on `slots` slots (frame i on slot i % slots, frames in flight):
+    each frame, downloaded after its render, equals a plain single-context render of its view."""
+    fx = load_frame("c2")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    views = path_views(W, H, K, 7)
+    with sf.SphereflakeDist(0, W, H, slots=slots) as d, sf.Sphereflake(W, H) as ref:
+        assert d.slots == slots
+        for i, v in enumerate(views):
+            d.SetView(*v)
+            d.Render()
+            if i % 3 == 2 or i == len(views) - 1:
+                pos, nrm = d.download()
+                assert d.last_slot() == i % slots
+                ref.SetView(*v)
+                ref.Render()
+                rp, rn, _, _ = ref.download()
+                assert np.array_equal(pos.view(np.uint32), rp.view(np.uint32)), i
+                assert np.array_equal(nrm.view(np.uint32), rn.view(np.uint32)), i
+        d.SetView(*sf.config_camera(W, H, K).corners())
+        d.Render()
+        pos, nrm = d.download()
+        assert frame_digest(pos, nrm) == fx["frame_digest"]
+        st = d.stats()
+    assert st.rays == (len(views) + 1) * W * H and st.max_depth == fx["stats"]["max_depth"]
+
+
+def test_dist_one_rank_rccl_communicator():
+    """ids given with one rank: every slot gets an RCCL communicator (ncclCommInitRank), the stats are
+    all-reduced through it, and the frames stay golden."""
+    fx = load_frame("c2")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    ids = b"".join(sf.dist_unique_id() for _ in range(2))
+    with sf.SphereflakeDist(0, W, H, rank=0, nranks=1, slots=2, ids=ids) as d:
+        d.SetCamera(sf.config_camera(W, H, K))
+        for _ in range(3):
+            d.Render()
+        pos, nrm = d.download()
+        st = d.stats()
+    assert frame_digest(pos, nrm) == fx["frame_digest"]
+    assert st.rays == 3 * W * H and st.max_depth == fx["stats"]["max_depth"]
+    assert np.float32(st.closest) == np.float32(float.fromhex(fx["stats"]["closest"]))

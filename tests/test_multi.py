@@ -98,3 +98,75 @@ def test_band_rows_validation():
         shard.owned_bands(100, 12, 2, 0)
     with pytest.raises(ValueError):
         shard.owned_bands(100, 8, 2, 2)
+
+
+# ---- the one-process-per-GPU gather (sf_dist_*, csrc/sf_dist.hip): packed slabs and the RCCL id exchange
+
+def _ray_dirs(setup):
+    """Ray directions of every pixel exactly as the kernels' ray_dir (reference Sphereflake.cpp:149-150,
+    162-167; SIMD_AVX.h:170-180 Normalize with the x86 rsqrtps of the C ABI's table), in float32 numpy
+    (IEEE per operation, no contraction)."""
+    from sphereflake_amd import lib
+    W, H = setup["W"], setup["H"]
+    f = np.float32
+    o, tl, tr, bl = (np.asarray(setup[k], f) for k in ("origin", "tl", "tr", "bl"))
+    dh, dv = tr - tl, bl - tl
+    u = (np.arange(W, dtype=f) / f(W))[None, :]
+    v = (np.arange(H, dtype=f) / f(H))[:, None]
+    d = [((tl[c] + dh[c] * u) + dv[c] * v) - o[c] for c in range(3)]
+    ln = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]
+    nr = np.vectorize(lambda x: lib().sf_rsqrtps(float(x)), otypes=[f])(ln)
+    sc = (f(0.5) * nr) * (f(3.0) - (ln * nr) * nr)
+    return [c * sc for c in d]
+
+
+@pytest.mark.parametrize("name", ["t1", "t2", "t3", "t4", "t5"])
+def test_packed_slab_format_is_lossless(name):
+    """A packed slab pixel is (nx, ny, nz, minT): rank 0 rebuilds the position as dir * minT
+    (sf_band_unpack). On every golden pixel that equals the reference's position bit for bit -- a hit's
+    position is exactly dir * t (Sphereflake.h:218-220), a miss keeps minT = FLT_MAX and writes (0,0,0,1)."""
+    from oracle import pyoracle
+    setup = pyoracle.load_setup(name)
+    ref = load_npz(name)
+    dx, dy, dz = _ray_dirs(setup)
+    t = ref["minT"]
+    hit = t < np.finfo(np.float32).max
+    rebuilt = np.zeros_like(ref["pos4"])
+    rebuilt[..., 0] = np.where(hit, dx * t, 0)
+    rebuilt[..., 1] = np.where(hit, dy * t, 0)
+    rebuilt[..., 2] = np.where(hit, dz * t, 0)
+    rebuilt[..., 3] = 1.0
+    assert np.array_equal(rebuilt.view(np.uint32), ref["pos4"].view(np.uint32))
+    assert np.all(ref["nrm4"][~hit][:, :3] == 0.0)
+
+
+def _ids_worker(rank, world, port, slots, errq, outq):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        ids = shard.dist_ids(slots)
+        outq.put((rank, ids))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:
+        errq.put(f"rank {rank}: {type(e).__name__}: {e}")
+        raise
+
+
+@pytest.mark.parametrize("world,slots", [(2, 2), (3, 3)])
+def test_dist_ids_reach_every_rank(world, slots):
+    """sf_dist_create needs the same RCCL unique id per slot on every rank: rank 0 makes them
+    (sf_dist_unique_id) and broadcasts them; every rank must hold the identical, distinct ids."""
+    ctx = mp.get_context("spawn")
+    errq, outq = ctx.SimpleQueue(), ctx.SimpleQueue()
+    mp.start_processes(_ids_worker, args=(world, _free_port(), slots, errq, outq), nprocs=world,
+                       start_method="spawn", join=True)
+    assert errq.empty(), errq.get()
+    got = dict(outq.get() for _ in range(world))
+    assert len(got) == world
+    first = got[0]
+    assert len(first) == slots * 128
+    assert all(v == first for v in got.values())
+    chunks = {first[k * 128:(k + 1) * 128] for k in range(slots)}
+    assert len(chunks) == slots
