@@ -503,8 +503,34 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         // first. Not allocated, not stored (uniform branch).
         if (d + 1u < levels) {
             float* const tb = L.table(d);
+#ifdef SF_EXP_MASKED_BUILD   // experiment: only the 36 builder lanes store (no mirrored or junk stores)
+            {
+                // EXEC = lanes 0..35 for the column store, lanes 27..35 (the centres) for the |c|^2 store, set
+                // inside the asm (no divergent region in the compiler's CFG); LDS ops of a wave complete in order
+                typedef float f3v __attribute__((ext_vector_type(3)));
+                const f3v v3 = {x, y, z};
+                typedef __attribute__((address_space(3))) float* LdsF;
+                const uint32_t a3 = (uint32_t)(uintptr_t)(LdsF)(tb + slot);
+                uint64_t sv;
+                __asm__ volatile(
+                    "s_mov_b64 %0, exec\n\t"
+                    "s_mov_b32 exec_lo, -1\n\t"
+                    "s_mov_b32 exec_hi, 15\n\t"
+                    "s_and_b64 exec, exec, %0\n\t"
+                    "ds_write_b96 %1, %2\n\t"
+                    "s_mov_b32 exec_lo, 0xf8000000\n\t"
+                    "s_mov_b32 exec_hi, 15\n\t"
+                    "s_and_b64 exec, exec, %0\n\t"
+                    "ds_write_b32 %1, %3 offset:12\n\t"
+                    "s_mov_b64 exec, %0\n\t"
+                    : "=&s"(sv)
+                    : "v"(a3), "v"(v3), "v"(w)
+                    : "memory");
+            }
+#else
             *reinterpret_cast<float3*>(tb + slot) = make_float3(x, y, z);
             *(bc == 3u ? tb + slot + 3u : L.cone() + 5u + (lane & 1u)) = w;
+#endif
         }
         const float R2b = dtc.x;
         const float T = dtc.w;
