@@ -5,25 +5,30 @@ A "step" is one full deterministic frame of the hot path (ray generation + spher
 G-buffer write, reference Sphereflake.h:86-226 / Sphereflake.cpp:149-201) over a 1920x1080 frame at
 the depth-8 camera (BASELINE configs[2]: main.cpp:92-96 camera position scaled by K = 0.25). The
 G-buffer stays resident in HBM (the D2H copy into the host GBuffer is timed separately and reported
-as `d2h_ms`, never as `value`).
+as `d2h`, never as `value`).
 
-The camera MOVES: step i renders frame f = i * N + rank of a camera path (the config camera with its
-yaw swept +-10 mrad around the config view at 1 mrad per frame, `frame_camera`), so the heavy-first tile
-schedule always works from the costs of a different view (the reference is an interactive app whose view changes every frame,
-main.cpp:304). `first_render_ms` is the first render of a fresh context (row-major tile order, no
-previous costs); `fixed_camera` repeats the timed loop on one unchanging view.
+The camera MOVES: step i renders frame i of a camera path (the config camera with its yaw swept +-10 mrad
+around the config view at 1 mrad per frame, `frame_camera`), so the heavy-first tile schedule always works
+from the costs of a different view (the reference is an interactive app whose view changes every frame,
+main.cpp:304). `first_render_ms` is the first render of a fresh context (row-major tile order, no previous
+costs); `fixed_camera` repeats the timed loop on one unchanging view; `frame_latency_ms` is one frame
+rendered and waited for alone.
 
-Multi-GPU (`--gpus N`, launched by torch.distributed.run): one process per GPU. The frames of a
-camera path are independent units, so each rank renders its own 1920x1080 depth-8 frame per step
-(frame index = step * N + rank); no data-path collective, `scaling: weak`. `--mode rows` renders ONE
-frame per step across N devices behind the C ABI (sf_group_*): interleaved 8-row
-bands, strided peer copies into device 0's G-buffer, driven by rank 0 alone (the other ranks only join
-the barriers); `scaling: strong`. `--mode rows-rccl` is the earlier per-rank variant (every rank traces
-its bands, torch RCCL gather + reassembly on rank 0).
+Default mode `dist` (sf_dist_*, csrc/sf_dist.hip): `--slots` frames in flight (frame i on slot i % slots, each
+slot its own context, stream and G-buffer), so a frame's persistent trace grid fills the wave slots the previous
+frame's heaviest tiles leave idle -- the reference's workers likewise trace continuously. Multi-GPU (`--gpus N`,
+launched by torch.distributed.run, one process per GPU): ONE frame per step split over the N GPUs in interleaved
+8-row bands; ranks k > 0 trace theirs as packed slabs (16 B/pixel) and RCCL carries them to rank 0 over xGMI,
+which unpacks them beside its own bands into the full G-buffer: `scaling: "strong"` (the frame is fixed, N
+GPUs share it). torch.distributed (gloo) is only the control plane: the RCCL ids, barriers and the max over
+ranks of the timed region. `independent_frames` adds the weak-scaling figure (every rank its own frames).
+`--mode frames` is that weak-scaling loop alone; `--mode rows` one frame over N devices from ONE process
+(sf_group_*: strided peer copies).
 
 rank 0 prints ONE JSON line. `roofline` prices the dominant kernel against HBM (32 B/ray of G-buffer
 stores); `cpu_baseline` times the reference's own AVX packet path (oracle/_ref,
-compiled from the reference sources) on this host's cores.
+compiled from the reference sources) on this host's cores. `configs.c4` is BASELINE configs[3]
+(3840x2160, K = 0.22, depth 9) on the same path.
 """
 from __future__ import annotations
 
@@ -54,7 +59,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--mode", choices=["frames", "rows", "rows-rccl"], default="frames")
+    ap.add_argument("--mode", choices=["dist", "frames", "rows"], default="dist")
+    ap.add_argument("--slots", type=int, default=DEFAULT_SLOTS, help="frames in flight (dist mode)")
     ap.add_argument("--kernel", choices=["wave", "ray"], default="wave")
     ap.add_argument("--width", type=int, default=W)
     ap.add_argument("--height", type=int, default=H)
@@ -62,10 +68,14 @@ def parse():
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip the post-process and transfer sections (profiling runs of the timed loop only)")
+                    help="skip the post-process, transfer, frame-less and c4 sections (profiling runs of the timed loop only)")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--check", action="store_true", help="verify the frame against the oracle rows")
+    ap.add_argument("--check", action="store_true", help="verify the last frame against the oracle rows")
     return ap.parse_args()
+
+
+DEFAULT_SLOTS = 3                    # frames in flight: 1080p 0.149 / 0.140 / 0.136 / 0.133 ms per frame at 1-4
+                                     # (profiles/r3/overlap_1080.txt); 3 keeps the latency at ~3 frames
 
 
 PATH_AMPLITUDE = 10                  # camera path: yaw sweeps +-10 mrad around the config view, 1 mrad/frame
@@ -319,18 +329,18 @@ def transfer_rates(ctx, torch, dev, stream, width, height, kernel, frames=8):
             "note": "PCIe-inclusive figures; `value` is the HBM-resident render rate"}
 
 
-def run_rows(args, torch, dist, dist_on, rank, n, kernel):
-    """--mode rows: ONE frame per step over N devices from one process (sf_group_*): member k traces the
+def run_rows(args, torch, ctl, n, kernel):
+    """--mode rows: ONE frame per step over N devices from ONE process (sf_group_*): member k traces the
     8-row bands b = k (mod N); members k > 0 ship theirs into member 0's G-buffer with strided peer copies.
-    The camera moves as in frames mode (frame i of the path at step i). When fewer than N devices are
-    visible (a one-GPU rehearsal) the members are N contexts on device 0, and the line says so."""
+    The camera moves as in the default mode. When fewer than N devices are visible (a one-GPU rehearsal) the
+    members are N contexts on device 0, and the line says so. The other ranks only join the barriers."""
     width, height, band = args.width, args.height, args.band_rows
     visible = torch.cuda.device_count()
     devices = list(range(n)) if visible >= n else [0] * n
     views = [frame_camera(width, height, args.K, i).corners() for i in range(args.warmup + args.steps)]
     g = None
-    first_ms = trace_ms = None
-    if rank == 0:
+    kp = ktiming_period(args.steps)
+    if ctl.rank == 0:
         g = sf.SphereflakeGroup(devices, width, height)
         if kernel != sf.SF_KERNEL_WAVE:
             raise SystemExit("--mode rows traces with the wave kernel")
@@ -342,51 +352,43 @@ def run_rows(args, torch, dist, dist_on, rank, n, kernel):
         for i in range(args.warmup):
             g.SetView(*views[i])
             g.Render(band)
-        g.member_kernel_timing(0, True, period=ktiming_period(args.steps))
+        g.member_kernel_timing(0, True, period=kp)
         g.Synchronize()
         g.reset_stats()
-    if dist_on:
-        dist.barrier()
+    ctl.barrier()
     t0 = time.perf_counter()
-    if rank == 0:
+    if ctl.rank == 0:
         for i in range(args.steps):
             g.SetView(*views[args.warmup + i])
             g.Render(band)
         g.Synchronize()
+    ctl.barrier()
     dt = time.perf_counter() - t0
-    if dist_on:
-        dist.barrier()
-    if rank != 0:
+    if ctl.rank != 0:
         return
     st = g.stats()
     if st.overflow_tiles:
         raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
-    tk = g.member_kernel_timing(0, n=min(-(-args.steps // ktiming_period(args.steps)), 64))
+    tk = g.member_kernel_timing(0, n=min(-(-args.steps // kp), 64))
     trace_ms = float(np.mean(tk)) if len(tk) else dt / args.steps * 1e3
     rays0 = sf.lib().sf_slab_rows(height, band, n, 0) * width   # member 0's rays per launch
     t_step = dt / args.steps
-    value = width * height / t_step / 1e6
     achieved = BYTES_PER_RAY * rays0 / (trace_ms * 1e-3) / 1e9
     gather_bytes = sum(sf.lib().sf_slab_rows(height, band, n, k) for k in range(1, n)) * width * BYTES_PER_RAY
     same_dev = len(set(devices)) < n
     g.close()
     out = {
-        "metric": "Mrays/sec into G-buffer at 1920x1080 depth-8; frame time ms",
-        "value": round(value, 2), "unit": "Mrays/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(t_step * 1e3, 4), "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic (deterministic camera path: config camera, yaw swept +-10 mrad at 1 mrad per frame; "
-                "no dataset)",
+        "metric": METRIC, "value": round(width * height / t_step / 1e6, 2), "unit": "Mrays/s", "n_gpus": n,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_step * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": DATA_MOVING,
         "config": {"workload": f"{width}x{height} primary-ray G-buffer, camera K={args.K:g}, one frame per step "
                                f"cut into {band}-row bands over {n} members, moving camera",
                    "width": width, "height": height, "K": args.K, "max_depth": st.max_depth, "camera": "moving",
                    "devices": devices,
-                   "parallelism": f"row-bands x{n} (sf_group: strided peer copies into device 0)"
+                   "parallelism": f"row-bands x{n} (sf_group: one process, strided peer copies into device 0)"
                                   + (" [rehearsal: all members on device 0]" if same_dev else "")},
-        "frame_ms": round(t_step * 1e3, 4),
-        "first_render_ms": round(first_ms, 4),
-        "gather_bytes_per_frame": gather_bytes,
-        "rays_per_step": width * height, "rays_counted": int(st.rays),
+        "frame_ms": round(t_step * 1e3, 4), "first_render_ms": round(first_ms, 4),
+        "gather_bytes_per_frame": gather_bytes, "rays_per_step": width * height, "rays_counted": int(st.rays),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": TRACE_KERNEL,
                      "kernel_ms": round(trace_ms, 4),
@@ -395,34 +397,148 @@ def run_rows(args, torch, dist, dist_on, rank, n, kernel):
     print(json.dumps(out), flush=True)
 
 
+METRIC = "Mrays/sec into G-buffer at 1920x1080 depth-8; frame time ms"
+DATA_MOVING = ("synthetic (deterministic camera path: config camera, yaw swept +-10 mrad at 1 mrad per frame; "
+               "no dataset)")
+
+
+class Control:
+    """Control plane of a multi-rank run: torch.distributed over gloo (barriers, the RCCL ids, the max over
+    ranks of the timed region). The frame data never goes through it: the gather is RCCL inside sf_dist."""
+
+    def __init__(self, world, rank):
+        self.world, self.rank = world, rank
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x):
+        if not self.dist:
+            return float(x)
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t[0])
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def slot_period(steps, slots):
+    """Kernel-timing period per slot so that every slot gives >= ceil(KTIMING_MIN_SAMPLES / slots) samples."""
+    per_slot = max(1, steps // slots)
+    need = -(-KTIMING_MIN_SAMPLES // slots)
+    return max(1, min(KTIMING_PERIOD, per_slot // need))
+
+
+def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows, nranks, frame_of,
+              fixed=False, latency=False, first=False):
+    """One timed loop of the sf_dist path: `steps` frames (frame_of(i) of the camera path at step i) after
+    `warmup`, `slots` in flight, over `nranks` ranks (1: this GPU alone, every rank its own frames). Barrier +
+    device sync on both sides of the timed region; the time is the max over ranks."""
+    rank = ctl.rank if nranks > 1 else 0
+    ids = shard.dist_ids(slots) if nranks > 1 else None
+    d = sf.SphereflakeDist(dev.index, width, height, rank=rank, nranks=nranks, slots=slots, ids=ids,
+                           band_rows=band_rows)
+    views = [frame_camera(width, height, k, frame_of(i)).corners() for i in range(warmup + steps)]
+    out = {}
+    ctl.barrier()
+    if first:   # the first render of a fresh context: row-major tile order, no cost history
+        d.SetView(*views[0])
+        t = time.perf_counter()
+        d.Render()
+        d.Synchronize()
+        out["first_render_ms"] = (time.perf_counter() - t) * 1e3
+    for i in range(warmup):
+        d.SetView(*views[i])
+        d.Render()
+    kp = slot_period(steps, slots)
+    for s in range(slots):
+        d.kernel_timing(s, True, period=kp)
+    d.Synchronize()
+    d.reset_stats()
+    torch.cuda.synchronize(dev)
+    ctl.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        d.SetView(*views[warmup + i])
+        d.Render()
+    d.Synchronize()
+    torch.cuda.synchronize(dev)
+    ctl.barrier()
+    torch.cuda.synchronize(dev)
+    out["t_step"] = ctl.max((time.perf_counter() - t0) / steps)
+    tk, clk = [], []
+    for s in range(slots):
+        tk += list(d.kernel_timing(s, n=64))
+        clk += list(d.kernel_clocks(s, n=64))
+        d.kernel_timing(s, False)
+    out["trace_ms"] = float(np.mean(tk)) if tk else None
+    out["kernel_samples"] = len(tk)
+    out["clock_mhz"] = float(np.median(clk)) if clk else None
+    st = d.stats()   # (collective over the ranks)
+    if st.overflow_tiles:
+        raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
+    out["stats"] = st
+    if fixed:   # the same loop on one unchanging view (the config camera)
+        d.SetView(*frame_camera(width, height, k, 0).corners())
+        for i in range(warmup):
+            d.Render()
+        d.Synchronize()
+        ctl.barrier()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            d.Render()
+        d.Synchronize()
+        ctl.barrier()
+        out["t_fixed"] = ctl.max((time.perf_counter() - t0) / steps)
+    out["last_view"] = frame_camera(width, height, k, 0).corners() if fixed else views[-1]
+    if latency:   # one frame at a time, each waited for (rank 0's wait includes the gather of the others)
+        lat = []
+        for i in range(20):
+            d.SetView(*views[i])
+            out["last_view"] = views[i]
+            ctl.barrier()
+            t = time.perf_counter()
+            d.Render()
+            d.Synchronize()
+            lat.append(time.perf_counter() - t)
+        out["latency_ms"] = ctl.max(float(np.median(lat))) * 1e3
+    out["dist"] = d
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
-    import torch.distributed as dist
-    dist_on = world > 1
-    # SF_BENCH_BACKEND=gloo + local ranks folded onto the visible devices: rehearses the multi-rank
-    # flow on a 1-GPU box (RCCL refuses two ranks on one GPU). The driver's runs use nccl (= RCCL).
-    backend = os.environ.get("SF_BENCH_BACKEND", "nccl")
-    gpu = local % max(1, torch.cuda.device_count()) if dist_on else 0
+    n = world
+    ndev = torch.cuda.device_count()
+    gpu = local % max(1, ndev) if world > 1 else 0
+    if args.mode == "dist" and world > 1 and ndev < world:
+        raise SystemExit(f"dist mode needs one GPU per rank (RCCL refuses two ranks on one device): {world} ranks, "
+                         f"{ndev} GPU(s); rehearse with --mode frames")
     torch.cuda.set_device(gpu)
-    if dist_on:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group(backend)
+    ctl = Control(world, rank)
     dev = torch.device("cuda", gpu)
     if not os.path.exists(sf.LIB_PATH):
         if rank == 0:
             sf.build()
-        if dist_on:
-            dist.barrier()
+        ctl.barrier()
     width, height = args.width, args.height
-    n = world
-    stream = torch.cuda.Stream(device=dev)
     kernel = sf.SF_KERNEL_WAVE if args.kernel == "wave" else sf.SF_KERNEL_PER_RAY
+    if kernel != sf.SF_KERNEL_WAVE and args.mode == "dist":
+        raise SystemExit("the per-ray kernel runs in --mode frames only")
 
     # a tiny render on a throw-away context first: loads the code object, so that `first_render_ms`
     # below is the first render of a fresh context, not the process's first kernel launch
@@ -432,171 +548,93 @@ def main():
         warm.Render()
         warm.Synchronize()
     module_load_ms = (time.perf_counter() - t_load) * 1e3
-    ctx = sf.Sphereflake(width, height, device=dev.index)
-    sh = stream.cuda_stream
 
     if args.mode == "rows":
-        run_rows(args, torch, dist, dist_on, rank, max(n, args.gpus), kernel)   # N devices, one driving process
-        ctx.close()
-        if dist_on:
-            dist.destroy_process_group()
+        run_rows(args, torch, ctl, max(n, args.gpus), kernel)
+        ctl.close()
         return
-    if args.mode == "frames":
-        # frame index = step * N + rank along the camera path (warmup, timed loop)
-        views = [frame_camera(width, height, args.K, i * n + rank).corners() for i in range(args.warmup + args.steps)]
-        rays_per_step_rank = width * height
-        slab_rows = height
-    else:
-        cam = sf.config_camera(width, height, args.K)
-        ctx.SetCamera(cam)
-        slab_rows = sf.lib().sf_slab_rows(height, args.band_rows, n, rank)
-        rays_per_step_rank = slab_rows * width
-        slab_p = torch.empty((slab_rows, width, 4), dtype=torch.float32, device=dev)
-        slab_n = torch.empty_like(slab_p)
-        max_rows = shard.max_slab_rows(height, args.band_rows, n)
-        send_p = torch.zeros((max_rows, width, 4), dtype=torch.float32, device=dev)
-        send_n = torch.zeros_like(send_p)
 
-    first_ms = None
-    if args.mode == "frames":
-        ctx.SetView(*views[0])
-        # the first render of a fresh context: row-major tile order, no cost history
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(stream):
-            e0.record(stream)
-            ctx.Render(kernel=kernel, stream=sh)
-            e1.record(stream)
-        torch.cuda.synchronize(dev)
-        first_ms = e0.elapsed_time(e1)
-    # HIP events around the dominant (trace) kernel of every KTIMING_PERIOD-th render: an event pair
-    # costs ~7 us of stream time per frame, so it is sampled (SF_BENCH_KTIMING=0: off, for A/B)
-    ktiming = os.environ.get("SF_BENCH_KTIMING", "1") != "0"
-    kp = ktiming_period(args.steps)
+    slots = max(1, min(8, args.slots))
+    if args.mode == "dist":
+        r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
+                      lambda i: i, fixed=True, latency=True, first=True)
+        rays_step = width * height
+    else:   # frames: every rank its own frames (frame i * N + rank), one GPU each, slots in flight
+        r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, 1,
+                      lambda i: i * n + rank, fixed=True, latency=True, first=True)
+        rays_step = width * height * n
+    d = r["dist"]
+    t_step = r["t_step"]
+    value = rays_step / t_step / 1e6
+    st = r["stats"]
 
-    ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    # weak-scaling companion of a multi-GPU run: every rank renders its own frames (no gather)
+    indep = None
+    if args.mode == "dist" and n > 1:
+        ri = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, 1,
+                       lambda i: i * n + rank)
+        ri["dist"].close()
+        indep = {"value": round(n * width * height / ri["t_step"] / 1e6, 2), "frame_ms": round(ri["t_step"] * 1e3, 4),
+                 "scaling": "weak", "note": "every rank renders its own full frames (frame i * N + rank), no gather"}
 
-    # whole-render events (kernel_ms) on the same sampled steps as the trace-kernel events: every
-    # event record on the stream costs GPU time between kernels (measured ~7 us per pair per frame)
-    def run_step(i, timed, view=None):
-        timed = timed and ktiming and i % kp == 0
-        with torch.cuda.stream(stream):
-            if timed:
-                ev_s[i].record(stream)
-            if args.mode == "frames":
-                if view is not None:
-                    ctx.SetView(*view)
-                ctx.Render(kernel=kernel, stream=sh)
-            else:
-                ctx.render_to(slab_p.data_ptr(), slab_n.data_ptr(), band_rows=args.band_rows, band_count=n,
-                              band_index=rank, compact=True, kernel=kernel, stream=sh)
-            if timed:
-                ev_e[i].record(stream)
-            if args.mode == "rows-rccl" and dist_on:
-                send_p[:slab_rows].copy_(slab_p)
-                send_n[:slab_rows].copy_(slab_n)
-                if backend == "nccl":
-                    shard.gather_frame(send_p, height, args.band_rows)   # RCCL gather + reassembly on rank 0
-                    shard.gather_frame(send_n, height, args.band_rows)
-                else:   # gloo rehearsal: host tensors
-                    shard.gather_frame(send_p.cpu(), height, args.band_rows)
-                    shard.gather_frame(send_n.cpu(), height, args.band_rows)
-
-    moving = args.mode == "frames"
-    for i in range(args.warmup):
-        run_step(i, False, views[i] if moving else None)
-    ctx.kernel_timing(ktiming, period=kp)   # samples timed renders 0, kp, 2 kp, ...
-    torch.cuda.synchronize(dev)
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        run_step(i, True, views[args.warmup + i] if moving else None)
-    torch.cuda.synchronize(dev)
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    dt = time.perf_counter() - t0
-    st = ctx.stats()
-    if st.overflow_tiles:
-        raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
-    kern_ms = (float(np.mean([ev_s[i].elapsed_time(ev_e[i]) for i in range(0, args.steps, kp)]))
-               if ktiming else dt / args.steps * 1e3)   # whole render, sampled
-    nks = min(-(-args.steps // kp), 64)
-    tk = ctx.kernel_timing(n=nks) if ktiming else []   # the trace kernel alone, last timed renders
-    clk = ctx.kernel_clocks(n=nks) if ktiming else []  # live shader clock of the same renders
-    trace_ms = float(np.mean(tk)) if len(tk) else kern_ms
-
-    # the same loop on one unchanging view (the config camera, frame 0 of the path): extra key, never `value`
-    fixed = None
-    if moving:
-        ctx.kernel_timing(False)
-        ctx.SetView(*views[0])
-        for i in range(args.warmup):
-            run_step(i, False)
-        torch.cuda.synchronize(dev)
-        if dist_on:
-            dist.barrier()
-        tf = time.perf_counter()
-        for i in range(args.steps):
-            run_step(i, False)
-        torch.cuda.synchronize(dev)
-        if dist_on:
-            dist.barrier()
-        t_fixed = (time.perf_counter() - tf) / args.steps
-        if dist_on:
-            tt = torch.tensor([t_fixed], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            t_fixed = float(tt[0])
-        fixed = {"value": round(n * width * height / t_fixed / 1e6, 2), "frame_ms": round(t_fixed * 1e3, 4),
-                 "note": "same timed loop on the unchanging config view (heavy-first order from identical frames)"}
-
-    t_step = dt / args.steps
-    if dist_on:
-        tt = torch.tensor([t_step, kern_ms, trace_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_step, kern_ms_max, trace_ms = float(tt[0]), float(tt[1]), float(tt[2])
-    else:
-        kern_ms_max = kern_ms
-    total_rays = rays_per_step_rank * n if args.mode == "frames" else width * height
-    value = total_rays / t_step / 1e6
-
-    # SSAO post-process of the rendered G-buffer, timed alone on the render stream
-    post = None
-    if rank == 0 and args.mode == "frames" and not args.no_extras:
-        post = post_rates(ctx, torch, stream, width, height)
-
-    # D2H into the host GBuffer (PCIe-inclusive, reported separately -- never `value`)
-    d2h = None
-    if rank == 0 and args.mode == "frames" and not args.no_extras:
-        d2h = transfer_rates(ctx, torch, dev, stream, width, height, kernel)
-    prog = None
-    if rank == 0 and args.mode == "frames" and not args.no_extras:
-        prog = progressive_rates(width, height, args.K)
+    # BASELINE configs[3] (3840x2160, K = 0.22, depth 9) on the same path, all ranks
+    c4 = None
+    if not args.no_extras and (width, height, round(args.K, 4)) == (W, H, K):
+        r4 = dist_loop(ctl, torch, dev, 3840, 2160, 0.22, 60, 15, slots, args.band_rows,
+                       n if args.mode == "dist" else 1, (lambda i: i) if args.mode == "dist" else (lambda i: i * n + rank))
+        rays0_4 = (sf.lib().sf_slab_rows(2160, args.band_rows, n, 0) if args.mode == "dist" else 2160) * 3840
+        a4 = BYTES_PER_RAY * rays0_4 / (r4["trace_ms"] * 1e-3) / 1e9 if r4["trace_ms"] else None
+        c4 = {"config": "BASELINE configs[3]: 3840x2160, K=0.22", "max_depth": r4["stats"].max_depth,
+              "value": round((3840 * 2160 * (n if args.mode == "frames" else 1)) / r4["t_step"] / 1e6, 2),
+              "frame_ms": round(r4["t_step"] * 1e3, 4), "steps": 60, "warmup": 15,
+              "roofline": {"achieved": round(a4, 2) if a4 else None, "frac": round(a4 / HBM_PEAK_GBS, 5) if a4 else None,
+                           "kernel_ms": round(r4["trace_ms"], 4) if r4["trace_ms"] else None,
+                           "kernel_samples": r4["kernel_samples"],
+                           "clock_mhz_live": round(r4["clock_mhz"], 1) if r4["clock_mhz"] else None}}
+        r4["dist"].close()
 
     check = None
-    if args.check and rank == 0 and args.mode == "frames":
+    if args.check and rank == 0:
         from oracle import pyoracle
-        pos, nrm, _, _ = ctx.download()
-        o, tl, tr, bl = views[0]
+        pos, nrm = d.download()
+        o, tl, tr, bl = r["last_view"]
         setup = {"W": width, "H": height, "origin": o, "tl": tl, "tr": tr, "bl": bl,
                  "root": sf.root_transform(o), "children": sf.child_transforms()}
         rows = np.linspace(0, height - 1, 12).astype(int)
-        r = pyoracle.render(setup, rows=rows)
-        check = bool(np.array_equal(r["pos4"].view(np.uint32), pos[rows].view(np.uint32)) and
-                     np.array_equal(r["nrm4"].view(np.uint32), nrm[rows].view(np.uint32)))
+        ro = pyoracle.render(setup, rows=rows)
+        check = bool(np.array_equal(ro["pos4"].view(np.uint32), pos[rows].view(np.uint32)) and
+                     np.array_equal(ro["nrm4"].view(np.uint32), nrm[rows].view(np.uint32)))
+    d.close()
+
+    post = d2h = prog = None
+    if rank == 0 and n == 1 and not args.no_extras:
+        # the consumers of the G-buffer on a plain context: SSAO post-process, D2H into the
+        # host GBuffer (PCIe-inclusive, never `value`, §8(f3)), the frame-less mode (§8(f1))
+        stream = torch.cuda.Stream(device=dev)
+        with sf.Sphereflake(width, height, device=dev.index) as ctx:
+            ctx.SetCamera(sf.config_camera(width, height, args.K))
+            ctx.Render()
+            ctx.Synchronize()
+            post = post_rates(ctx, torch, stream, width, height)
+            d2h = transfer_rates(ctx, torch, dev, stream, width, height, kernel)
+        prog = progressive_rates(width, height, args.K)
 
     if rank == 0:
-        per_launch_bytes = BYTES_PER_RAY * rays_per_step_rank
-        achieved = per_launch_bytes / (trace_ms * 1e-3) / 1e9
-        camera = "moving" if moving else "fixed"
+        band = args.band_rows
+        rays0 = (sf.lib().sf_slab_rows(height, band, n, 0) if args.mode == "dist" else height) * width
+        trace_ms = r["trace_ms"] or t_step * 1e3
+        achieved = BYTES_PER_RAY * rays0 / (trace_ms * 1e-3) / 1e9
         build = sf.build_info()
-        pmc, _ = load_pmc(TRACE_KERNEL, pmc_config_key(width, height, args.K, camera), build)
-        traffic = pmc_traffic(pmc)
+        pmc, _ = load_pmc(TRACE_KERNEL, pmc_config_key(width, height, args.K, "moving"), build)
+        traffic = pmc_traffic(pmc) if n == 1 else None
         cfg_name = BASELINE_CONFIGS.get((width, height, round(args.K, 4)))
+        if args.mode == "dist":
+            par = (f"dist x{n}: interleaved {band}-row bands, ranks > 0 send packed slabs (16 B/px) to rank 0 over "
+                   f"RCCL; {slots} frames in flight" if n > 1 else f"1 GPU, {slots} frames in flight (sf_dist slots)")
+        else:
+            par = f"frames x{n} (independent frames per rank, {slots} in flight each)"
         out = {
-            "metric": "Mrays/sec into G-buffer at 1920x1080 depth-8; frame time ms",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "Mrays/s",
             "n_gpus": n,
@@ -604,38 +642,46 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(t_step * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak" if args.mode == "frames" else "strong",
+            "scaling": "strong" if args.mode == "dist" else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (deterministic camera path: config camera, yaw swept +-10 mrad at 1 mrad per frame; "
-                    "no dataset)"
-                    if moving else "synthetic (deterministic fixed-camera frames; no dataset)",
+            "data": DATA_MOVING,
             "config": {"workload": f"{width}x{height} primary-ray G-buffer, camera K={args.K:g} (reference max "
-                                   f"depth {st.max_depth})"
-                                   + (f", BASELINE {cfg_name}" if cfg_name else "")
-                                   + f", {camera} camera, {args.kernel} kernel",
-                       "width": width, "height": height, "K": args.K, "max_depth": st.max_depth, "camera": camera,
-                       "parallelism": f"frames x{n}" if args.mode == "frames" else f"row-bands x{n} + RCCL gather (per rank)"},
+                                   f"depth {st.max_depth})" + (f", BASELINE {cfg_name}" if cfg_name else "")
+                                   + f", moving camera, {args.kernel} kernel",
+                       "width": width, "height": height, "K": args.K, "max_depth": st.max_depth, "camera": "moving",
+                       "slots": slots, "parallelism": par},
             "frame_ms": round(t_step * 1e3, 4),
-            "kernel_ms": round(kern_ms_max, 4),
-            "first_render_ms": round(first_ms, 4) if first_ms is not None else None,
+            "frame_latency_ms": round(r["latency_ms"], 4),
+            "first_render_ms": round(r["first_render_ms"], 4),
             "process_first_launch_ms": round(module_load_ms, 3),
-            "fixed_camera": fixed,
-            "post": post,
-            "d2h": d2h,
-            "frameless": prog,
+            "fixed_camera": {"value": round(rays_step / r["t_fixed"] / 1e6, 2), "frame_ms": round(r["t_fixed"] * 1e3, 4),
+                             "note": "same timed loop on the unchanging config view"},
+            "rays_counted": int(st.rays),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": round(traffic) if traffic else None,
-                         "kernel": TRACE_KERNEL, "kernel_ms": round(trace_ms, 4), "kernel_samples": len(tk),
-                         "clock_mhz_live": round(float(np.median(clk)), 1) if len(clk) else None,
-                         "note": "path is VALU/latency-bound (SURVEY.md §8(d), see `valu`); achieved = 32 B/ray x "
-                                 "rays per launch / mean duration of the trace kernel (HIP events around it on its "
-                                 "launch stream); traffic = PMC WRITE_SIZE + 2 x FETCH_SIZE per launch "
-                                 "(profiles/pmc_traffic.json, only when profiled on this config, else null)"},
-            "valu": pmc_valu(pmc),
+                         "kernel": TRACE_KERNEL, "kernel_ms": round(trace_ms, 4), "kernel_samples": r["kernel_samples"],
+                         "clock_mhz_live": round(r["clock_mhz"], 1) if r["clock_mhz"] else None,
+                         "frame_rate_GBps": round(BYTES_PER_RAY * width * height / t_step / 1e9, 2),
+                         "note": "path is VALU/latency-bound (SURVEY.md §8(d), see `valu`); achieved = 32 B/ray x rank 0's "
+                                 "rays per launch / mean duration of its trace kernel (HIP events around it on its "
+                                 "stream; with frames in flight a kernel shares the GPU with the next frame's); "
+                                 "frame_rate_GBps = 32 B/ray of the whole frame per frame period; traffic = PMC "
+                                 "WRITE_SIZE + 2 x FETCH_SIZE per launch (profiles/pmc_traffic.json, only for this "
+                                 "config and this library build, else null)"},
+            "valu": pmc_valu(pmc) if n == 1 else None,
             "build": build,
         }
+        if n > 1 and args.mode == "dist":
+            out["gather"] = {"bytes_per_frame": sum(sf.lib().sf_slab_rows(height, band, n, k) for k in range(1, n)) * width * 16,
+                             "format": "packed float4 (nx, ny, nz, minT) per pixel; rank 0 rebuilds pos = dir * minT",
+                             "transport": "RCCL grouped ncclSend/ncclRecv to rank 0 (xGMI), one communicator per slot"}
+            out["independent_frames"] = indep
+        if c4 is not None:
+            out["configs"] = {"c4": c4}
+        if post is not None:
+            out["post"], out["d2h"], out["frameless"] = post, d2h, prog
         if check is not None:
             out["check_rows_bit_exact"] = check
         if not args.no_cpu_baseline and n == 1:
@@ -655,9 +701,7 @@ def main():
             except Exception as e:  # never lose the GPU number over the baseline leg
                 out["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(out), flush=True)
-    ctx.close()
-    if dist_on:
-        dist.destroy_process_group()
+    ctl.close()
 
 
 if __name__ == "__main__":

@@ -12,8 +12,8 @@
 //   the frame-less loop under a moving view (main.cpp:304 calls SetView every frame while the workers
 //   trace): views.bin holds V views (12 float32 each: origin, TL, TR, BL); view 0 is set before
 //   Initialize, then view j % V every period_us. Each SetView's latency is measured; log.txt gets one line
-//   "view packet" per call (the loop's counter when it took effect). Prints
-//   "packets max_depth rays calls max_latency_us elapsed_us".
+//   "view packet" per call (the loop's counter when it took effect). Latencies are taken once the loop has
+//   traced 2 batches. Prints "packets max_depth rays calls max_latency_us elapsed_us batches_in_elapsed".
 //
 // usage: class_drive --initialize W H corners(12) out.bin seed batch ms
 //   the frame-less mode as main.cpp:120-121 starts it: SetView, Initialize(seed, batch), let the loop run
@@ -99,7 +99,11 @@ static int moving_mode(int argc, char** argv)
     if (!log) return 4;
     std::fprintf(log, "0 0\n");
     flake.Initialize(seed, batch);
+    // latencies are measured once the loop runs steadily: its first batches also allocate the frame-less
+    // buffers and load the kernels (tens of ms)
+    while (flake.GetPacketsTraced() < 2ull * batch) std::this_thread::sleep_for(std::chrono::microseconds(200));
     const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t p0 = flake.GetPacketsTraced();
     double max_lat = 0.0;
     size_t calls = 0;
     while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(ms)) {
@@ -112,8 +116,9 @@ static int moving_mode(int argc, char** argv)
         std::fprintf(log, "%zu %llu\n", j, (unsigned long long)flake.GetViewChangePacket());
         ++calls;
     }
-    flake.Deinitialize();
+    const uint64_t p1 = flake.GetPacketsTraced();
     const double elapsed = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    flake.Deinitialize();
     std::fclose(log);
     const uint64_t packets = flake.GetPacketsTraced();
     const GBuffer& g = flake.GetGBuffer();
@@ -122,8 +127,8 @@ static int moving_mode(int argc, char** argv)
     std::fwrite(g.positions.data(), sizeof(sf_vec4), g.positions.size(), out);
     std::fwrite(g.normals.data(), sizeof(sf_vec4), g.normals.size(), out);
     std::fclose(out);
-    std::printf("%llu %d %lld %zu %.1f %.1f\n", (unsigned long long)packets, flake.GetMaxDepthReached(),
-                flake.GetRaysPerSecond(), calls, max_lat, elapsed);
+    std::printf("%llu %d %lld %zu %.1f %.1f %llu\n", (unsigned long long)packets, flake.GetMaxDepthReached(),
+                flake.GetRaysPerSecond(), calls, max_lat, elapsed, (unsigned long long)((p1 - p0) / batch));
     return 0;
 }
 
