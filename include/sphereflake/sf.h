@@ -294,11 +294,13 @@ int sf_kernel_clocks(sf_ctx* ctx, float* mhz, uint32_t n);
 /* --- multi-GPU ------------------------------------------ */
 /* One process, n member devices (the reference's host thread pool, Sphereflake.cpp:67-74, becomes n
    GPUs). The frame is cut into interleaved bands of band_rows rows, band b traced by member b % n;
-   member 0 holds the final G-buffer (its context's buffers): it writes its bands in place, member
-   k > 0 traces its bands into a compact slab on its device and copies it into member 0's G-buffer with
-   one strided peer copy per buffer over xGMI, queued on its own stream right behind its render (so a
-   member's copies overlap the other members' still-running traces). A device may appear more than once (n contexts on one GPU: the single-GPU test of the
-   path). Stats combine: max depth max, closest min, rays and overflow tiles summed. */
+   member 0 holds the final G-buffer (its context's buffers): it writes its bands in place; member k > 0
+   traces its bands as a packed slab (16 B/pixel, sf_render_params.packed) and copies it over xGMI into
+   member 0's stage on a copy stream of its own (overlapping its next frame's trace); member 0's stream
+   waits for the copies and unpacks the stage into its G-buffer (sf_unpack_bands). Slabs and stages are
+   double-buffered by frame parity, so members run a frame ahead of member 0. A device may appear more than
+   once (n contexts on one GPU: the single-GPU test of the path). Stats combine: max depth max, closest min,
+   rays and overflow tiles summed. */
 typedef struct sf_group sf_group;
 int sf_group_create(const int* devices, int n, uint32_t width, uint32_t height, sf_group** out);
 void sf_group_destroy(sf_group* group);

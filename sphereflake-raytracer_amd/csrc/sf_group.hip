@@ -4,14 +4,16 @@
 // renders into the one shared G-buffer. Here the frame is cut into interleaved bands of band_rows
 // rows (band b -> member b mod n: flake rows cost ~150 nodes per ray, sky rows ~1, so contiguous
 // halves would be badly unbalanced) and every member device traces its own bands. Member 0 writes its
-// bands straight into its own (final) G-buffer at frame positions; member k > 0 traces its bands into
-// a compact slab in its own HBM and ships it to member 0 with ONE strided 2D copy per buffer over
-// xGMI (slab band i -> frame band i*n + k: source pitch one band, destination pitch n bands), queued
-// on its own stream right behind its render, so they overlap the other members' still-running traces. No
-// reassembly pass, no staging copy, no host round trip. The copies into member 0's buffers wait for
-// the work member 0's stream had queued when the frame was issued (its consumers of the previous
-// frame), and member 0's stream waits for every member's copies, so anything queued on member 0's
-// context after sf_group_render (download, post-process) sees the whole frame.
+// bands straight into its own (final) G-buffer at frame positions; member k > 0 traces its bands into a
+// PACKED compact slab in its own HBM (one float4 (nx, ny, nz, minT) per pixel: half the G-buffer's 32 B;
+// the position is dir * minT, rebuilt bit for bit on member 0) and ships it with one contiguous peer copy
+// over xGMI into member 0's stage, on a copy stream of its own, so the next frame's trace on the member
+// overlaps the copy. Member 0's stream waits for the frame's copies and unpacks the stage into the G-buffer
+// (sf_unpack_bands): only member 0's own stream ever writes its G-buffer, so work queued on member 0's
+// context after sf_group_render (download, post-process) sees the whole frame, and consumers of the
+// previous frame queued before it are never overwritten. Slabs and stages are double-buffered by frame
+// parity: member k traces frame f + 1 while frame f's copy drains, and frame f + 2's copy into a stage waits
+// only for member 0's unpack of frame f from it.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -28,10 +30,16 @@ struct sf_group {
     uint32_t W = 0, H = 0;
     std::vector<int> device;
     std::vector<sf_ctx*> ctx;
-    std::vector<float*> slab_pos, slab_nrm;   // members k > 0: compact band slabs on their device
-    std::vector<uint32_t> slab_rows;
-    std::vector<hipEvent_t> copied;      // member k's copies of the frame done (its stream)
-    hipEvent_t issued = nullptr;         // member 0's stream at frame issue (its previous consumers)
+    // per parity b (frame & 1)
+    std::vector<float*> slab[2];         // members k > 0: packed compact band slab on their device
+    float* stage[2] = { nullptr, nullptr };   // member 0: members 1..n-1's slabs, stage_rows x W float4 each
+    std::vector<hipEvent_t> traced[2];   // member k's trace of the frame done (its context stream)
+    std::vector<hipEvent_t> copied[2];   // member k's copy into member 0's stage done (its copy stream)
+    hipEvent_t unpacked[2] = { nullptr, nullptr };   // member 0 done reading stage[b] (its stream)
+    std::vector<hipStream_t> copy;       // members k > 0: copy stream
+    uint32_t band_rows = 0, stage_rows = 0;   // the split the buffers are sized for (0: none yet)
+    uint64_t frames = 0;
+    bool stage_used[2] = { false, false };
     int last_hip = 0;
 };
 
@@ -59,20 +67,47 @@ struct Dev {
         }                                       \
     } while (0)
 
+void free_buffers(sf_group* g)
+{
+    for (int b = 0; b < 2; ++b) {
+        for (int k = 0; k < g->n; ++k) {
+            if (k < (int)g->slab[b].size() && g->slab[b][k]) {
+                Dev d(g->device[k]);
+                (void)hipFree(g->slab[b][k]);
+                g->slab[b][k] = nullptr;
+            }
+        }
+        if (g->stage[b]) {
+            Dev d(g->device[0]);
+            (void)hipFree(g->stage[b]);
+            g->stage[b] = nullptr;
+        }
+        g->stage_used[b] = false;
+    }
+    g->band_rows = g->stage_rows = 0;
+}
+
 void free_group(sf_group* g)
 {
-    for (int k = 0; k < g->n; ++k) {
+    for (int k = 0; k < g->n; ++k)
         if (k < (int)g->ctx.size() && g->ctx[k]) sf_synchronize(g->ctx[k]);
-    }
     for (int k = 0; k < g->n; ++k) {
         Dev d(g->device[k]);
-        if (k < (int)g->copied.size() && g->copied[k]) (void)hipEventDestroy(g->copied[k]);
-        if (k < (int)g->slab_pos.size()) (void)hipFree(g->slab_pos[k]);
-        if (k < (int)g->slab_nrm.size()) (void)hipFree(g->slab_nrm[k]);
+        if (k < (int)g->copy.size() && g->copy[k]) (void)hipStreamSynchronize(g->copy[k]);
     }
-    if (g->issued) {
+    free_buffers(g);
+    for (int k = 0; k < g->n; ++k) {
+        Dev d(g->device[k]);
+        for (int b = 0; b < 2; ++b) {
+            if (k < (int)g->traced[b].size() && g->traced[b][k]) (void)hipEventDestroy(g->traced[b][k]);
+            if (k < (int)g->copied[b].size() && g->copied[b][k]) (void)hipEventDestroy(g->copied[b][k]);
+        }
+        if (k < (int)g->copy.size() && g->copy[k]) (void)hipStreamDestroy(g->copy[k]);
+    }
+    {
         Dev d(g->device[0]);
-        (void)hipEventDestroy(g->issued);
+        for (int b = 0; b < 2; ++b)
+            if (g->unpacked[b]) (void)hipEventDestroy(g->unpacked[b]);
     }
     for (sf_ctx* c : g->ctx) sf_destroy(c);
     delete g;
@@ -91,10 +126,12 @@ extern "C" int sf_group_create(const int* devices, int n, uint32_t width, uint32
     g->H = height;
     g->device.assign(devices, devices + n);
     g->ctx.assign(n, nullptr);
-    g->slab_pos.assign(n, nullptr);
-    g->slab_nrm.assign(n, nullptr);
-    g->slab_rows.assign(n, 0u);
-    g->copied.assign(n, nullptr);
+    g->copy.assign(n, nullptr);
+    for (int b = 0; b < 2; ++b) {
+        g->slab[b].assign(n, nullptr);
+        g->traced[b].assign(n, nullptr);
+        g->copied[b].assign(n, nullptr);
+    }
     for (int k = 0; k < n; ++k) {
         const int rc = sf_create(devices[k], width, height, &g->ctx[k]);
         if (rc != SF_OK) {
@@ -102,7 +139,7 @@ extern "C" int sf_group_create(const int* devices, int n, uint32_t width, uint32
             return rc;
         }
     }
-    // peer access between member 0 and every other device (copies into member 0's G-buffer)
+    // peer access between member 0 and every other device (copies into member 0's stage)
     for (int k = 1; k < n; ++k) {
         if (devices[k] == devices[0]) continue;
         int ok = 0;
@@ -121,16 +158,18 @@ extern "C" int sf_group_create(const int* devices, int n, uint32_t width, uint32
             (void)hipGetLastError();   // clear an "already enabled"
         }
     }
-    {
-        Dev d(devices[0]);
-        if (hipEventCreateWithFlags(&g->issued, hipEventDisableTiming) != hipSuccess) {
-            free_group(g);
-            return SF_EHIP;
-        }
-    }
     for (int k = 0; k < n; ++k) {
         Dev d(devices[k]);
-        if (hipEventCreateWithFlags(&g->copied[k], hipEventDisableTiming) != hipSuccess) {
+        bool ok = true;
+        for (int b = 0; b < 2; ++b) {
+            if (k == 0) ok = ok && hipEventCreateWithFlags(&g->unpacked[b], hipEventDisableTiming) == hipSuccess;
+            if (k > 0) {
+                ok = ok && hipEventCreateWithFlags(&g->traced[b][k], hipEventDisableTiming) == hipSuccess;
+                ok = ok && hipEventCreateWithFlags(&g->copied[b][k], hipEventDisableTiming) == hipSuccess;
+            }
+        }
+        if (k > 0) ok = ok && hipStreamCreateWithFlags(&g->copy[k], hipStreamNonBlocking) == hipSuccess;
+        if (!ok) {
             free_group(g);
             return SF_EHIP;
         }
@@ -175,77 +214,74 @@ extern "C" int sf_group_render(sf_group* g, uint32_t band_rows)
     if (band_rows == 0) band_rows = 8;
     if (band_rows % 8 != 0) return SF_EINVAL;
     const uint32_t n = (uint32_t)g->n, W = g->W, H = g->H;
-    const uint32_t bands = (H + band_rows - 1) / band_rows;
-    const size_t band_bytes = (size_t)band_rows * W * 16;   // one band of one buffer (float4 per pixel)
-    float *pos0 = nullptr, *nrm0 = nullptr;
-    if (int rc = sf_device_buffers(g->ctx[0], &pos0, &nrm0, nullptr, nullptr)) return rc;
-    for (uint32_t k = 0; k < n; ++k) {
+    if (g->band_rows != band_rows) {   // (re)size the slabs and stages for this split
+        if (int rc = sf_group_synchronize(g)) return rc;
+        for (uint32_t k = 1; k < n; ++k) {
+            Dev d(g->device[k]);
+            SFG_HIP(g, hipStreamSynchronize(g->copy[k]));
+        }
+        free_buffers(g);
+        uint32_t sr = 0;
+        for (uint32_t k = 1; k < n; ++k) sr = std::max(sr, sf_slab_rows(H, band_rows, n, k));
+        for (int b = 0; b < 2; ++b) {
+            for (uint32_t k = 1; k < n; ++k) {
+                const uint32_t rows = sf_slab_rows(H, band_rows, n, k);
+                if (!rows) continue;
+                Dev d(g->device[k]);
+                SFG_HIP(g, hipMalloc(&g->slab[b][k], (size_t)rows * W * 16));
+            }
+            if (sr) {
+                Dev d(g->device[0]);
+                SFG_HIP(g, hipMalloc(&g->stage[b], (size_t)(n - 1) * sr * W * 16));
+            }
+        }
+        g->band_rows = band_rows;
+        g->stage_rows = sr;
+    }
+    const int b = (int)(g->frames & 1u);
+    const size_t stage_slab = (size_t)g->stage_rows * W * 16;   // bytes per member in the stage
+    // members k > 0: trace the packed slab, then copy it into member 0's stage on the copy stream
+    for (uint32_t k = 1; k < n; ++k) {
+        const uint32_t rows = sf_slab_rows(H, band_rows, n, k);
+        if (rows == 0) continue;
+        Dev d(g->device[k]);
+        hipStream_t sk = (hipStream_t)sf_context_stream(g->ctx[k]);
+        // slab[b] was last read by the copy of frame f - 2
+        if (g->frames >= 2) SFG_HIP(g, hipStreamWaitEvent(sk, g->copied[b][k], 0));
         sf_render_params p;
         std::memset(&p, 0, sizeof p);
         p.band_rows = band_rows;
         p.band_count = n;
         p.band_index = k;
-        if (k == 0) {
-            // member 0: its bands straight into the final G-buffer, at frame positions
-            if (int rc = sf_render(g->ctx[0], &p)) return rc;
-            continue;
-        }
         p.compact = 1;
-        const uint32_t rows = sf_slab_rows(H, band_rows, n, k);
-        if (rows == 0) continue;
-        Dev d(g->device[k]);
-        if (g->slab_rows[k] != rows || !g->slab_pos[k]) {
-            // the old slabs may still be copied from
-            SFG_HIP(g, hipStreamSynchronize((hipStream_t)sf_context_stream(g->ctx[k])));
-            (void)hipFree(g->slab_pos[k]);
-            (void)hipFree(g->slab_nrm[k]);
-            g->slab_pos[k] = g->slab_nrm[k] = nullptr;
-            g->slab_rows[k] = 0;
-            SFG_HIP(g, hipMalloc(&g->slab_pos[k], (size_t)rows * W * 16));
-            SFG_HIP(g, hipMalloc(&g->slab_nrm[k], (size_t)rows * W * 16));
-            g->slab_rows[k] = rows;
-        }
-        if (int rc = sf_render_to(g->ctx[k], &p, g->slab_pos[k], g->slab_nrm[k], nullptr, nullptr)) return rc;
+        p.packed = 1;
+        if (int rc = sf_render_to(g->ctx[k], &p, g->slab[b][k], nullptr, nullptr, nullptr)) return rc;
+        SFG_HIP(g, hipEventRecord(g->traced[b][k], sk));
+        SFG_HIP(g, hipStreamWaitEvent(g->copy[k], g->traced[b][k], 0));
+        // stage[b] was last read by member 0's unpack of frame f - 2
+        if (g->stage_used[b]) SFG_HIP(g, hipStreamWaitEvent(g->copy[k], g->unpacked[b], 0));
+        SFG_HIP(g, hipMemcpyAsync(reinterpret_cast<char*>(g->stage[b]) + (size_t)(k - 1) * stage_slab, g->slab[b][k],
+                                  (size_t)rows * W * 16, hipMemcpyDeviceToDevice, g->copy[k]));
+        SFG_HIP(g, hipEventRecord(g->copied[b][k], g->copy[k]));
     }
-    // Member 0's stream now ends with this frame's render, behind everything queued on it before
-    // (consumers of the previous frame): the copies into its buffers wait for that point.
-    hipStream_t s0 = (hipStream_t)sf_context_stream(g->ctx[0]);
-    {
+    // member 0: its bands in place, then (after the copies) the others' unpacked beside them, all on its
+    // own stream
+    sf_render_params p;
+    std::memset(&p, 0, sizeof p);
+    p.band_rows = band_rows;
+    p.band_count = n;
+    p.band_index = 0;
+    if (int rc = sf_render(g->ctx[0], &p)) return rc;
+    if (n > 1 && g->stage_rows) {
         Dev d(g->device[0]);
-        SFG_HIP(g, hipEventRecord(g->issued, s0));
-    }
-    for (uint32_t k = 1; k < n; ++k) {
-        const uint32_t rows = sf_slab_rows(H, band_rows, n, k);
-        if (rows == 0) continue;
-        Dev d(g->device[k]);
-        // owned bands: k, k + n, ...; the full ones as one strided copy per buffer, a partial last band apart
-        uint32_t nb = 0, full = 0;
-        for (uint32_t b = k; b < bands; b += n) {
-            ++nb;
-            if ((b + 1) * band_rows <= H) ++full;
-        }
-        hipStream_t sk = (hipStream_t)sf_context_stream(g->ctx[k]);
-        SFG_HIP(g, hipStreamWaitEvent(sk, g->issued, 0));   // (the member's render is queued before this)
-        for (int buf = 0; buf < 2; ++buf) {
-            char* dst = reinterpret_cast<char*>(buf ? nrm0 : pos0);
-            const char* src = reinterpret_cast<const char*>(buf ? g->slab_nrm[k] : g->slab_pos[k]);
-            if (full)
-                SFG_HIP(g, hipMemcpy2DAsync(dst + (size_t)k * band_bytes, (size_t)n * band_bytes, src, band_bytes,
-                                            band_bytes, full, hipMemcpyDeviceToDevice, sk));
-            if (full < nb) {   // the frame's last band, shorter than band_rows
-                const uint32_t b = k + full * n;
-                const size_t bytes = (size_t)(H - b * band_rows) * W * 16;
-                SFG_HIP(g, hipMemcpyAsync(dst + (size_t)b * band_bytes, src + (size_t)full * band_bytes, bytes,
-                                          hipMemcpyDeviceToDevice, sk));
-            }
-        }
-        SFG_HIP(g, hipEventRecord(g->copied[k], sk));
-    }
-    {   // member 0's stream waits for every member's copies: later work on it sees the whole frame
-        Dev d(g->device[0]);
+        hipStream_t s0 = (hipStream_t)sf_context_stream(g->ctx[0]);
         for (uint32_t k = 1; k < n; ++k)
-            if (sf_slab_rows(H, band_rows, n, k)) SFG_HIP(g, hipStreamWaitEvent(s0, g->copied[k], 0));
+            if (sf_slab_rows(H, band_rows, n, k)) SFG_HIP(g, hipStreamWaitEvent(s0, g->copied[b][k], 0));
+        if (int rc = sf_unpack_bands(g->ctx[0], g->stage[b], g->stage_rows, band_rows, n, 1, n - 1, nullptr)) return rc;
+        SFG_HIP(g, hipEventRecord(g->unpacked[b], s0));
+        g->stage_used[b] = true;
     }
+    ++g->frames;
     return SF_OK;
 }
 

@@ -1,8 +1,9 @@
 """GPU: single-process multi-GPU rendering behind the C ABI (sf_group_*). The group
-cuts the frame into interleaved bands, traces them on its members and gathers them into member 0's
-G-buffer with strided peer copies. On a one-GPU box the members are n contexts on device 0 (own
-streams, same copy path); the assembled frame must equal the golden c2/c3 frames bit for bit and the
-one-context render of any other view, frame after frame."""
+cuts the frame into interleaved bands, traces them on its members (members > 0 as packed slabs) and
+copies those into member 0's stage, where they are unpacked into its G-buffer. On a one-GPU box the
+members are n contexts on device 0 (own streams, same copy path); the assembled frame must equal the
+golden c2/c3 frames bit for bit and the one-context render of any other view, frame after frame, also
+with several frames in flight (double-buffered slabs and stages)."""
 import numpy as np
 import pytest
 
@@ -113,3 +114,50 @@ def test_group_across_devices(device):
         g.Render(8)
         pos, nrm = g.download()
     assert frame_digest(pos, nrm) == fx["frame_digest"]
+
+
+def test_group_pipelined_frames_equal_single():
+    """Five frames of different views issued back to back (members race ahead of member 0 by a frame:
+    double-buffered slabs and stages), each captured by an asynchronous D2H queued on member 0's stream
+    right after its render: every capture equals the one-context render of its view."""
+    import ctypes
+    W, H = 200, 120
+    views = []
+    for j in range(5):
+        cam = sf.config_camera(W, H, 0.25)
+        cam.SetYaw(np.float32(sf.DEFAULT_YAW + 0.015 * (j - 2)))
+        views.append(cam)
+    L = sf.lib()
+    caps = [(np.zeros((H, W, 4), np.float32), np.zeros((H, W, 4), np.float32)) for _ in views]
+    for p, n in caps:
+        for a in (p, n):
+            assert L.sf_host_register(a.ctypes.data_as(ctypes.c_void_p), a.nbytes) == 0
+    try:
+        with sf.SphereflakeGroup([0, 0, 0], W, H) as g:
+            c0 = g.member(0)
+            for cam, (p, n) in zip(views, caps):
+                g.SetCamera(cam)
+                g.Render(8)
+                assert L.sf_download_async(c0, p.ctypes.data_as(ctypes.c_void_p), n.ctypes.data_as(ctypes.c_void_p),
+                                           None, None, None) == 0
+            g.Synchronize()
+        for j, (cam, (p, n)) in enumerate(zip(views, caps)):
+            spos, snrm, _ = single(W, H, cam)
+            assert same_bits(p, spos) and same_bits(n, snrm), f"frame {j}"
+    finally:
+        for p, n in caps:
+            for a in (p, n):
+                L.sf_host_unregister(a.ctypes.data_as(ctypes.c_void_p))
+
+
+def test_group_band_split_change_resizes():
+    """Switching the band height between frames re-sizes the slabs and stages (after draining the old ones)."""
+    W, H = 96, 72
+    cam = sf.config_camera(W, H, 0.25)
+    spos, snrm, _ = single(W, H, cam)
+    with sf.SphereflakeGroup([0, 0], W, H) as g:
+        g.SetCamera(cam)
+        for band in (8, 16, 8, 24):
+            g.Render(band)
+            pos, nrm = g.download()
+            assert same_bits(pos, spos) and same_bits(nrm, snrm), band
