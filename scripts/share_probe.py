@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""A multi-GPU member's share of a frame on one GPU: rank 0's interleaved 8-row bands of an N-way split
+(band_count N, band_index 0), traced at `slots` frames in flight on the bench's moving camera path, for split
+rules (SF_SPLIT_BUCKETS: auto = into idle wave slots only; model = the makespan model of sf_order_scan).
+Prints ms per frame of the share and the N x speed-up over the whole frame. Usage: share_probe.py [W H K]"""
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "sphereflake-raytracer_amd"))
+sys.path.insert(0, REPO)
+import sphereflake_amd as sf  # noqa: E402
+from bench import frame_camera  # noqa: E402
+
+W, H, K = (int(sys.argv[1]), int(sys.argv[2]), float(sys.argv[3])) if len(sys.argv) > 3 else (1920, 1080, 0.25)
+STEPS, WARM = 120, 30
+views = [frame_camera(W, H, K, i).corners() for i in range(WARM + STEPS)]
+
+
+def run(n, slots, split):
+    os.environ["SF_SPLIT_BUCKETS"] = split
+    cs = [sf.Sphereflake(W, H) for _ in range(slots)]
+    try:
+        def frame(i):
+            c = cs[i % slots]
+            c.SetView(*views[i])
+            c.Render(band_rows=8, band_count=n, band_index=0)
+        for i in range(WARM):
+            frame(i)
+        for c in cs:
+            c.Synchronize()
+        t = time.perf_counter()
+        for i in range(STEPS):
+            frame(WARM + i)
+        for c in cs:
+            c.Synchronize()
+        return (time.perf_counter() - t) / STEPS * 1e3
+    finally:
+        for c in cs:
+            c.close()
+
+
+for slots in (1, 3):
+    for split in ("auto", "model"):
+        base = None
+        row = []
+        for n in (1, 2, 4, 8):
+            ms = np.median([run(n, slots, split) for _ in range(2)])
+            base = ms if n == 1 else base
+            row.append(f"N={n} {ms:.4f} ms ({base / ms:.2f}x)")
+        print(f"{W}x{H} K={K} slots={slots} split={split}: " + "  ".join(row), flush=True)

@@ -26,7 +26,8 @@ extern "C" __global__ void sf_trace_queue2(FrameArgs a);
 extern "C" __global__ void sf_trace_queue4(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2p(FrameArgs a);
 extern "C" __global__ void sf_order_scan(const uint32_t* chunk_cnt, uint32_t nc, uint32_t n_tiles,
-                                         uint32_t split_buckets, uint32_t parts, uint32_t spare, uint32_t prio_buckets,
+                                         uint32_t split_buckets, uint32_t parts, uint32_t spare, uint32_t waves,
+                                         uint32_t prio_buckets,
                                          uint32_t* chunk_off, uint32_t* order_meta);
 extern "C" __global__ void sf_order_scatter(const uint32_t* cost, uint32_t n, uint32_t* chunk_cnt,
                                             const uint32_t* chunk_off, const uint32_t* order_meta, uint32_t* order,
@@ -409,7 +410,8 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if (const char* ev = std::getenv("SF_PROG_PREFETCH")) c->prog_prefetch = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_ADAPT")) c->prog_adapt = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_ORDER")) c->prog_order = std::atoi(ev) != 0;
-    if (const char* ev = std::getenv("SF_SPLIT_BUCKETS")) c->split_buckets = (uint32_t)std::atoi(ev);
+    if (const char* ev = std::getenv("SF_SPLIT_BUCKETS"))
+        c->split_buckets = std::strcmp(ev, "model") == 0 ? SF_SPLIT_MODEL : (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_SPLIT_PARTS")) c->split_parts = std::atoi(ev) == 4 ? 4u : 2u;
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_PRIO_BUCKETS")) c->prio_buckets = (uint32_t)std::atoi(ev);
@@ -699,7 +701,8 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 const uint32_t waves = nblk * wpb;   // resident waves of the persistent grid
                 const uint32_t spare = waves > ntiles ? waves - ntiles : 0u;
                 hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->chunk_cnt, nc, ntiles,
-                                   c->split_buckets, c->split_parts, spare, c->prio_buckets, c->chunk_off, c->order_meta);
+                                   c->split_buckets, c->split_parts, spare, waves, c->prio_buckets, c->chunk_off,
+                                   c->order_meta);
                 SF_HIP(c, hipGetLastError());
                 hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost, ntiles,
                                    c->chunk_cnt, (const uint32_t*)c->chunk_off, (const uint32_t*)c->order_meta,
@@ -903,7 +906,7 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
                 hipLaunchKernelGGL(sf_bin_hist, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->bin_cost, nbins,
                                    c->bin_chunk_cnt);
                 hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->bin_chunk_cnt, nc, nbins,
-                                   0u, 2u, 0u, 0u, c->bin_chunk_off, c->bin_meta);
+                                   0u, 2u, 0u, 0u, 0u, c->bin_chunk_off, c->bin_meta);
                 hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->bin_cost, nbins,
                                    c->bin_chunk_cnt, (const uint32_t*)c->bin_chunk_off, (const uint32_t*)c->bin_meta,
                                    c->bin_order, c->bin_rank);

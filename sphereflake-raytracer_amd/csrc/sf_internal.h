@@ -180,6 +180,9 @@ struct PostArgs {
 // (1920x1080: 32400 tiles, 7168 waves) nothing is split -- measured: splitting there costs +1.5-3.5 %;
 // at 640x360 (3600 tiles) it takes the frame from 0.198 to 0.144 ms.
 #define SF_SPLIT_AUTO 0xffffffffu
+// env SF_SPLIT_BUCKETS=model: split the buckets a makespan model of the last render's costs says shorten the
+// frame (sf_order_scan) -- also on full grids, where the heaviest tile exceeds the slots' fair share
+#define SF_SPLIT_MODEL 0xfffffffeu
 // Parts a split tile is traced as (env SF_SPLIT_PARTS): 2 halves or 4 quarters. A split tile's cost for
 // the next schedule is its slowest part's, scaled to whole-tile terms (measured: the slowest half takes
 // ~0.68 of the whole tile, the slowest quarter ~0.5).

@@ -1266,7 +1266,7 @@ extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(
 
 extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t* __restrict__ chunk_cnt, uint32_t nc,
                                                                    uint32_t n_tiles, uint32_t split_buckets, uint32_t parts,
-                                                                   uint32_t spare, uint32_t prio_buckets,
+                                                                   uint32_t spare, uint32_t waves, uint32_t prio_buckets,
                                                                    uint32_t* __restrict__ chunk_off,
                                                                    uint32_t* __restrict__ order_meta)
 {
@@ -1323,6 +1323,34 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t*
             // S is non-increasing in the bucket: the buckets that fit form a suffix
             const uint64_t ok = __builtin_amdgcn_ballot_w64(l >= 1u && l < SF_ORDER_BUCKETS && S * (parts - 1u) <= spare);
             if (ok >> (SF_ORDER_BUCKETS - 1u) & 1ull) bs = __builtin_ctzll(ok);
+        } else if (split_buckets == SF_SPLIT_MODEL && waves > 0u) {
+            // Makespan model (LPT list scheduling on `waves` slots, the last render's costs): unsplit, the
+            // frame takes at least max(C / waves, c_top); splitting buckets >= l into `parts` units adds their
+            // work x (parts x rho - 1) and leaves max(the heaviest unsplit bucket, rho x c_top) as the longest
+            // unit (rho: the slowest part's share of its tile, measured 0.6 for quarters, 0.68 for halves).
+            // Take the l of the least estimate when it is >= 10 % below the unsplit one.
+            const float rho = parts == 4u ? 0.6f : 0.68f;
+            const uint32_t e = (l + 16u) >> 1;   // bucket l covers [2^e (1 + m/2), ...) cycles, m = (l + 16) & 1
+            const float c = l < SF_ORDER_BUCKETS ? __builtin_ldexpf((l + 16u) & 1u ? 1.75f : 1.25f, (int)e) : 0.0f;
+            const float w = (float)t * c;   // this bucket's work
+            float A = w;                    // A(l) = work of the buckets >= l
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                const float up = __shfl_down(A, o, 64);
+                A += l + (uint32_t)o < SF_ORDER_BUCKETS ? up : 0.0f;
+            }
+            const float C = __shfl(A, 0, 64);                 // all the work
+            const float ctop = __shfl(c, btop, 64);
+            const uint64_t below = nz & ((1ull << l) - 1ull);   // occupied buckets under l
+            const float cun = below ? __shfl(c, 63 - __builtin_clzll(below), 64) : 0.0f;
+            const float Tn = fmaxf(C / (float)waves, ctop);
+            float T = fmaxf(fmaxf((C + A * ((float)parts * rho - 1.0f)) / (float)waves, cun), rho * ctop);
+            if (!(l >= 1u && (int)l <= btop)) T = __builtin_inff();
+            float Tm = T;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) Tm = fminf(Tm, __shfl_xor(Tm, o, 64));
+            const uint64_t best = __builtin_amdgcn_ballot_w64(T == Tm);
+            if (Tm < 0.9f * Tn && best) bs = 63 - __builtin_clzll(best);   // (ties: the fewest splits)
         } else if (split_buckets != 0u) {
             int b0 = btop - (int)split_buckets + 1;
             if (b0 < 1) b0 = 1;
