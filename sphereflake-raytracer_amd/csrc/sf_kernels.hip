@@ -16,18 +16,24 @@
 // SIMD_AVX.h:247-258) bit for bit.
 //
 // Kernels
-//   sf_trace_wave   -- default full-frame kernel. One wave64 traces one 8x8 pixel tile. The DFS
-//                      over the sphereflake is wave-uniform: a node is visited iff at least one
-//                      lane of the tile visits it; each lane carries its own "active" bit per
-//                      level, so every lane sees exactly its per-ray visit sequence. When a node
-//                      expands, the 64 lanes build its 9 child transforms cooperatively (108
-//                      matrix entries, 2 per lane) into the wave's LDS level, instead of every
-//                      ray doing 9 4x4 products per node as the reference packets do.
-//   sf_fixup_wave   -- re-traces the tiles sf_trace_wave flagged as needing more LDS levels than
-//                      provisioned, with SF_MAX_LEVELS levels.
+//   sf_trace_queue2 -- the product kernel (full frames): a persistent grid of 2-wave workgroups; each wave64
+//                      traces one 8x8 pixel tile (or a part of one) per work unit, taken from the previous
+//                      render's heavy-first unit order (static first unit, then its block group's atomic
+//                      queue). The DFS over the sphereflake is wave-uniform: a node is visited iff at least
+//                      one lane of the tile visits it, and each lane keeps exactly its own per-ray visit
+//                      semantics through lane masks. When a node expands, 36 lanes build its 9 child
+//                      transforms cooperatively (one 4-float column each) into the wave's LDS level,
+//                      instead of every ray doing 9 4x4 products per node as the reference packets do.
+//                      sf_trace_queue1/4: 1 / 4 waves per workgroup; sf_trace_queue2p: the latency variant
+//                      (pipelined child loop) for frames that fill the grid less than twice.
+//   sf_order_scan / sf_order_scatter -- the next render's unit order from this render's tile costs.
+//   sf_trace_wave{1,2,4} -- the same traversal, one workgroup per tile group (non-persistent A/B path).
+//   sf_fixup_wave   -- re-traces the tiles flagged as needing more LDS levels than provisioned, with
+//                      SF_MAX_LEVELS levels.
 //   sf_trace_ray    -- one thread per ray with a private traversal stack (the straightforward
 //                      formulation; cross-check and comparison point).
-//   sf_mt_draws / sf_progressive_trace / sf_progressive_scatter -- frame-less progressive mode.
+//   sf_band_unpack  -- packed band slabs of a multi-GPU frame -> the G-buffer at frame positions.
+//   sf_mt_draws / sf_packet_* / sf_progressive_* -- frame-less progressive mode.
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
@@ -182,12 +188,14 @@ __device__ __forceinline__ bool group_any(bool p)
 //   1. builds its 9 child world transforms cooperatively into the LDS table of its level
 //      (36 lanes: one column each; child translation scaled by (4/3) r, world = parent * child,
 //      SIMD_AVX.h:59-81, Sphereflake.h:162-172) plus Dot(centre, centre) of each child;
-//   2. evaluates the bounding + LOD tests of all 9 children at once (independent, so they overlap
-//      instead of forming a serial chain), giving each lane a 9-bit "child expands" vector E and
-//      the wave a 9-bit "pending" mask of children some lane expands.
-// Children are then entered in index order; a node's own sphere is tested after all its children
-// (post-order, Sphereflake.h:174-224), exactly the reference's per-ray visiting order. Children that
-// no lane expands cost only their (batched) bounding test, as in the reference.
+//   2. culls the children no ray of the tile's cone can reach (9 centre lanes in parallel), then tests
+//      the remaining ones one after the other in index order (a uniform loop over a 9-bit mask), giving
+//      each lane a 9-bit "child expands" vector E and the wave a 9-bit "pending" mask of children some
+//      lane expands.
+// Children are then entered in index order. A node's own sphere is tested when the node is entered
+// (pre-order) with an ancestor tie-break that reproduces the reference's post-order "first strictly smaller
+// t wins" (Sphereflake.h:174-224) -- see self_test. Children that no lane expands cost only their bounding
+// test, as in the reference.
 //
 // Per node (group = the lane itself for per-ray semantics, the 8 lanes of a reference AVX packet
 // for packet semantics):
