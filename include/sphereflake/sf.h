@@ -257,6 +257,11 @@ int sf_root_transform(const float origin[3], float root[16]);
    threshold T_d with  sqrtf(t / r_d) < 70 || t < 0   <=>   t < T_d  (Sphereflake.h:146). */
 int sf_depth_constants(uint32_t depth, float* radius, float* lod_threshold);
 
+/* std::mt19937 jump-ahead (host; the frame-less draws' parallel generation): the state (624 words + next
+   index, libstdc++ layout: sf_progressive's generator state) after `outputs` more draws, computed with the
+   generator's characteristic polynomial (t^m mod phi), not by stepping. */
+int sf_mt19937_jump(const uint32_t state_in[625], uint64_t outputs, uint32_t state_out[625]);
+
 /* Reproduction of x86 rsqrtps (the table the kernels use). */
 float sf_rsqrtps(float x);
 

@@ -1349,6 +1349,13 @@ int sf_depth_constants(uint32_t depth, float* radius, float* lod)
     return SF_OK;
 }
 
+int sf_mt19937_jump(const uint32_t state_in[625], uint64_t outputs, uint32_t state_out[625])
+{
+    if (!state_in || !state_out) return SF_EINVAL;
+    sfhost::mt_jump(state_in, outputs, state_out);
+    return SF_OK;
+}
+
 float sf_rsqrtps(float x)
 {
     uint32_t b;

@@ -198,6 +198,11 @@ void depth_tables(DepthTables* t, float lod_constant = 70.0f);
 float leaf_threshold(const DepthTables* t, uint32_t depth);
 void sobol_matrices(uint32_t out[2][52]);
 void mt19937_seed(uint32_t seed, uint32_t state[625]);
+// mt19937 jump-ahead (sf_mtjump.cpp): t^(j L) mod phi for j < K (K x mt_poly_words() u64, cached), and the
+// host reference jump of a std::mt19937 state by `outputs` draws
+int mt_poly_words();
+const uint64_t* mt_jump_polys(uint64_t L, uint32_t K);
+void mt_jump(const uint32_t in[625], uint64_t outputs, uint32_t out[625]);
 void ssao_noise(float out[SF_NOISE_SIZE * SF_NOISE_SIZE * 4]);
 bool post_centre_exact(uint32_t n);
 }  // namespace sfhost

@@ -118,6 +118,7 @@ SIGNATURES = {
     "sf_root_transform": (ctypes.c_int, [_F, _F]),
     "sf_depth_constants": (ctypes.c_int, [ctypes.c_uint32, _F, _F]),
     "sf_rsqrtps": (ctypes.c_float, [ctypes.c_float]),
+    "sf_mt19937_jump": (ctypes.c_int, [_U, ctypes.c_uint64, _U]),
     "sf_set_tile_trace": (ctypes.c_int, [_CTX, ctypes.c_int]),
     "sf_get_tile_trace": (ctypes.c_int, [_CTX, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t]),
     "sf_get_tile_order": (ctypes.c_int, [_CTX, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
