@@ -1,7 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r3c
-timeout -k 10 600 python -u -m pytest tests/test_gpu_dist.py tests/test_gpu_initialize.py tests/test_gpu_group.py -v --timeout 120 --timeout-method thread > gpurun_out/r3c/pytest_new.log 2>&1; rc=$?
-tail -3 gpurun_out/r3c/pytest_new.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/r3c/pytest_gpu.log 2>&1; rc=$?
+tail -3 gpurun_out/r3c/pytest_gpu.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 300 python -u bench.py --steps 60 --warmup 10 --no-cpu-baseline > gpurun_out/r3c/bench_quick.json 2> gpurun_out/r3c/bench_quick.err || { tail -30 gpurun_out/r3c/bench_quick.err; exit 4; }
 tail -1 gpurun_out/r3c/bench_quick.json

@@ -42,6 +42,11 @@ extern "C" __global__ void sf_post_blur(PostArgs a, uint32_t dir);
 extern "C" __global__ void sf_post_final(PostArgs a);
 extern "C" __global__ void sf_post_fused(PostArgs a);
 extern "C" __global__ void sf_mt_draws(uint32_t* state, uint32_t* out, uint32_t n);
+extern "C" __global__ void sf_mt_raw(const uint32_t* state, uint32_t* raw, uint32_t blocks);
+extern "C" __global__ void sf_mt_jump_partial(const uint32_t* raw, const uint64_t* polys, uint32_t poly_words,
+                                              uint32_t* partial);
+extern "C" __global__ void sf_mt_segments(const uint32_t* state, const uint32_t* partial, uint32_t L, uint32_t n,
+                                          uint32_t* out, uint32_t* state_out);
 extern "C" __global__ void sf_progressive_trace(FrameArgs a, const uint32_t* draws, uint64_t counter0, uint32_t packets,
                                                 uint64_t ticket0, PacketLane* lanes, unsigned long long* owner,
                                                 const uint32_t* perm, uint32_t levels, uint32_t* ovf_list,
@@ -75,6 +80,10 @@ static const uint32_t kLut[2048] = {
 namespace {
 
 constexpr uint32_t kDefaultLevels = 12;   // depths 0..11 expand; every BASELINE camera stays <= 10
+// parallel mt19937 draws (sf_mtjump.cpp, sf_kernels.hip): from this many draws per call, in K <= kMtSegMax
+// segments of >= kMtSegMin draws, each jumped to by a convolution split over SF_MT_PARTS (8) workgroups
+constexpr uint32_t kMtParMin = 32768, kMtSegMin = 8192, kMtSegMax = 32;
+constexpr uint32_t kMtParts = 8, kMtRawBlocks = 33;   // raw words x_0..x_20559 (19937 + 623 + 1)
 
 struct DevGuard {
     int prev = -1;
@@ -152,6 +161,13 @@ struct sf_ctx {
     hipEvent_t pf_done = nullptr;      // prefetch written (pf_stream)
     hipEvent_t mt_ready = nullptr;     // this batch's draws generated on the render stream
     hipEvent_t traced = nullptr;       // the last batch's trace done reading its draws
+    // parallel draws (env SF_MT_PARALLEL=0: the single-workgroup generator only)
+    bool mt_parallel = true;
+    uint32_t* mt_raw = nullptr;        // kMtRawBlocks x 624 raw words from the state's buffer
+    uint32_t* mt_partial = nullptr;    // (kMtSegMax - 1) x kMtParts partial windows
+    uint32_t* mt_state2 = nullptr;     // the state after the batch (copied back into mt_state)
+    uint64_t* mt_polys = nullptr;      // kMtSegMax jump polynomials t^(j L) mod phi
+    uint64_t mt_poly_key = 0;          // (L << 8 | K) of the uploaded polynomials
     bool traced_valid = false;
     uint32_t pf_packets = 0;           // draws pending for a batch of this many packets (0: none)
     bool prog_prefetch = true;         // env SF_PROG_PREFETCH=0: off
@@ -274,6 +290,10 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->prog_ovf_cnt);
     (void)hipFree(c->draws_pf);
     (void)hipFree(c->mt_saved);
+    (void)hipFree(c->mt_raw);
+    (void)hipFree(c->mt_partial);
+    (void)hipFree(c->mt_state2);
+    (void)hipFree(c->mt_polys);
     if (c->pf_done) (void)hipEventDestroy(c->pf_done);
     if (c->mt_ready) (void)hipEventDestroy(c->mt_ready);
     if (c->traced) (void)hipEventDestroy(c->traced);
@@ -410,6 +430,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if (const char* ev = std::getenv("SF_PROG_PREFETCH")) c->prog_prefetch = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_ADAPT")) c->prog_adapt = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_ORDER")) c->prog_order = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_MT_PARALLEL")) c->mt_parallel = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_SPLIT_BUCKETS"))
         c->split_buckets = std::strcmp(ev, "model") == 0 ? SF_SPLIT_MODEL : (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_SPLIT_PARTS")) c->split_parts = std::atoi(ev) == 4 ? 4u : 2u;
@@ -774,9 +795,43 @@ int sf_unpack_bands(sf_ctx* c, const float* stage4, uint32_t stage_rows, uint32_
     return SF_OK;
 }
 
+// n draws of the context's mt19937 stream into `out`, on stream s (advances c->mt_state): the single-workgroup
+// generator for small counts, else the parallel jump-ahead path (same stream bit for bit).
+static int gen_draws(sf_ctx* c, hipStream_t s, uint32_t* out, uint32_t n)
+{
+    if (!c->mt_parallel || n < kMtParMin) {
+        hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(256), 0, s, c->mt_state, out, n);
+        SF_HIP(c, hipGetLastError());
+        return SF_OK;
+    }
+    uint32_t K = n / kMtSegMin;
+    K = K < 2u ? 2u : K > kMtSegMax ? kMtSegMax : K;
+    const uint32_t L = (n + K - 1u) / K;
+    const uint32_t pw = (uint32_t)sfhost::mt_poly_words();
+    if (!c->mt_raw) {
+        SF_HIP(c, hipMalloc(&c->mt_raw, (size_t)kMtRawBlocks * 624 * 4));
+        SF_HIP(c, hipMalloc(&c->mt_partial, (size_t)(kMtSegMax - 1) * kMtParts * 624 * 4));
+        SF_HIP(c, hipMalloc(&c->mt_state2, 625 * 4));
+        SF_HIP(c, hipMalloc(&c->mt_polys, (size_t)kMtSegMax * pw * 8));
+    }
+    const uint64_t key = ((uint64_t)L << 8) | K;
+    if (c->mt_poly_key != key) {   // (host polynomials cached per (L, K); ~20 ms for a new batch size)
+        SF_HIP(c, hipMemcpyAsync(c->mt_polys, sfhost::mt_jump_polys(L, K), (size_t)K * pw * 8, hipMemcpyHostToDevice, s));
+        c->mt_poly_key = key;
+    }
+    hipLaunchKernelGGL(sf_mt_raw, dim3(1), dim3(256), 0, s, (const uint32_t*)c->mt_state, c->mt_raw, kMtRawBlocks);
+    hipLaunchKernelGGL(sf_mt_jump_partial, dim3(K - 1u, kMtParts), dim3(256), 0, s, (const uint32_t*)c->mt_raw,
+                       (const uint64_t*)c->mt_polys, pw, c->mt_partial);
+    hipLaunchKernelGGL(sf_mt_segments, dim3(K), dim3(256), 0, s, (const uint32_t*)c->mt_state,
+                       (const uint32_t*)c->mt_partial, L, n, out, c->mt_state2);
+    SF_HIP(c, hipGetLastError());
+    SF_HIP(c, hipMemcpyAsync(c->mt_state, c->mt_state2, 625 * 4, hipMemcpyDeviceToDevice, s));
+    return SF_OK;
+}
+
 // Frame-less progressive mode (Sphereflake.cpp:67-74, 86-214). The device MT stream is kept in the
 // context; a call that does not continue where the previous one stopped (other seed or counter)
-// reseeds and skips ahead by generating and discarding 2 * counter0 draws.
+// reseeds and jumps ahead by 2 * counter0 draws on the host (sfhost::mt_jump).
 int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets, void* stream)
 {
     if (!c) return SF_EINVAL;
@@ -826,17 +881,11 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
         c->prog_cap = packets;
     }
     if (!c->prog_seeded || seed != c->prog_seed || counter0 != c->prog_next) {
-        uint32_t st[625];
+        uint32_t st[625], sj[625];
         sfhost::mt19937_seed(seed, st);
-        SF_HIP(c, hipMemcpyAsync(c->mt_state, st, sizeof st, hipMemcpyHostToDevice, s));
+        sfhost::mt_jump(st, 2 * counter0, sj);   // the stream 2 * counter0 draws on (2 per packet)
+        SF_HIP(c, hipMemcpyAsync(c->mt_state, sj, sizeof sj, hipMemcpyHostToDevice, s));
         SF_HIP(c, hipStreamSynchronize(s));
-        uint64_t skip = 2 * counter0;
-        while (skip > 0) {
-            uint32_t n = (uint32_t)(skip < 2ull * c->prog_cap ? skip : 2ull * c->prog_cap);
-            hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(256), 0, s, c->mt_state, c->draws, n);
-            SF_HIP(c, hipGetLastError());
-            skip -= n;
-        }
         c->prog_seeded = true;
         c->prog_seed = seed;
     }
@@ -847,10 +896,8 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     a.emit_aux = 1;
     a.packet_lanes = pl;
     if (c->flags & SF_FLAG_DIAG_UNITS) a.tile_trace = c->tile_trace;   // per-wave diagnostics (sf_set_tile_trace)
-    if (!prefetched) {
-        hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(256), 0, s, c->mt_state, c->draws, 2 * packets);
-        SF_HIP(c, hipGetLastError());
-    }
+    if (!prefetched)
+        if (int rc = gen_draws(c, s, c->draws, 2 * packets)) return rc;
     // Prefetch the next batch's draws (a continuing stream of the same batch size) on pf_stream, into
     // the buffer the previous batch traced from, overlapped with this batch's trace.
     if (c->prog_prefetch && packets >= SF_PROG_PREFETCH_MIN) {
@@ -866,8 +913,7 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
         SF_HIP(c, hipStreamWaitEvent(c->pf_stream, c->mt_ready, 0));
         if (c->traced_valid) SF_HIP(c, hipStreamWaitEvent(c->pf_stream, c->traced, 0));   // draws_pf free
         SF_HIP(c, hipMemcpyAsync(c->mt_saved, c->mt_state, 625 * 4, hipMemcpyDeviceToDevice, c->pf_stream));
-        hipLaunchKernelGGL(sf_mt_draws, dim3(1), dim3(256), 0, c->pf_stream, c->mt_state, c->draws_pf, 2 * packets);
-        SF_HIP(c, hipGetLastError());
+        if (int rc = gen_draws(c, c->pf_stream, c->draws_pf, 2 * packets)) return rc;
         SF_HIP(c, hipEventRecord(c->pf_done, c->pf_stream));
         c->pf_packets = packets;
     }

@@ -1675,6 +1675,152 @@ extern "C" __global__ __launch_bounds__(SF_MT_THREADS) void sf_mt_draws(uint32_t
     if (tid == 0) state[624] = pos;
 }
 
+// ---- parallel mt19937 draws (jump-ahead; host side sf_mtjump.cpp). A batch's n draws: the r = 624 - pos still
+// in the loaded buffer, then n - r "post-buffer" draws cut into K segments of L; segment j starts from the window
+// V_{jL} = (t^{jL} mod phi)(A) V_0 (V_0 = the buffer), i.e. word k of it is the XOR of x_{i+k} over the set
+// coefficients i of the polynomial -- a convolution of the raw sequence x (sf_mt_raw) split over P workgroups
+// per segment (sf_mt_jump_partial), then each segment's workgroup XORs its P partial windows and generates its
+// draws (sf_mt_segments). Same stream, bit for bit, as the sequential sf_mt_draws.
+namespace {
+__device__ __forceinline__ uint32_t mt_f(uint32_t a, uint32_t b, uint32_t c)
+{
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y)
+{
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+// One twist in LDS: nb = the block after ob (both 624 words); 227 threads run the chains (words j, j + 227,
+// j + 454), word 623 after a barrier. Returns after a barrier (nb complete).
+__device__ __forceinline__ void mt_twist(const uint32_t* ob, uint32_t* nb)
+{
+    const uint32_t j = threadIdx.x;
+    if (j < 227u) {
+        const uint32_t a = mt_f(ob[j], ob[j + 1u], ob[j + 397u]);
+        nb[j] = a;
+        const uint32_t b = mt_f(ob[j + 227u], ob[j + 228u], a);
+        nb[j + 227u] = b;
+        if (j < 169u) nb[j + 454u] = mt_f(ob[j + 454u], ob[j + 455u], b);
+    }
+    __syncthreads();
+    if (j == 0u) nb[623] = mt_f(ob[623], nb[0], nb[396]);
+    __syncthreads();
+}
+}  // namespace
+
+#define SF_MT_PAR_THREADS 256
+
+// The raw sequence x_0..x_{nraw-1} from the state's buffer (x_0..x_623 = the buffer). One workgroup.
+extern "C" __global__ __launch_bounds__(SF_MT_PAR_THREADS) void sf_mt_raw(const uint32_t* __restrict__ state,
+                                                                           uint32_t* __restrict__ raw, uint32_t blocks)
+{
+    __shared__ uint32_t buf[2][624];
+    for (uint32_t i = threadIdx.x; i < 624u; i += SF_MT_PAR_THREADS) {
+        buf[0][i] = state[i];
+        raw[i] = state[i];
+    }
+    __syncthreads();
+    for (uint32_t b = 1; b < blocks; ++b) {
+        mt_twist(buf[(b - 1u) & 1u], buf[b & 1u]);
+        for (uint32_t i = threadIdx.x; i < 624u; i += SF_MT_PAR_THREADS) raw[b * 624u + i] = buf[b & 1u][i];
+    }
+}
+
+// Partial jumped windows: workgroup (s, p) XORs x_{i+k} (k < 624) over the set coefficients i of segment
+// s + 1's polynomial within [p C, (p + 1) C), C = ceil(19937 / P); the raw words it needs are staged in LDS.
+#define SF_MT_PARTS 8u
+#define SF_MT_CHUNK ((19937u + SF_MT_PARTS - 1u) / SF_MT_PARTS)
+extern "C" __global__ __launch_bounds__(SF_MT_PAR_THREADS) void sf_mt_jump_partial(const uint32_t* __restrict__ raw,
+                                                                                    const uint64_t* __restrict__ polys,
+                                                                                    uint32_t poly_words,
+                                                                                    uint32_t* __restrict__ partial)
+{
+    __shared__ uint32_t xs[SF_MT_CHUNK + 624u];
+    const uint32_t seg = blockIdx.x + 1u, part = blockIdx.y;   // segment 0 needs no jump
+    const uint32_t i0 = part * SF_MT_CHUNK, i1 = min(19937u, i0 + SF_MT_CHUNK);
+    for (uint32_t i = threadIdx.x; i < (i1 - i0) + 624u; i += SF_MT_PAR_THREADS) xs[i] = raw[i0 + i];
+    __syncthreads();
+    const uint32_t k0 = threadIdx.x, k1 = k0 + 256u, k2 = k0 + 512u;   // this thread's window words (k2 < 624)
+    uint32_t a0 = 0u, a1 = 0u, a2 = 0u;
+    const uint64_t* pl = polys + (size_t)seg * poly_words;
+    for (uint32_t q = i0 >> 6; q <= (i1 - 1u) >> 6; ++q) {
+        uint64_t bits = pl[q];   // (uniform)
+        const uint32_t lo = q * 64u;
+        if (lo < i0) bits &= ~0ull << (i0 - lo);
+        if (lo + 64u > i1) bits &= (i1 - lo) >= 64u ? ~0ull : ((1ull << (i1 - lo)) - 1ull);
+        while (bits) {
+            const uint32_t i = lo + (uint32_t)__builtin_ctzll(bits) - i0;
+            bits &= bits - 1ull;
+            a0 ^= xs[i + k0];
+            a1 ^= xs[i + k1];
+            if (k2 < 624u) a2 ^= xs[i + k2];
+        }
+    }
+    uint32_t* out = partial + ((size_t)blockIdx.x * SF_MT_PARTS + part) * 624u;
+    out[k0] = a0;
+    out[k1] = a1;
+    if (k2 < 624u) out[k2] = a2;
+}
+
+// Segment j of the batch's n draws: workgroup j builds its window (segment 0: the buffer; others: the XOR of
+// their partial windows), then twists and tempers its L post-buffer draws; workgroup 0 also emits the r draws
+// left in the buffer. The workgroup holding the last draw stores the generator state after the batch
+// (libstdc++ layout) into state_out -- not into `state`, which the other workgroups may still be reading.
+extern "C" __global__ __launch_bounds__(SF_MT_PAR_THREADS) void sf_mt_segments(const uint32_t* __restrict__ state,
+                                                                                const uint32_t* __restrict__ partial,
+                                                                                uint32_t L, uint32_t n,
+                                                                                uint32_t* __restrict__ out,
+                                                                                uint32_t* __restrict__ state_out)
+{
+    __shared__ uint32_t buf[2][624];
+    const uint32_t j = blockIdx.x, tid = threadIdx.x;
+    const uint32_t pos = min(state[624], 624u);
+    const uint32_t r = min(624u - pos, n);            // draws still in the buffer
+    const uint32_t m = n - r;                         // post-buffer draws
+    const uint32_t s0 = j * L;
+    if (j == 0u)
+        for (uint32_t i = tid; i < r; i += SF_MT_PAR_THREADS) out[i] = mt_temper(state[pos + i]);
+    if (m == 0u) {   // the batch ends inside the buffer
+        if (j == 0u) {
+            for (uint32_t k = tid; k < 624u; k += SF_MT_PAR_THREADS) state_out[k] = state[k];
+            if (tid == 0u) state_out[624] = pos + n;
+        }
+        return;
+    }
+    if (s0 >= m) return;   // (workgroup-uniform)
+    const uint32_t cnt = min(L, m - s0);
+    for (uint32_t k = tid; k < 624u; k += SF_MT_PAR_THREADS) {
+        uint32_t w;
+        if (j == 0u) {
+            w = state[k];
+        } else {
+            const uint32_t* pp = partial + (size_t)(j - 1u) * SF_MT_PARTS * 624u + k;
+            w = 0u;
+#pragma unroll
+            for (uint32_t p = 0; p < SF_MT_PARTS; ++p) w ^= pp[(size_t)p * 624u];
+        }
+        buf[0][k] = w;
+    }
+    __syncthreads();
+    uint32_t cur = 0, done = 0;
+    while (done < cnt) {
+        mt_twist(buf[cur], buf[cur ^ 1u]);
+        cur ^= 1u;
+        const uint32_t take = min(624u, cnt - done);
+        for (uint32_t k = tid; k < take; k += SF_MT_PAR_THREADS) out[r + s0 + done + k] = mt_temper(buf[cur][k]);
+        done += take;
+    }
+    if (s0 + cnt == m) {   // the last draw of the batch: the state for the next batch
+        for (uint32_t k = tid; k < 624u; k += SF_MT_PAR_THREADS) state_out[k] = buf[cur][k];
+        if (tid == 0u) state_out[624] = ((cnt - 1u) % 624u) + 1u;
+    }
+}
+
 namespace {
 // Sobol::Sample (Sobol.cpp:41-55) for dims 0/1.
 __device__ __forceinline__ float sobol_sample(uint64_t index, const uint32_t* __restrict__ m, uint32_t scramble)

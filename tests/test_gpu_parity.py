@@ -647,3 +647,31 @@ def test_tiny_grid_many_queues_bit_exact(blocks, nq, monkeypatch):
             for k, got in (("pos4", pos), ("nrm4", nrm), ("minT", mint), ("index", idx)):
                 assert np.array_equal(np.ascontiguousarray(got).view(np.uint8),
                                       np.ascontiguousarray(exp[k]).view(np.uint8)), (k, blocks, nq)
+
+
+@pytest.mark.parametrize("sizes", [(40000,), (16400, 70001, 5), (1 << 18, 1 << 18), (300, 50000, 624 * 40 + 7)])
+def test_parallel_mt_draws_equal_sequential(sizes, monkeypatch):
+    """The frame-less draws from the jump-ahead generator (K segments, each started from the stream state
+    the polynomial t^(j L) mod phi jumps to; sf_mt_raw / sf_mt_jump_partial / sf_mt_segments) equal the
+    single-workgroup generator's (SF_MT_PARALLEL=0) over batch sequences of assorted sizes, including
+    mid-buffer starts: same frames, same stats. (Prefetch off, so every batch generates its own draws.)"""
+    W, H, K = 320, 180, 0.25
+    monkeypatch.setenv("SF_PROG_PREFETCH", "0")
+
+    def run():
+        with sf.Sphereflake(W, H) as s:
+            s.SetCamera(sf.config_camera(W, H, K))
+            c = 0
+            for n in sizes:
+                s.Progressive(2024, n, counter0=c)
+                c += n
+            s.Progressive(2024, 3000, counter0=c + 12345)   # a jump (host) into the stream
+            pos, nrm, _, _ = s.download()
+            return pos, nrm, s.stats()
+
+    pos, nrm, st = run()
+    monkeypatch.setenv("SF_MT_PARALLEL", "0")
+    epos, enrm, est = run()
+    assert np.array_equal(pos.view(np.uint32), epos.view(np.uint32))
+    assert np.array_equal(nrm.view(np.uint32), enrm.view(np.uint32))
+    assert (st.max_depth, st.closest, st.rays) == (est.max_depth, est.closest, est.rays)

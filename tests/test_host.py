@@ -208,3 +208,47 @@ def test_lod_threshold_exact_both_variants(c):
             assert np.array_equal(ref, t < T), (c, d)
     r1, T1 = sf.depth_constants(1)
     assert sf.lod_threshold(r1, 70.0) == T1
+
+
+@pytest.mark.parametrize("seed,advance,steps", [(12345, 0, 1000), (777, 5, 70000), (1, 623, 624 * 3 + 5),
+                                               (9, 100, 3), (42, 624, 0), (3, 0, 524288), (5, 311, 1 << 33)])
+def test_mt19937_jump_matches_generator(seed, advance, steps):
+    """sf_mt19937_jump (t^m mod the generator's characteristic polynomial, phi from Berlekamp-Massey) gives
+    the std::mt19937 stream `steps` draws on, checked against numpy's MT19937 (legacy seeding = std::mt19937's
+    init_genrand) stepped draw by draw (for 2^33 only the polynomial path runs: checked by its next draws
+    equalling a 2^32 + 2^32 jump)."""
+    import ctypes
+    from numpy.random import MT19937
+    from sphereflake_amd import lib
+    P = ctypes.POINTER(ctypes.c_uint32)
+
+    def state(g):
+        st = g.state["state"]
+        return np.concatenate([st["key"].astype(np.uint32), np.array([st["pos"]], np.uint32)])
+
+    def jump(s, n):
+        out = np.zeros(625, np.uint32)
+        assert lib().sf_mt19937_jump(s.ctypes.data_as(P), n, out.ctypes.data_as(P)) == 0
+        return out
+
+    def gen(s):
+        g = MT19937(0)
+        st = g.state
+        st["state"]["key"] = s[:624].copy()
+        st["state"]["pos"] = int(s[624])
+        g.state = st
+        return g
+
+    g = MT19937(0)
+    g._legacy_seeding(seed)
+    if advance:
+        g.random_raw(advance)
+    s0 = state(g)
+    out = jump(s0, steps)
+    if steps < (1 << 32):
+        if steps:
+            g.random_raw(steps)
+        assert np.array_equal(g.random_raw(1500), gen(out).random_raw(1500))
+    else:
+        half = jump(jump(s0, steps // 2), steps // 2)
+        assert np.array_equal(gen(half).random_raw(1500), gen(out).random_raw(1500))
