@@ -14,7 +14,10 @@
  *     is kept in the context (sf_last_hip_error()).
  *   - The caller owns host buffers; the context owns its device buffers.
  *   - One context per device per host thread. Calls are stream-ordered on the
- *     context stream (or params->stream); sf_download() synchronises.
+ *     context stream (or params->stream); sf_download() synchronises. Calls on
+ *     different streams of one context run in call order; a caller's stream is
+ *     not touched after the call that used it returns (it may be destroyed once
+ *     its work is done).
  *   - G-buffer layout is the reference's: float4 (x, y, z, 1) per pixel,
  *     row-major x + y*W, y = 0 is the TOP edge (Sphereflake.cpp:186-196). Misses
  *     are (0, 0, 0, 1), so the GL SSAO post-process consumes it unchanged

@@ -206,7 +206,7 @@ struct sf_ctx {
     // the stream of the previous such call (ctx_join), so renders, frame-less batches, post-processing
     // and downloads issued on different streams of one context run in call order, as on one stream.
     hipStream_t last_stream = nullptr; // stream of the latest enqueued work (nullptr: the context stream)
-    hipEvent_t join_ev = nullptr;      // recorded on last_stream when a call switches streams
+    hipEvent_t join_ev = nullptr;      // the point later calls order after (see ctx_join / StreamMark)
     bool use_order = true;             // env SF_ORDER=0: row-major order always
     uint32_t order_every = 0;          // env SF_ORDER_EVERY = k: rebuild the order after every k-th render only
                                        // (0 = auto: 3 for small frames, 1 otherwise)
@@ -238,17 +238,29 @@ struct sf_ctx {
     } while (0)
 
 // Order work about to be enqueued on `s` after everything the context enqueued before, on whatever
-// stream (one event record + wait, only when the stream changes; same-stream calls cost nothing).
+// stream (one event wait, only when the stream changes; same-stream calls cost nothing). A call that
+// enqueued on a caller's stream records join_ev on it when it returns (StreamMark), so the context never
+// touches that stream again afterwards: the caller may destroy it once the work is done.
 static int ctx_join(sf_ctx* c, hipStream_t s)
 {
     hipStream_t last = c->last_stream ? c->last_stream : c->stream;
     if (s == last) return SF_OK;
-    if (!c->join_ev) SF_HIP(c, hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming));
-    SF_HIP(c, hipEventRecord(c->join_ev, last));
+    if (last == c->stream) SF_HIP(c, hipEventRecord(c->join_ev, c->stream));   // (the context's own stream)
     SF_HIP(c, hipStreamWaitEvent(s, c->join_ev, 0));
-    c->last_stream = s;
+    c->last_stream = s == c->stream ? nullptr : s;
     return SF_OK;
 }
+
+// End of a call that enqueued on `s`: on a caller's stream, mark the point every later call orders after.
+struct StreamMark {
+    sf_ctx* c;
+    hipStream_t s;
+    StreamMark(sf_ctx* c_, hipStream_t s_) : c(c_), s(s_) {}
+    ~StreamMark()
+    {
+        if (s != c->stream) (void)hipEventRecord(c->join_ev, s);
+    }
+};
 
 // Host-synchronous drain: all work the context enqueued on any stream is done.
 static int ctx_drain(sf_ctx* c)
@@ -262,7 +274,7 @@ static void free_ctx(sf_ctx* c)
 {
     if (!c) return;
     DevGuard g(c->device);
-    if (c->last_stream) (void)hipStreamSynchronize(c->last_stream);
+    if (c->last_stream && c->join_ev) (void)hipEventSynchronize(c->join_ev);   // (never the caller's stream)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->join_ev) (void)hipEventDestroy(c->join_ev);
     (void)hipFree(c->pos);
@@ -459,6 +471,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     };
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+    if ((e = hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->pos, npx * 16)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->nrm, npx * 16)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->min_t, npx * 4)) != hipSuccess) return fail(e);
@@ -592,6 +605,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
     DevGuard g(c->device);
     if (tile_rows == 0) return SF_OK;
     if (int rc = ctx_join(c, s)) return rc;
+    StreamMark mark_(c, s);
 
     FrameArgs a = frame_args(c);
     a.tile_rows = tile_rows;
@@ -782,6 +796,7 @@ int sf_unpack_bands(sf_ctx* c, const float* stage4, uint32_t stage_rows, uint32_
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     DevGuard g(c->device);
     if (int rc = ctx_join(c, s)) return rc;
+    StreamMark mark_(c, s);
     FrameArgs a = frame_args(c);
     a.pos = c->pos;
     a.nrm = c->nrm;
@@ -844,6 +859,7 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     DevGuard g(c->device);
     if (int rc = ctx_join(c, s)) return rc;
+    StreamMark mark_(c, s);
     if (!c->mt_state) {
         SF_HIP(c, hipMalloc(&c->mt_state, 625 * 4));
         SF_HIP(c, hipMalloc(&c->owner, (size_t)c->W * c->H * 8));
@@ -1063,6 +1079,7 @@ int sf_download_async(sf_ctx* c, float* pos4, float* nrm4, float* min_t, uint32_
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     const size_t npx = (size_t)c->W * c->H;
     if (int rc = ctx_join(c, s)) return rc;
+    StreamMark mark_(c, s);
     if (pos4) SF_HIP(c, hipMemcpyAsync(pos4, c->pos, npx * 16, hipMemcpyDeviceToHost, s));
     if (nrm4) SF_HIP(c, hipMemcpyAsync(nrm4, c->nrm, npx * 16, hipMemcpyDeviceToHost, s));
     if (min_t) SF_HIP(c, hipMemcpyAsync(min_t, c->min_t, npx * 4, hipMemcpyDeviceToHost, s));
@@ -1114,6 +1131,7 @@ int sf_post_process(sf_ctx* c, const sf_post_params* prm, const float* pos4, con
     hipStream_t s = prm->stream ? (hipStream_t)prm->stream : c->stream;
     const size_t npx = (size_t)c->W * c->H;
     if (int rc = ctx_join(c, s)) return rc;
+    StreamMark mark_(c, s);
     if (!c->noise) {
         static float host_noise[SF_NOISE_SIZE * SF_NOISE_SIZE * 4];
         sfhost::ssao_noise(host_noise);

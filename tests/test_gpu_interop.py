@@ -158,3 +158,34 @@ def test_renders_on_alternating_streams_stay_ordered():
         assert frame_digest(pos, nrm) == fx["frame_digest"]
     for h in hs:
         hip.hipStreamDestroy(h)
+
+
+def test_caller_stream_destroyed_after_use():
+    """A caller renders on its own stream, waits for it and destroys it, then keeps using the context on
+    the context stream and finally destroys the context: the context must never touch the dead stream
+    (its join point is an event recorded when the call returned), and the frame stays golden."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    fx = load_frame("c2")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    s = sf.Sphereflake(W, H)
+    try:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for _ in range(2):
+            h = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+            s.Render(stream=h.value)
+            s.Progressive(7, 1000, 0, stream=h.value)
+            assert hip.hipStreamSynchronize(h) == 0
+            assert hip.hipStreamDestroy(h) == 0
+            s.Render()                       # the context stream, after the destroyed one
+            s.Synchronize()
+            pos, nrm, _, _ = s.download()
+            assert frame_digest(pos, nrm) == fx["frame_digest"]
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        s.Render(stream=h.value)             # the last call on a caller's stream ...
+        assert hip.hipStreamSynchronize(h) == 0
+        assert hip.hipStreamDestroy(h) == 0
+    finally:
+        s.close()                            # ... then sf_destroy
