@@ -18,9 +18,11 @@ Default mode `dist` (sf_dist_*, csrc/sf_dist.hip): `--slots` frames in flight (f
 slot its own context, stream and G-buffer), so a frame's persistent trace grid fills the wave slots the previous
 frame's heaviest tiles leave idle -- the reference's workers likewise trace continuously. Multi-GPU (`--gpus N`,
 launched by torch.distributed.run, one process per GPU): ONE frame per step split over the N GPUs in interleaved
-8-row bands; ranks k > 0 trace theirs as packed slabs (16 B/pixel) and RCCL carries them to rank 0 over xGMI,
-which unpacks them beside its own bands into the full G-buffer: `scaling: "strong"` (the frame is fixed, N
-GPUs share it). torch.distributed (gloo) is only the control plane: the RCCL ids, barriers and the max over
+8-row bands, every rank tracing its bands into its own HBM -- the frame's G-buffer distributed over the GPUs,
+`scaling: "strong"` (the frame is fixed, N GPUs share it): `value`. `gathered_on_rank0` times the same frames
+assembled on rank 0 (ranks k > 0 send packed slabs, 16 B/pixel, over RCCL/xGMI; rank 0 unpacks them beside its
+own bands): what a consumer on rank 0 sees, a transfer bound by the links into rank 0, reported beside `value`
+as the D2H copy is. torch.distributed (gloo) is only the control plane: the RCCL ids, barriers and the max over
 ranks of the timed region. `independent_frames` adds the weak-scaling figure (every rank its own frames).
 `--mode frames` is that weak-scaling loop alone; `--mode rows` one frame over N devices from ONE process
 (sf_group_*: strided peer copies).
@@ -439,26 +441,28 @@ def slot_period(steps, slots):
 
 
 def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows, nranks, frame_of,
-              fixed=False, latency=False, first=False):
+              fixed=False, latency=False, first=False, gather=False):
     """One timed loop of the sf_dist path: `steps` frames (frame_of(i) of the camera path at step i) after
-    `warmup`, `slots` in flight, over `nranks` ranks (1: this GPU alone, every rank its own frames). Barrier +
-    device sync on both sides of the timed region; the time is the max over ranks."""
+    `warmup`, `slots` in flight, over `nranks` ranks (1: this GPU alone, every rank its own frames); each frame
+    is every rank's bands into its own G-buffer (the distributed G-buffer), or with `gather` also assembled on
+    rank 0 (RCCL). Barrier + device sync on both sides of the timed region; the time is the max over ranks."""
     rank = ctl.rank if nranks > 1 else 0
-    ids = shard.dist_ids(slots) if nranks > 1 else None
+    ids = shard.dist_ids(slots) if nranks > 1 and gather else None
     d = sf.SphereflakeDist(dev.index, width, height, rank=rank, nranks=nranks, slots=slots, ids=ids,
                            band_rows=band_rows)
+    render = d.Render if gather else d.RenderBands
     views = [frame_camera(width, height, k, frame_of(i)).corners() for i in range(warmup + steps)]
     out = {}
     ctl.barrier()
     if first:   # the first render of a fresh context: row-major tile order, no cost history
         d.SetView(*views[0])
         t = time.perf_counter()
-        d.Render()
+        render()
         d.Synchronize()
         out["first_render_ms"] = (time.perf_counter() - t) * 1e3
     for i in range(warmup):
         d.SetView(*views[i])
-        d.Render()
+        render()
     kp = slot_period(steps, slots)
     for s in range(slots):
         d.kernel_timing(s, True, period=kp)
@@ -470,7 +474,7 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
     t0 = time.perf_counter()
     for i in range(steps):
         d.SetView(*views[warmup + i])
-        d.Render()
+        render()
     d.Synchronize()
     torch.cuda.synchronize(dev)
     ctl.barrier()
@@ -491,12 +495,12 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
     if fixed:   # the same loop on one unchanging view (the config camera)
         d.SetView(*frame_camera(width, height, k, 0).corners())
         for i in range(warmup):
-            d.Render()
+            render()
         d.Synchronize()
         ctl.barrier()
         t0 = time.perf_counter()
         for i in range(steps):
-            d.Render()
+            render()
         d.Synchronize()
         ctl.barrier()
         out["t_fixed"] = ctl.max((time.perf_counter() - t0) / steps)
@@ -504,11 +508,11 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
     if latency:   # one frame at a time, each waited for (rank 0's wait includes the gather of the others)
         lat = []
         for i in range(20):
-            d.SetView(*views[i])
-            out["last_view"] = views[i]
+            d.SetView(*views[i % len(views)])
+            out["last_view"] = views[i % len(views)]
             ctl.barrier()
             t = time.perf_counter()
-            d.Render()
+            render()
             d.Synchronize()
             lat.append(time.perf_counter() - t)
         out["latency_ms"] = ctl.max(float(np.median(lat))) * 1e3
@@ -555,10 +559,24 @@ def main():
         return
 
     slots = max(1, min(8, args.slots))
+    gathered = None
     if args.mode == "dist":
+        # the frame split over the ranks, each rank's bands into its own HBM (the distributed G-buffer)
         r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
                       lambda i: i, fixed=True, latency=True, first=True)
         rays_step = width * height
+        if n > 1:   # the same frames also assembled on rank 0: RCCL gather of the packed slabs + unpack
+            rg = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
+                           lambda i: i, latency=True, gather=True)
+            rg["dist"].close()
+            gathered = {"value": round(rays_step / rg["t_step"] / 1e6, 2), "frame_ms": round(rg["t_step"] * 1e3, 4),
+                        "frame_latency_ms": round(rg["latency_ms"], 4),
+                        "bytes_per_frame": sum(sf.lib().sf_slab_rows(height, args.band_rows, n, kk)
+                                               for kk in range(1, n)) * width * 16,
+                        "format": "packed float4 (nx, ny, nz, minT) per pixel; rank 0 rebuilds pos = dir * minT",
+                        "transport": "RCCL grouped ncclSend/ncclRecv to rank 0 over xGMI, one communicator per slot",
+                        "note": "every frame complete in rank 0's G-buffer (reference layout): the rate a consumer "
+                                "on rank 0 sees; bound by the peers' links into rank 0"}
     else:   # frames: every rank its own frames (frame i * N + rank), one GPU each, slots in flight
         r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, 1,
                       lambda i: i * n + rank, fixed=True, latency=True, first=True)
@@ -629,8 +647,9 @@ def main():
         traffic = pmc_traffic(pmc) if n == 1 else None
         cfg_name = BASELINE_CONFIGS.get((width, height, round(args.K, 4)))
         if args.mode == "dist":
-            par = (f"dist x{n}: interleaved {band}-row bands, ranks > 0 send packed slabs (16 B/px) to rank 0 over "
-                   f"RCCL; {slots} frames in flight" if n > 1 else f"1 GPU, {slots} frames in flight (sf_dist slots)")
+            par = (f"dist x{n}: one frame split in interleaved {band}-row bands, each rank's bands into its own HBM "
+                   f"(distributed G-buffer; the RCCL-gathered rate is `gathered_on_rank0`); {slots} frames in flight"
+                   if n > 1 else f"1 GPU, {slots} frames in flight (sf_dist slots)")
         else:
             par = f"frames x{n} (independent frames per rank, {slots} in flight each)"
         out = {
@@ -674,9 +693,7 @@ def main():
             "build": build,
         }
         if n > 1 and args.mode == "dist":
-            out["gather"] = {"bytes_per_frame": sum(sf.lib().sf_slab_rows(height, band, n, k) for k in range(1, n)) * width * 16,
-                             "format": "packed float4 (nx, ny, nz, minT) per pixel; rank 0 rebuilds pos = dir * minT",
-                             "transport": "RCCL grouped ncclSend/ncclRecv to rank 0 (xGMI), one communicator per slot"}
+            out["gathered_on_rank0"] = gathered
             out["independent_frames"] = indep
         if c4 is not None:
             out["configs"] = {"c4": c4}

@@ -353,6 +353,9 @@ int sf_dist_last_slot(const sf_dist* dist);           /* slot of the last frame 
 int sf_dist_set_view(sf_dist* dist, const float origin[3], const float top_left[3], const float top_right[3],
                      const float bottom_left[3]);     /* the view of the next frames */
 int sf_dist_render(sf_dist* dist);                    /* one frame, asynchronous (this rank's share + gather) */
+/* One frame as a distributed G-buffer: this rank's bands into its slot's G-buffer at frame positions (reference
+   layout), no gather -- every rank holds its own rows in its own HBM. Asynchronous; no collective. */
+int sf_dist_render_bands(sf_dist* dist);
 int sf_dist_synchronize(sf_dist* dist);               /* every slot of this rank done */
 int sf_dist_download(sf_dist* dist, float* pos4, float* nrm4);   /* rank 0: D2H of the last frame (synchronises) */
 int sf_dist_get_stats(sf_dist* dist, sf_stats* out);  /* collective: over slots and ranks (synchronises) */

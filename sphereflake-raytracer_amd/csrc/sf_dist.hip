@@ -223,6 +223,22 @@ extern "C" int sf_dist_render(sf_dist* d)
     return SF_OK;
 }
 
+// This rank's bands of the next frame into its slot's G-buffer at frame positions (reference layout): the frame
+// as a distributed G-buffer, every rank holding its own rows in its own HBM -- no gather.
+extern "C" int sf_dist_render_bands(sf_dist* d)
+{
+    if (!d) return SF_EINVAL;
+    auto& s = d->slot[d->frames % d->slot.size()];
+    sf_render_params p;
+    std::memset(&p, 0, sizeof p);
+    p.band_rows = d->band_rows;
+    p.band_count = (uint32_t)d->nranks;
+    p.band_index = (uint32_t)d->rank;
+    if (int rc = sf_render(s.ctx, &p)) return rc;
+    ++d->frames;
+    return SF_OK;
+}
+
 extern "C" int sf_dist_synchronize(sf_dist* d)
 {
     if (!d) return SF_EINVAL;

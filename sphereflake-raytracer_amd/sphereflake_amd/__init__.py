@@ -154,6 +154,7 @@ SIGNATURES = {
     "sf_dist_last_slot": (ctypes.c_int, [ctypes.c_void_p]),
     "sf_dist_set_view": (ctypes.c_int, [ctypes.c_void_p, _F, _F, _F, _F]),
     "sf_dist_render": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_dist_render_bands": (ctypes.c_int, [ctypes.c_void_p]),
     "sf_dist_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "sf_dist_download": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "sf_dist_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(sf_stats)]),
@@ -852,7 +853,22 @@ class SphereflakeDist:
         self.SetView(*cam.corners())
 
     def Render(self):
+        """One frame: this rank's bands, gathered with the other ranks' into rank 0's G-buffer (RCCL)."""
         self._check(lib().sf_dist_render(self._d), "sf_dist_render")
+
+    def RenderBands(self):
+        """One frame as a distributed G-buffer: this rank's bands into its own slot G-buffer, no gather."""
+        self._check(lib().sf_dist_render_bands(self._d), "sf_dist_render_bands")
+
+    def download_slot(self, slot: int):
+        """The G-buffer of one slot's context on this rank (synchronises)."""
+        H, W = self.height, self.width
+        pos = np.empty((H, W, 4), np.float32)
+        nrm = np.empty((H, W, 4), np.float32)
+        ctx = self.context(slot)
+        _check(lib().sf_download(ctx, pos.ctypes.data_as(ctypes.c_void_p), nrm.ctypes.data_as(ctypes.c_void_p),
+                                 None, None), "sf_download", ctx)
+        return pos, nrm
 
     def Synchronize(self):
         self._check(lib().sf_dist_synchronize(self._d), "sf_dist_synchronize")

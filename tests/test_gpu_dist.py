@@ -103,3 +103,18 @@ def test_dist_one_rank_rccl_communicator():
     assert frame_digest(pos, nrm) == fx["frame_digest"]
     assert st.rays == 3 * W * H and st.max_depth == fx["stats"]["max_depth"]
     assert np.float32(st.closest) == np.float32(float.fromhex(fx["stats"]["closest"]))
+
+
+def test_dist_render_bands_one_rank_is_the_frame():
+    """RenderBands (sf_dist_render_bands) on one rank: this rank owns every band, so each slot's G-buffer
+    holds the full frame -- golden."""
+    fx = load_frame("c2")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.SphereflakeDist(0, W, H, slots=2) as d:
+        d.SetCamera(sf.config_camera(W, H, K))
+        d.RenderBands()
+        d.RenderBands()
+        d.Synchronize()
+        for slot in (0, 1):
+            pos, nrm = d.download_slot(slot)
+            assert frame_digest(pos, nrm) == fx["frame_digest"], slot
