@@ -1,13 +1,14 @@
 #!/bin/bash
 # A/B of library builds (SF_LIB) on the GPU box: interleaved bench lines (timing) and, with PMC=1, one
 # rocprofv3 --pmc pass per build of the LDS / issue counters of the trace kernel.
-# Usage (on the box, repo root): scripts/lib_ab.sh <tag> "<bench args>" <lib.so> ...
+# Usage (on the box, repo root): [REPS=3] [PMC=1] scripts/lib_ab.sh <tag> "<bench args>" <lib.so> ...
+#   REPS=0: no timing runs
 set -e
 TAG=${1:-libab}; shift; ARGS=$1; shift
 R=$PWD
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
-for rep in 1 2 3; do
+for rep in $(seq 1 ${REPS:-3}); do
   for L in "$@"; do
     SF_LIB=$R/$L timeout -k 10 120 python3 -u bench.py --no-cpu-baseline --no-extras --steps 200 --warmup 30 $ARGS > $OUT/b.json
     python3 -c "import json; j=json.loads(open('$OUT/b.json').read().strip().split(chr(10))[-1]); print('$L', 'frame', j['frame_ms'], 'trace', j['roofline']['kernel_ms'], 'clk', j['roofline'].get('clock_mhz_live'), 'Mrays', j['value'], 'fixed', j['fixed_camera']['frame_ms'] if j.get('fixed_camera') else None)"
