@@ -7,7 +7,7 @@ R=$PWD
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-BENCH="python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline $*"
+BENCH="python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras $*"
 run() {  # run <name> <counters...>
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc "$@" -d $OUT/$name -o run --output-format csv -- $BENCH > $OUT/$name.log 2>&1

@@ -1278,6 +1278,9 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t*
                                                                    uint32_t* __restrict__ chunk_off,
                                                                    uint32_t* __restrict__ order_meta)
 {
+    // (with frames in flight this one workgroup shares the CUs with other frames' trace waves, whose heavy
+    // tiles run at raised priority: without its own it waited ~125 us instead of ~8 for issue slots)
+    __builtin_amdgcn_s_setprio(3);
     // thread = (bucket b = tid % 32, slice k = tid / 32): chunks [k * per, (k + 1) * per) of bucket b
     __shared__ uint32_t part[32][SF_ORDER_BUCKETS + 1];
     __shared__ uint32_t tot[SF_ORDER_BUCKETS];
@@ -1414,6 +1417,7 @@ extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t
                                                                     uint32_t* __restrict__ rank_out)
 {
     // (rank_out, when not NULL: rank_out[i] = item i's position, the inverse permutation; unsplit orders only)
+    __builtin_amdgcn_s_setprio(3);   // (see sf_order_scan)
     const uint32_t c = blockIdx.x, lane = threadIdx.x, i = c * 64u + lane;
     const uint32_t split_from = order_meta[1], parts = order_meta[2], pb = order_meta[3];
     const uint32_t first = parts == 4u ? SF_PART_QUARTER0 : SF_PART_HALF0;
