@@ -411,13 +411,17 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     if (lane < 5u) L.cone()[lane] = lane == 0u ? ax : lane == 1u ? ay : lane == 2u ? az : lane == 3u ? cosT : sinT;
     }
 
-    // This lane's column of the cooperative child build: column c = lane / 9, child i = lane % 9, so
-    // lanes 27..35 hold the 9 child centres (read back by v_readlane, no LDS round trip) and one ballot
-    // yields a per-child mask (bits 27..35).
-    // Lanes 36..63 mirror lanes 0..27 (same column, same value, same address), so the build has no
-    // divergent region; its VALU cost is per wave either way.
-    const uint32_t bl = lane < 36u ? lane : lane - 36u;
-    const uint32_t bi = bl % 9u, bc = bl / 9u;
+    // This lane's column of the cooperative child build. The 27 axis columns (column c = lane / 9 of child
+    // i = lane % 9) are built by lanes 0..26 of the first 32-lane LDS group, the 9 centres (column 3) by
+    // lanes 32..40 of the second, so a table store never mixes the float3 column plane and the float4 centre
+    // plane in one bank group: every other lane repeats a builder of its own group (27..31: lane 26;
+    // 41..63: the centres again) -- the same address and value, which the LDS merges, not a bank conflict
+    // (round 2's layout, centres at lanes 27..35 with lanes 36..63 mirroring 0..27, put 40 % of the LDS
+    // cycles into conflicts). No divergent region; the build's VALU cost is per wave either way. Lanes
+    // 32..40 hold the 9 child centres (read back by v_readlane) and one ballot yields a per-child mask
+    // (bits 32..40).
+    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 8u : (lane - 32u) % 9u;
+    const uint32_t bc = lane < 27u ? lane / 9u : lane < 32u ? 2u : 3u;
     // The leaf-threshold skip bounds t from below for every ray. In packet semantics a lane with tca < 0
     // can also pass LOD through another lane's bounding hit (negative t, SIMD_AVX.h:254), which that
     // bound does not cover: there the skip additionally needs every sphere of the child's subtree in
@@ -437,8 +441,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
 #pragma unroll
     for (int j = 0; j < 4; ++j) b[j] = K->child[bi][4u * bc + j];
     // where this lane's column goes in a level table: centre lanes (bc = 3) xyz + cc at plane 0, the others
-    // xyz in their column plane; the centre lanes' cc store goes to plane 0, the others' to a junk word of
-    // the cone block (so both stores are unconditional: no divergent region)
+    // xyz in their column plane; the centre lanes' cc store goes to plane 0, the others' to one junk word of
+    // the cone block (so both stores are unconditional: no divergent region; one address, no conflict)
     const uint32_t slot = bc == 3u ? bi * 4u : SF_LDS_PLANE + bc * SF_LDS_COLS + bi * 3u;
 
     uint32_t d = 0;                 // uniform: depth of the open (expanded) node
@@ -511,38 +515,12 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         // first. Not allocated, not stored (uniform branch).
         if (d + 1u < levels) {
             float* const tb = L.table(d);
-#ifdef SF_EXP_MASKED_BUILD   // experiment: only the 36 builder lanes store (no mirrored or junk stores)
-            {
-                // EXEC = lanes 0..35 for the column store, lanes 27..35 (the centres) for the |c|^2 store, set
-                // inside the asm (no divergent region in the compiler's CFG); LDS ops of a wave complete in order
-                typedef float f3v __attribute__((ext_vector_type(3)));
-                const f3v v3 = {x, y, z};
-                typedef __attribute__((address_space(3))) float* LdsF;
-                const uint32_t a3 = (uint32_t)(uintptr_t)(LdsF)(tb + slot);
-                uint64_t sv;
-                __asm__ volatile(
-                    "s_mov_b64 %0, exec\n\t"
-                    "s_mov_b32 exec_lo, -1\n\t"
-                    "s_mov_b32 exec_hi, 15\n\t"
-                    "s_and_b64 exec, exec, %0\n\t"
-                    "ds_write_b96 %1, %2\n\t"
-                    "s_mov_b32 exec_lo, 0xf8000000\n\t"
-                    "s_mov_b32 exec_hi, 15\n\t"
-                    "s_and_b64 exec, exec, %0\n\t"
-                    "ds_write_b32 %1, %3 offset:12\n\t"
-                    "s_mov_b64 exec, %0\n\t"
-                    : "=&s"(sv)
-                    : "v"(a3), "v"(v3), "v"(w)
-                    : "memory");
-            }
-#else
             *reinterpret_cast<float3*>(tb + slot) = make_float3(x, y, z);
-            *(bc == 3u ? tb + slot + 3u : L.cone() + 5u + (lane & 1u)) = w;
-#endif
+            *(bc == 3u ? tb + slot + 3u : L.cone() + 5u) = w;
         }
         const float R2b = dtc.x;
         const float T = dtc.w;
-        // Cone cull of child bi (centre c in lanes 27..35): no ray of the wave's cone can hit its bounding
+        // Cone cull of child bi (centre c in lanes 32..40): no ray of the wave's cone can hit its bounding
         // sphere. With ca = c.a, q = c - ca a, every lane's angle phi to c is >= alpha - theta, so its
         // line passes at distance |c| sin(phi) >= |q| cosT - ca sinT from c. A float hit
         // (tca >= 0, cc - tca^2 <= R^2, SIMD_AVX.h:247-258) needs |c| sin(phi) <= sqrt(R^2 + dl),
@@ -560,7 +538,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         // skip = ca > 0 && w > 2 (R2b + dl) && lhs > rhs, as ONE compare of a v_min3 (with denormals kept,
         // a > b exactly when fl(a - b) > 0; every operand is finite): the kept children straight from a ballot
         const float mk = __builtin_fminf(__builtin_fminf(ca, w - 2.0f * (R2b + dl)), lhs - rhs);
-        uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 27) & 0x1ffu;
+        uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 32) & 0x1ffu;
         M = __builtin_amdgcn_readfirstlane(M);
         SF_STAMP(6);
         uint32_t e = 0, pm = 0;
@@ -679,8 +657,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                         const float4 c4 = *reinterpret_cast<const float4*>(ctab + i * 4u);
                         cx = c4.x, cy = c4.y, cz = c4.z, cc = c4.w;
                     } else {
-                        cx = readlane_f(x, 27u + i), cy = readlane_f(y, 27u + i);
-                        cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
+                        cx = readlane_f(x, 32u + i), cy = readlane_f(y, 32u + i);
+                        cz = readlane_f(z, 32u + i), cc = readlane_f(w, 32u + i);
                     }
                     test_child(i, cx, cy, cz, cc);
                 }
@@ -707,8 +685,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                     const float4 c4 = *reinterpret_cast<const float4*>(ctab + i * 4u);
                     cx = c4.x, cy = c4.y, cz = c4.z, cc = c4.w;
                 } else {
-                    cx = readlane_f(x, 27u + i), cy = readlane_f(y, 27u + i);
-                    cz = readlane_f(z, 27u + i), cc = readlane_f(w, 27u + i);
+                    cx = readlane_f(x, 32u + i), cy = readlane_f(y, 32u + i);
+                    cz = readlane_f(z, 32u + i), cc = readlane_f(w, 32u + i);
                 }
                 const float tca = (cx * dx + cy * dy) + cz * dz;
                 const float d2 = cc - tca * tca;
@@ -739,8 +717,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         }
         pend = pm;
         // children none of whose own children can pass LOD for any ray (sfhost::leaf_threshold of their depth;
-        // |c|^2 of child i is w on lane 27 + i): entered as inline leaves
-        leafm = (uint32_t)(wave_ballot(w > leafc) >> 27) & 0x1ffu;
+        // |c|^2 of child i is w on lane 32 + i): entered as inline leaves
+        leafm = (uint32_t)(wave_ballot(w > leafc) >> 32) & 0x1ffu;
         return e;
     };
 
@@ -1744,12 +1722,14 @@ extern "C" __global__ __launch_bounds__(SF_MT_PAR_THREADS) void sf_mt_jump_parti
                                                                                     uint32_t poly_words,
                                                                                     uint32_t* __restrict__ partial)
 {
-    __shared__ uint32_t xs[SF_MT_CHUNK + 624u];
+    // xs: the chunk's raw words, then 624 zeros that the unused slots of an unrolled batch read (XOR 0)
+    __shared__ uint32_t xs[SF_MT_CHUNK + 624u + 624u];
     const uint32_t seg = blockIdx.x + 1u, part = blockIdx.y;   // segment 0 needs no jump
     const uint32_t i0 = part * SF_MT_CHUNK, i1 = min(19937u, i0 + SF_MT_CHUNK);
-    for (uint32_t i = threadIdx.x; i < (i1 - i0) + 624u; i += SF_MT_PAR_THREADS) xs[i] = raw[i0 + i];
+    const uint32_t nx = (i1 - i0) + 624u;
+    for (uint32_t i = threadIdx.x; i < nx + 624u; i += SF_MT_PAR_THREADS) xs[i] = i < nx ? raw[i0 + i] : 0u;
     __syncthreads();
-    const uint32_t k0 = threadIdx.x, k1 = k0 + 256u, k2 = k0 + 512u;   // this thread's window words (k2 < 624)
+    const uint32_t k0 = threadIdx.x, k1 = k0 + 256u, k2 = k0 < 112u ? k0 + 512u : k0;   // window words (k2: 624 total; unused past 112)
     uint32_t a0 = 0u, a1 = 0u, a2 = 0u;
     const uint64_t* pl = polys + (size_t)seg * poly_words;
     for (uint32_t q = i0 >> 6; q <= (i1 - 1u) >> 6; ++q) {
@@ -1757,18 +1737,34 @@ extern "C" __global__ __launch_bounds__(SF_MT_PAR_THREADS) void sf_mt_jump_parti
         const uint32_t lo = q * 64u;
         if (lo < i0) bits &= ~0ull << (i0 - lo);
         if (lo + 64u > i1) bits &= (i1 - lo) >= 64u ? ~0ull : ((1ull << (i1 - lo)) - 1ull);
+        // 8 coefficients per batch, their 24 LDS reads issued together (the zero block stands in for the
+        // coefficients past the word's last set bit): the loop is LDS-latency bound otherwise
         while (bits) {
-            const uint32_t i = lo + (uint32_t)__builtin_ctzll(bits) - i0;
-            bits &= bits - 1ull;
-            a0 ^= xs[i + k0];
-            a1 ^= xs[i + k1];
-            if (k2 < 624u) a2 ^= xs[i + k2];
+            uint32_t ix[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                ix[u] = bits ? lo + (uint32_t)__builtin_ctzll(bits) - i0 : nx;
+                bits &= bits - 1ull;
+            }
+            uint32_t v0[8], v1[8], v2[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                v0[u] = xs[ix[u] + k0];
+                v1[u] = xs[ix[u] + k1];
+                v2[u] = xs[ix[u] + k2];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                a0 ^= v0[u];
+                a1 ^= v1[u];
+                a2 ^= v2[u];
+            }
         }
     }
     uint32_t* out = partial + ((size_t)blockIdx.x * SF_MT_PARTS + part) * 624u;
     out[k0] = a0;
     out[k1] = a1;
-    if (k2 < 624u) out[k2] = a2;
+    if (k0 < 112u) out[k0 + 512u] = a2;
 }
 
 // Segment j of the batch's n draws: workgroup j builds its window (segment 0: the buffer; others: the XOR of
