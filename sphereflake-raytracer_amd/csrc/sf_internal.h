@@ -25,11 +25,15 @@
 // a level table stores them in 4 planes of 9 float4 (plane k = float4 k of children 0..8).
 #define SF_LDS_ROOT 16
 #define SF_LDS_CONE 8                     // the wave's ray cone {ax, ay, az, cosT, sinT, -, -, -}
-#define SF_LDS_PLANE 36                   // plane 0: {centre, cc} float4 of each of the 9 children
+// plane 0: {centre, cc} float4 of each of the 9 children (36 floats), 2 floats of skew, then planes 1..3:
+// column j (xyz, float3) of each child. The skew puts the column stores of the 27 column builders (lanes
+// 0..26, dwords 38 + 3l..) on other banks than child 0's centre store in the same 32-lane LDS group (lane 31,
+// dwords 0..3): the table build is free of bank conflicts (sf_kernels.hip, the builder lanes)
+#define SF_LDS_PLANE 38
 #define SF_LDS_COLS 27                    // planes 1..3: column j (xyz, float3) of each of the 9 children
 #define SF_LDS_TABLE (SF_LDS_PLANE + 3 * SF_LDS_COLS)   // the 9 child transforms of the node open at a level
 #define SF_LDS_E 32                       // 64 lanes x u16: per-lane child-expand bits of that node
-#define SF_LDS_LEVEL (SF_LDS_TABLE + SF_LDS_E + 3)      // (+3: levels stay 16-byte aligned)
+#define SF_LDS_LEVEL (SF_LDS_TABLE + SF_LDS_E + 1)      // (+1: levels stay 16-byte aligned)
 // levels - 1 level images: the deepest provisioned level's table is never read (see traverse)
 #define SF_LDS_WAVE_FLOATS(levels) (SF_LDS_ROOT + SF_LDS_CONE + ((levels) - 1) * SF_LDS_LEVEL)
 

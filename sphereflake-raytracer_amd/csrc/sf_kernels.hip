@@ -412,16 +412,17 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     }
 
     // This lane's column of the cooperative child build. The 27 axis columns (column c = lane / 9 of child
-    // i = lane % 9) are built by lanes 0..26 of the first 32-lane LDS group, the 9 centres (column 3) by
-    // lanes 32..40 of the second, so a table store never mixes the float3 column plane and the float4 centre
-    // plane in one bank group: every other lane repeats a builder of its own group (27..31: lane 26;
-    // 41..63: the centres again) -- the same address and value, which the LDS merges, not a bank conflict
-    // (round 2's layout, centres at lanes 27..35 with lanes 36..63 mirroring 0..27, put 40 % of the LDS
-    // cycles into conflicts). No divergent region; the build's VALU cost is per wave either way. Lanes
-    // 32..40 hold the 9 child centres (read back by v_readlane) and one ballot yields a per-child mask
-    // (bits 32..40).
-    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 8u : (lane - 32u) % 9u;
-    const uint32_t bc = lane < 27u ? lane / 9u : lane < 32u ? 2u : 3u;
+    // i = lane % 9) are built by lanes 0..26 of the first 32-lane LDS bank group, the 9 centres (column 3)
+    // by lanes 31 + i: child 0's by lane 31 of the first group, children 1..8 by lanes 32..39 of the second.
+    // With the column planes skewed by 2 floats (SF_LDS_PLANE) no store of the table build has two distinct
+    // addresses on one bank in a group; every other lane repeats a builder of its own group (27..30: child 0's
+    // centre; 40..63: children 1..8 again) -- the same address and value, merged by the LDS, not a conflict.
+    // (Round 2's layout -- centres on lanes 27..35, lanes 36..63 mirroring 0..27 -- put 4.9 M extra cycles per
+    // 1080p frame into bank conflicts, 40 % of the LDS instruction cycles.) No divergent region; the build's
+    // VALU cost is per wave either way. Lanes 31..39 hold the 9 child centres (read back by v_readlane) and
+    // one ballot yields a per-child mask (bits 31..39).
+    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 0u : 1u + ((lane - 32u) & 7u);
+    const uint32_t bc = lane < 27u ? lane / 9u : 3u;
     // The leaf-threshold skip bounds t from below for every ray. In packet semantics a lane with tca < 0
     // can also pass LOD through another lane's bounding hit (negative t, SIMD_AVX.h:254), which that
     // bound does not cover: there the skip additionally needs every sphere of the child's subtree in
@@ -520,7 +521,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         }
         const float R2b = dtc.x;
         const float T = dtc.w;
-        // Cone cull of child bi (centre c in lanes 32..40): no ray of the wave's cone can hit its bounding
+        // Cone cull of child bi (centre c in lanes 31..39): no ray of the wave's cone can hit its bounding
         // sphere. With ca = c.a, q = c - ca a, every lane's angle phi to c is >= alpha - theta, so its
         // line passes at distance |c| sin(phi) >= |q| cosT - ca sinT from c. A float hit
         // (tca >= 0, cc - tca^2 <= R^2, SIMD_AVX.h:247-258) needs |c| sin(phi) <= sqrt(R^2 + dl),
@@ -538,7 +539,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         // skip = ca > 0 && w > 2 (R2b + dl) && lhs > rhs, as ONE compare of a v_min3 (with denormals kept,
         // a > b exactly when fl(a - b) > 0; every operand is finite): the kept children straight from a ballot
         const float mk = __builtin_fminf(__builtin_fminf(ca, w - 2.0f * (R2b + dl)), lhs - rhs);
-        uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 32) & 0x1ffu;
+        uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 31) & 0x1ffu;
         M = __builtin_amdgcn_readfirstlane(M);
         SF_STAMP(6);
         uint32_t e = 0, pm = 0;
@@ -657,8 +658,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                         const float4 c4 = *reinterpret_cast<const float4*>(ctab + i * 4u);
                         cx = c4.x, cy = c4.y, cz = c4.z, cc = c4.w;
                     } else {
-                        cx = readlane_f(x, 32u + i), cy = readlane_f(y, 32u + i);
-                        cz = readlane_f(z, 32u + i), cc = readlane_f(w, 32u + i);
+                        cx = readlane_f(x, 31u + i), cy = readlane_f(y, 31u + i);
+                        cz = readlane_f(z, 31u + i), cc = readlane_f(w, 31u + i);
                     }
                     test_child(i, cx, cy, cz, cc);
                 }
@@ -685,8 +686,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                     const float4 c4 = *reinterpret_cast<const float4*>(ctab + i * 4u);
                     cx = c4.x, cy = c4.y, cz = c4.z, cc = c4.w;
                 } else {
-                    cx = readlane_f(x, 32u + i), cy = readlane_f(y, 32u + i);
-                    cz = readlane_f(z, 32u + i), cc = readlane_f(w, 32u + i);
+                    cx = readlane_f(x, 31u + i), cy = readlane_f(y, 31u + i);
+                    cz = readlane_f(z, 31u + i), cc = readlane_f(w, 31u + i);
                 }
                 const float tca = (cx * dx + cy * dy) + cz * dz;
                 const float d2 = cc - tca * tca;
@@ -717,8 +718,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         }
         pend = pm;
         // children none of whose own children can pass LOD for any ray (sfhost::leaf_threshold of their depth;
-        // |c|^2 of child i is w on lane 32 + i): entered as inline leaves
-        leafm = (uint32_t)(wave_ballot(w > leafc) >> 32) & 0x1ffu;
+        // |c|^2 of child i is w on lane 31 + i): entered as inline leaves
+        leafm = (uint32_t)(wave_ballot(w > leafc) >> 31) & 0x1ffu;
         return e;
     };
 
