@@ -1,0 +1,196 @@
+/* occl_sim.c -- CPU estimate of exact occlusion culling for the per-ray traversal (experiment, not product).
+ *
+ * The kernel's traversal order is pre-order (a node's own sphere is tested when it is entered, ties resolved
+ * by the ancestor rule), so when child c of a node is entered the lane's minT already holds its ancestors'
+ * spheres and everything before c in the DFS. Every sphere of c's subtree lies in c's bounding sphere
+ * (radius 2r around c). If the entry of that ball -- fattened by a margin covering every float rounding of
+ * the descendants' tests -- lies strictly beyond minT, no sphere of the subtree can be accepted: the lane
+ * may skip the subtree. The max-depth statistic is kept exact by culling only where no node of the subtree
+ * could expand deeper than the depth already reached (T_{maxd+1} <= lb).
+ *
+ * This program runs the plain per-ray traversal and the culling one over a frame, checks that minT, the
+ * hit index and the max depth agree on every pixel, and counts bounding tests and expansions of both.
+ * Built against oracle/sf_oracle.c (included) by scripts/experiments/occl_sim.py.
+ */
+#include "../../oracle/sf_oracle.c"
+
+typedef struct {
+    const float* child;
+    const uint32_t* lut;
+    int max_depth;
+    long long tests, interior, culled;
+    float margin;     /* relative margin (x |c|) */
+    int mode;         /* 1: lb = tca - rho, 2: lb = tca - sqrt(rho^2 - d2); +4: children front to back */
+    uint64_t* set;    /* per-tile set of expanded heap indices (open addressing, 0 = empty: stores idx + 1) */
+    uint32_t set_mask;
+    long long uniq;
+} ctrav_t;
+
+static void set_add(ctrav_t* tv, uint64_t idx)
+{
+    if (!tv->set) return;
+    uint64_t k = idx + 1, hsh = (k * 0x9E3779B97F4A7C15ull) >> 20;
+    for (;;) {
+        uint64_t* e = &tv->set[hsh & tv->set_mask];
+        if (*e == k) return;
+        if (*e == 0) { *e = k; tv->uniq++; return; }
+        ++hsh;
+    }
+}
+
+static int is_ancestor(uint64_t a, uint64_t n)
+{
+    while (n > a) n = (n - 1) / 9;
+    return n == a;
+}
+
+static float lod_T(float r) { return g_lod_constant * g_lod_constant * r; } /* t < T (approximately: sim only) */
+
+static void intersect_cull(ctrav_t* tv, const float D[3], const float* node_m, hit_t* h, float r, int depth,
+                           uint64_t node)
+{
+    /* node_m: this node's world transform; called for a node that passed bounding + LOD (expanded) */
+    if (depth > tv->max_depth) tv->max_depth = depth;
+    tv->interior++;
+    set_add(tv, node);
+    const float* C = node_m + 12;
+    float scale = (4.0f / 3.0f) * r;
+    float rc = r / 3.0f;              /* children's radius */
+    float R2b = (rc * 2.0f) * (rc * 2.0f);
+    float R2s = rc * rc;
+    float Wall[9][16];
+    int order[9];
+    for (int i = 0; i < 9; ++i) {
+        float T[16];
+        memcpy(T, tv->child + 16 * i, sizeof T);
+        T[12] *= scale; T[13] *= scale; T[14] *= scale;
+        matmul(node_m, T, Wall[i]);
+        order[i] = i;
+    }
+    if (tv->mode & 4) {   /* insertion sort by tca (sim only: ties not resolved in reference order) */
+        float key[9];
+        for (int i = 0; i < 9; ++i) key[i] = (Wall[i][12] * D[0] + Wall[i][13] * D[1]) + Wall[i][14] * D[2];
+        for (int i = 1; i < 9; ++i)
+            for (int j = i; j > 0 && key[order[j]] < key[order[j - 1]]; --j) { int t_ = order[j]; order[j] = order[j - 1]; order[j - 1] = t_; }
+    }
+    for (int oi = 0; oi < 9; ++oi) {
+        const int i = order[oi];
+        float* Wm = Wall[i];
+        const float* Cc = Wm + 12;
+        tv->tests++;
+        float tb;
+        if (!ray_sphere(D, Cc, R2b, &tb)) continue;
+        int expands = sqrtf(tb / rc) < g_lod_constant || tb < 0.0f;
+        /* child's own sphere is tested by the reference even when it does not expand? No: the reference
+           returns before the children and the self test when LOD fails (Sphereflake.h:146-153). */
+        if (!expands) continue;
+        if (depth + 1 > tv->max_depth) tv->max_depth = depth + 1;
+        /* cull check at entry */
+        if (tv->margin >= 0.0f) {
+            float tca = (Cc[0] * D[0] + Cc[1] * D[1]) + Cc[2] * D[2];
+            float cc = (Cc[0] * Cc[0] + Cc[1] * Cc[1]) + Cc[2] * Cc[2];
+            float R = 2.0f * rc;
+            float M = tv->margin * (sqrtf(cc) + R);
+            float rho = R + M, lb;
+            if ((tv->mode & 3) == 1) lb = tca - rho;
+            else {
+                float d2 = cc - tca * tca;
+                float a = rho * rho - d2;
+                lb = tca - sqrtf(a > 0.0f ? a : 0.0f) - M;
+            }
+            float Tn = lod_T(1.0f / powf(3.0f, (float)(tv->max_depth + 1)));
+            if (lb > h->minT && lb >= Tn && lb >= 0.0f) {
+                tv->culled++;
+                continue;
+            }
+        }
+        /* own sphere, pre-order with the ancestor tie rule */
+        float ts;
+        uint64_t idx = 9 * node + 1 + (uint64_t)i;
+        if (ray_sphere(D, Cc, R2s, &ts)) {
+            if (ts < h->minT || (ts == h->minT && h->depth >= 0 && is_ancestor(h->index, idx))) {
+                h->minT = ts;
+                h->index = idx;
+                h->depth = depth + 1;
+            }
+        }
+        intersect_cull(tv, D, Wm, h, rc, depth + 1, idx);
+    }
+}
+
+/* plain / culling traversal over rows [y0, y1): minT, index out; stats[0] max depth, [1] tests, [2] interior,
+   [3] culled */
+int sim_rows(uint32_t W, uint32_t H, const float o[3], const float tl[3], const float tr[3], const float bl[3],
+             const float root[16], const float child[9 * 16], const uint32_t* lut, uint32_t y0, uint32_t y1,
+             float margin, int mode, float* minT, uint32_t* index, long long* stats)
+{
+    ctrav_t tv = { child, lut, 0, 0, 0, 0, margin, mode, NULL, 0, 0 };
+    float fw = (float)W, fh = (float)H;
+    float dx_ = tr[0] - tl[0], dy_ = tr[1] - tl[1], dz_ = tr[2] - tl[2];
+    float ex_ = bl[0] - tl[0], ey_ = bl[1] - tl[1], ez_ = bl[2] - tl[2];
+    for (uint32_t y = y0; y < y1; ++y)
+        for (uint32_t x = 0; x < W; ++x) {
+            float u = (float)x / fw, v = (float)y / fh, D[3];
+            D[0] = ((tl[0] + dx_ * u) + ex_ * v) - o[0];
+            D[1] = ((tl[1] + dy_ * u) + ey_ * v) - o[1];
+            D[2] = ((tl[2] + dz_ * u) + ez_ * v) - o[2];
+            normalize3(D, lut);
+            hit_t h;
+            h.minT = FLT_MAX;
+            h.index = 0xffffffffu;
+            h.depth = -1;
+            /* root: bounding + LOD, then its own sphere, then children */
+            const float* C = root + 12;
+            float tb;
+            tv.tests++;
+            if (ray_sphere(D, C, 4.0f, &tb) && (sqrtf(tb / 1.0f) < g_lod_constant || tb < 0.0f)) {
+                float ts;
+                if (ray_sphere(D, C, 1.0f, &ts) && ts < h.minT) { h.minT = ts; h.index = 0; h.depth = 0; }
+                intersect_cull(&tv, D, root, &h, 1.0f, 0, 0);
+            }
+            size_t p = (size_t)(y - y0) * W + x;
+            minT[p] = h.minT;
+            index[p] = (uint32_t)h.index;
+        }
+    stats[0] = tv.max_depth; stats[1] = tv.tests; stats[2] = tv.interior; stats[3] = tv.culled;
+    return 0;
+}
+
+/* tile-level: 8x8 tiles of rows [ty*8, ty*8+8), unique expanded nodes per tile summed (a wave visits a node iff
+   some lane does) */
+int sim_tile_row(uint32_t W, uint32_t H, const float o[3], const float tl[3], const float tr[3], const float bl[3],
+                 const float root[16], const float child[9 * 16], const uint32_t* lut, uint32_t ty,
+                 float margin, int mode, long long* stats)
+{
+    const uint32_t cap = 1u << 18;
+    uint64_t* set = (uint64_t*)calloc(cap, 8);
+    float fw = (float)W, fh = (float)H;
+    float dx_ = tr[0] - tl[0], dy_ = tr[1] - tl[1], dz_ = tr[2] - tl[2];
+    float ex_ = bl[0] - tl[0], ey_ = bl[1] - tl[1], ez_ = bl[2] - tl[2];
+    long long uniq = 0, tests = 0, interior = 0;
+    for (uint32_t tx = 0; tx < (W + 7) / 8; ++tx) {
+        memset(set, 0, (size_t)cap * 8);
+        ctrav_t tv = { child, lut, 0, 0, 0, 0, margin, mode, set, cap - 1, 0 };
+        for (uint32_t y = ty * 8; y < ty * 8 + 8 && y < H; ++y)
+            for (uint32_t x = tx * 8; x < tx * 8 + 8 && x < W; ++x) {
+                float u = (float)x / fw, v = (float)y / fh, D[3];
+                D[0] = ((tl[0] + dx_ * u) + ex_ * v) - o[0];
+                D[1] = ((tl[1] + dy_ * u) + ey_ * v) - o[1];
+                D[2] = ((tl[2] + dz_ * u) + ez_ * v) - o[2];
+                normalize3(D, lut);
+                hit_t h;
+                h.minT = FLT_MAX; h.index = 0xffffffffu; h.depth = -1;
+                const float* C = root + 12;
+                float tb;
+                if (ray_sphere(D, C, 4.0f, &tb) && (sqrtf(tb) < g_lod_constant || tb < 0.0f)) {
+                    float ts;
+                    if (ray_sphere(D, C, 1.0f, &ts) && ts < h.minT) { h.minT = ts; h.index = 0; h.depth = 0; }
+                    intersect_cull(&tv, D, root, &h, 1.0f, 0, 0);
+                }
+            }
+        uniq += tv.uniq; tests += tv.tests; interior += tv.interior;
+    }
+    free(set);
+    stats[0] = uniq; stats[1] = interior; stats[2] = tests;
+    return 0;
+}

@@ -1,0 +1,12 @@
+# occlusion cull: parity suite (cull on by default), then cull on vs off (SF_FLAGS=0x100) timing + PMC, loop probe
+set -o pipefail
+R=$PWD; OUT=$R/gpurun_out/r3i; mkdir -p $OUT
+L=sphereflake-raytracer_amd/build/libsphereflake_hip.so
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
+tail -3 $OUT/pytest_gpu.log
+grep -E "FAILED|Error" $OUT/pytest_gpu.log | head -20
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+REPS=3 PMC=1 scripts/lib_ab.sh r3i/occl "" $L@0 $L@0x100 || exit 5
+timeout -k 10 300 python -u scripts/loop_probe.py > $OUT/loop.txt 2>&1 || exit 6
+cat $OUT/loop.txt
+exit $rc

@@ -11,6 +11,9 @@
 #endif
 
 #define SF_DEPTH_TABLE 33      // depths 0..32 (SF_MAX_DEPTH_LIMIT)
+// relative margin of the occlusion cull: a subtree's bounding ball (radius R around c) is fattened to
+// R + SF_OCCL_MARGIN (|c| + R), about 4.6x the worst-case rounding of the float tests inside it
+#define SF_OCCL_MARGIN 0x1p-7f
 #define SF_TILE 8              // a wave64 traces one 8x8 pixel tile
 #define SF_WAVES_PER_BLOCK 4   // 256-thread workgroups (per-ray kernel)
 #ifndef SF_WAVES_PER_EU
@@ -68,6 +71,8 @@
 // flat wave priority (A/B): every raised-priority cost bucket at s_setprio 2 (default: graded, see
 // trace_queue_body)
 #define SF_FLAG_PRIO_FLAT 0x80u
+// disable the occlusion cull of the per-ray traversal (A/B only; results identical)
+#define SF_FLAG_NO_OCCL_CULL 0x100u
 
 struct DepthTables {
     float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)
@@ -81,8 +86,9 @@ struct DeviceConsts {
     float child[9][16];               // unit child frames, glm column-major (Sphereflake.cpp:216-249)
     DepthTables dt;
     // the same interleaved per depth d, one scalar load: {r2_bound, r2_self, scale, lod,
-    // leaf, 0, 0, 0}; leaf = |c|^2 threshold beyond which no child of a depth-d node centred at c can
-    // pass the LOD test for any ray (sfhost::leaf_threshold)
+    // leaf, cull, 0, 0}; leaf = |c|^2 threshold beyond which no child of a depth-d node centred at c can
+    // pass the LOD test for any ray (sfhost::leaf_threshold); cull = 2 r_d (1 + SF_OCCL_MARGIN), rounded
+    // up: the occlusion cull's fattened bounding radius without its |c| term (see traverse)
     float depth8[SF_DEPTH_TABLE][8];
     uint32_t lut[2048];               // x86 rsqrtps table (rsqrtps_lut.inc)
     uint32_t sobol[2][52];            // Sobol direction numbers, dims 0 and 1 (Sobol.cpp:34-39, 57-162)

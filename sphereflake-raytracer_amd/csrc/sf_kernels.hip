@@ -330,6 +330,18 @@ __device__ __forceinline__ float depth_leaf(const DeviceConsts* K, uint32_t d)
 #endif
 }
 
+// {.., cull} of depth d: 2 r_d (1 + SF_OCCL_MARGIN), rounded up (see DeviceConsts::depth8)
+__device__ __forceinline__ float depth_cull(const DeviceConsts* K, uint32_t d)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) float* ConstF;
+    typedef const __attribute__((address_space(4))) char* ConstC;
+    return *(ConstF)((ConstC)(const void*)K->depth8 + (d << 5) + 20u);
+#else
+    return reinterpret_cast<const float4*>(K->depth8)[2u * d + 1u].y;
+#endif
+}
+
 // Root transform -> the wave's LDS image in the transform layout (Sphereflake.cpp:83). The same for
 // every tile of a frame: kernels stage it once per wave, before any tile loop.
 __device__ __forceinline__ void stage_root(float* __restrict__ Lbase, const float* root)
@@ -363,6 +375,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     const uint32_t lane = threadIdx.x & 63u;
     const TraverseLds L{ Lbase };
     const bool cone_cull = (K_flags & SF_FLAG_NO_CONE_CULL) == 0u;
+    const bool occl_cull = (K_flags & SF_FLAG_NO_OCCL_CULL) == 0u;
     SF_STAMP_DECL;
 
     h.minT = FLT_MAX;
@@ -758,6 +771,28 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             const float4 pc = *reinterpret_cast<const float4*>(node);
             const float4 dc1 = depth_consts(K, d + 1u);
             maxd = (int32_t)d + 1 > maxd ? (int32_t)d + 1 : maxd;   // Sphereflake.h:157-160
+            // Occlusion cull (per-ray semantics): every sphere of the child's subtree, and every bounding sphere
+            // the subtree's LOD tests use, lies in the child's bounding ball (radius R = 2r around c). A lane
+            // whose float test of any of them accepts has t >= c.d - rho, rho = R + m (|c| + R), m =
+            // SF_OCCL_MARGIN covering every rounding of those tests (tca, the d2 cancellation -- the dominant
+            // 2^-9.2 (|c| + R) --, the centres' transform chain, |d| != 1). So where c.d - rho > minT the lane
+            // can accept nothing in the subtree (ties included: strict), and where c.d - rho >= T of depth
+            // maxd + 1 no node of the subtree can pass LOD deeper than the depth already reached (T falls with
+            // depth): the max-depth statistic is unchanged. Such lanes do not enter; if none is left, the child
+            // is skipped. (The child itself passed LOD for some lane: maxd above counts it either way.)
+            uint64_t amx = am;
+            float avx = av;
+            if constexpr (!PACKET) {
+                if (occl_cull) {
+                    const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
+                    const float rho = depth_cull(K, d + 1u) + SF_OCCL_MARGIN * __builtin_amdgcn_sqrtf(pc.w);
+                    const float te = depth_consts(K, (uint32_t)maxd + 1u).w;
+                    const uint64_t cm = wave_ballot(__builtin_fminf(tca - h.minT, tca - te) > rho);
+                    amx = am & ~cm;
+                    if (amx == 0ull) continue;
+                    avx = sel_mask(av, -1.0f, cm);
+                }
+            }
             self_test(pc, d + 1u, am, av, idxB + c, dc1.y);
             // A child none of whose children can pass LOD for any ray (sfhost::leaf_threshold) only needs its
             // own sphere: no push, no level, no child build. (leafN: decided for all 9 children when the parent
@@ -776,7 +811,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             idxB = 9u * (idxB + c) + 1u;
             d += 1u;
             SF_STAMP(1);
-            eN = expand(node, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, a, am, av, pend, leafN);
+            eN = expand(node, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, a, amx, avx, pend, leafN);
             SF_STAMP(2);
             continue;
         }

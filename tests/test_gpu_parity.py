@@ -629,6 +629,30 @@ def test_raised_priority_tiles_bit_exact(prio, monkeypatch):
         assert 0 < np.count_nonzero(lv) < len(units)
 
 
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c4"])
+def test_occlusion_cull_on_off_identical(name, monkeypatch):
+    """The per-ray traversal's occlusion cull (a lane skips a subtree whose fattened bounding ball starts
+    beyond its nearest hit, and only where the subtree cannot pass LOD deeper than the depth already
+    reached) changes neither a pixel nor a statistic: frames with the cull off (SF_FLAGS=0x100) and on are
+    identical -- G-buffer, minT, hit index, max depth, closest -- and equal the golden frame."""
+    fx = load_frame(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    out = {}
+    for flags in ("0x100", "0"):
+        monkeypatch.setenv("SF_FLAGS", flags)
+        with sf.Sphereflake(W, H) as s:
+            s.SetCamera(sf.config_camera(W, H, K))
+            for _ in range(2):   # row-major, then heavy-first order
+                s.Render(emit_aux=True)
+            out[flags] = s.download(aux=True), s.stats()
+    (a, sa), (b, sb) = out["0x100"], out["0"]
+    for x, y in zip(a, b):
+        assert np.array_equal(np.ascontiguousarray(x).view(np.uint8), np.ascontiguousarray(y).view(np.uint8))
+    assert (sa.max_depth, sa.closest, sa.rays) == (sb.max_depth, sb.closest, sb.rays)
+    assert frame_digest(b[0], b[1]) == fx["frame_digest"]
+    assert sb.max_depth == fx["stats"]["max_depth"]
+
+
 @pytest.mark.parametrize("blocks,nq", [("4", "8"), ("3", "8"), ("1", "8"), ("6", "4")])
 def test_tiny_grid_many_queues_bit_exact(blocks, nq, monkeypatch):
     """A persistent grid of fewer blocks than tile queues (SF_MAX_BLOCKS below SF_NQUEUES, as a CU-masked
