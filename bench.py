@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--settle-ms", type=float, default=SETTLE_MS,
+                    help="untimed frames beyond --warmup until the GPU has been under load this long (0: off)")
     ap.add_argument("--mode", choices=["dist", "frames", "rows"], default="dist")
     ap.add_argument("--slots", type=int, default=DEFAULT_SLOTS, help="frames in flight (dist mode)")
     ap.add_argument("--kernel", choices=["wave", "ray"], default="wave")
@@ -78,6 +80,24 @@ def parse():
 
 DEFAULT_SLOTS = 3                    # frames in flight: 1080p 0.149 / 0.140 / 0.136 / 0.133 ms per frame at 1-4
                                      # (profiles/r3/overlap_1080.txt); 3 keeps the latency at ~3 frames
+
+
+SETTLE_MS = 150.0                    # the shader clock ramps from ~2075 to ~2370 MHz over the first ~60 ms of load
+                                     # (profiles/r3/ramp.txt): warm-up lasts at least this long
+
+
+def settle(d, render, views, n_views, t_start, ms):
+    """Untimed frames (cycling views[:n_views]) until `ms` have passed since t_start with the GPU under load;
+    returns the number of extra frames."""
+    k = 0
+    d.Synchronize()
+    while (time.perf_counter() - t_start) * 1e3 < ms:
+        for _ in range(20):
+            d.SetView(*views[k % n_views])
+            render()
+            k += 1
+        d.Synchronize()
+    return k
 
 
 PATH_AMPLITUDE = 10                  # camera path: yaw sweeps +-10 mrad around the config view, 1 mrad/frame
@@ -351,9 +371,11 @@ def run_rows(args, torch, ctl, n, kernel):
         g.Render(band)
         g.Synchronize()
         first_ms = (time.perf_counter() - t) * 1e3
+        t_w = time.perf_counter()
         for i in range(args.warmup):
             g.SetView(*views[i])
             g.Render(band)
+        settle(g, lambda: g.Render(band), views, max(1, args.warmup), t_w, args.settle_ms)
         g.member_kernel_timing(0, True, period=kp)
         g.Synchronize()
         g.reset_stats()
@@ -441,7 +463,7 @@ def slot_period(steps, slots):
 
 
 def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows, nranks, frame_of,
-              fixed=False, latency=False, first=False, gather=False):
+              fixed=False, latency=False, first=False, gather=False, settle_ms=SETTLE_MS):
     """One timed loop of the sf_dist path: `steps` frames (frame_of(i) of the camera path at step i) after
     `warmup`, `slots` in flight, over `nranks` ranks (1: this GPU alone, every rank its own frames); each frame
     is every rank's bands into its own G-buffer (the distributed G-buffer), or with `gather` also assembled on
@@ -460,9 +482,11 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
         render()
         d.Synchronize()
         out["first_render_ms"] = (time.perf_counter() - t) * 1e3
+    t_w = time.perf_counter()
     for i in range(warmup):
         d.SetView(*views[i])
         render()
+    out["settle_frames"] = settle(d, render, views, max(1, warmup), t_w, settle_ms)
     kp = slot_period(steps, slots)
     for s in range(slots):
         d.kernel_timing(s, True, period=kp)
@@ -563,11 +587,11 @@ def main():
     if args.mode == "dist":
         # the frame split over the ranks, each rank's bands into its own HBM (the distributed G-buffer)
         r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
-                      lambda i: i, fixed=True, latency=True, first=True)
+                      lambda i: i, fixed=True, latency=True, first=True, settle_ms=args.settle_ms)
         rays_step = width * height
         if n > 1:   # the same frames also assembled on rank 0: RCCL gather of the packed slabs + unpack
             rg = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
-                           lambda i: i, latency=True, gather=True)
+                           lambda i: i, latency=True, gather=True, settle_ms=args.settle_ms)
             rg["dist"].close()
             gathered = {"value": round(rays_step / rg["t_step"] / 1e6, 2), "frame_ms": round(rg["t_step"] * 1e3, 4),
                         "frame_latency_ms": round(rg["latency_ms"], 4),
@@ -579,7 +603,7 @@ def main():
                                 "on rank 0 sees; bound by the peers' links into rank 0"}
     else:   # frames: every rank its own frames (frame i * N + rank), one GPU each, slots in flight
         r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, 1,
-                      lambda i: i * n + rank, fixed=True, latency=True, first=True)
+                      lambda i: i * n + rank, fixed=True, latency=True, first=True, settle_ms=args.settle_ms)
         rays_step = width * height * n
     d = r["dist"]
     t_step = r["t_step"]
@@ -590,7 +614,7 @@ def main():
     indep = None
     if args.mode == "dist" and n > 1:
         ri = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, 1,
-                       lambda i: i * n + rank)
+                       lambda i: i * n + rank, settle_ms=args.settle_ms)
         ri["dist"].close()
         indep = {"value": round(n * width * height / ri["t_step"] / 1e6, 2), "frame_ms": round(ri["t_step"] * 1e3, 4),
                  "scaling": "weak", "note": "every rank renders its own full frames (frame i * N + rank), no gather"}
@@ -599,7 +623,8 @@ def main():
     c4 = None
     if not args.no_extras and (width, height, round(args.K, 4)) == (W, H, K):
         r4 = dist_loop(ctl, torch, dev, 3840, 2160, 0.22, 60, 15, slots, args.band_rows,
-                       n if args.mode == "dist" else 1, (lambda i: i) if args.mode == "dist" else (lambda i: i * n + rank))
+                       n if args.mode == "dist" else 1, (lambda i: i) if args.mode == "dist" else (lambda i: i * n + rank),
+                       settle_ms=args.settle_ms)
         rays0_4 = (sf.lib().sf_slab_rows(2160, args.band_rows, n, 0) if args.mode == "dist" else 2160) * 3840
         a4 = BYTES_PER_RAY * rays0_4 / (r4["trace_ms"] * 1e-3) / 1e9 if r4["trace_ms"] else None
         c4 = {"config": "BASELINE configs[3]: 3840x2160, K=0.22", "max_depth": r4["stats"].max_depth,
@@ -659,6 +684,9 @@ def main():
             "n_gpus": n,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle": {"min_ms": args.settle_ms, "frames": r["settle_frames"],
+                       "note": "untimed frames after --warmup until the GPU has been under load min_ms: the shader "
+                               "clock ramps from ~2075 to ~2370 MHz over the first ~60 ms (profiles/r3/ramp.txt)"},
             "ms_per_step": round(t_step * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong" if args.mode == "dist" else "weak",

@@ -18,9 +18,10 @@ typedef struct {
     const float* child;
     const uint32_t* lut;
     int max_depth;
-    long long tests, interior, culled;
+    long long tests, interior, culled, ties;
     float margin;     /* relative margin (x |c|) */
     int mode;         /* 1: lb = tca - rho, 2: lb = tca - sqrt(rho^2 - d2); +4: children front to back */
+    float axis[3];    /* mode & 8: children ordered along this direction (the tile's centre ray) for every lane */
     uint64_t* set;    /* per-tile set of expanded heap indices (open addressing, 0 = empty: stores idx + 1) */
     uint32_t set_mask;
     long long uniq;
@@ -67,9 +68,18 @@ static void intersect_cull(ctrav_t* tv, const float D[3], const float* node_m, h
         matmul(node_m, T, Wall[i]);
         order[i] = i;
     }
-    if (tv->mode & 4) {   /* insertion sort by tca (sim only: ties not resolved in reference order) */
+    if (tv->mode & 16) {   /* two buckets: children with key below the parent's centre first, index order in each */
+        const float* A = tv->axis;
+        const float kp = (C[0] * A[0] + C[1] * A[1]) + C[2] * A[2];
+        int n = 0;
+        for (int i = 0; i < 9; ++i)
+            if ((Wall[i][12] * A[0] + Wall[i][13] * A[1]) + Wall[i][14] * A[2] < kp) order[n++] = i;
+        for (int i = 0; i < 9; ++i)
+            if (!((Wall[i][12] * A[0] + Wall[i][13] * A[1]) + Wall[i][14] * A[2] < kp)) order[n++] = i;
+    } else if (tv->mode & 12) {   /* insertion sort by tca (sim only: ties not resolved in reference order) */
         float key[9];
-        for (int i = 0; i < 9; ++i) key[i] = (Wall[i][12] * D[0] + Wall[i][13] * D[1]) + Wall[i][14] * D[2];
+        const float* A = (tv->mode & 8) ? tv->axis : D;
+        for (int i = 0; i < 9; ++i) key[i] = (Wall[i][12] * A[0] + Wall[i][13] * A[1]) + Wall[i][14] * A[2];
         for (int i = 1; i < 9; ++i)
             for (int j = i; j > 0 && key[order[j]] < key[order[j - 1]]; --j) { int t_ = order[j]; order[j] = order[j - 1]; order[j - 1] = t_; }
     }
@@ -108,6 +118,7 @@ static void intersect_cull(ctrav_t* tv, const float D[3], const float* node_m, h
         float ts;
         uint64_t idx = 9 * node + 1 + (uint64_t)i;
         if (ray_sphere(D, Cc, R2s, &ts)) {
+            if (ts == h->minT && h->depth >= 0 && !is_ancestor(h->index, idx)) tv->ties++;
             if (ts < h->minT || (ts == h->minT && h->depth >= 0 && is_ancestor(h->index, idx))) {
                 h->minT = ts;
                 h->index = idx;
@@ -124,7 +135,7 @@ int sim_rows(uint32_t W, uint32_t H, const float o[3], const float tl[3], const 
              const float root[16], const float child[9 * 16], const uint32_t* lut, uint32_t y0, uint32_t y1,
              float margin, int mode, float* minT, uint32_t* index, long long* stats)
 {
-    ctrav_t tv = { child, lut, 0, 0, 0, 0, margin, mode, NULL, 0, 0 };
+    ctrav_t tv = { child, lut, 0, 0, 0, 0, 0, margin, mode, {0, 0, 0}, NULL, 0, 0 };
     float fw = (float)W, fh = (float)H;
     float dx_ = tr[0] - tl[0], dy_ = tr[1] - tl[1], dz_ = tr[2] - tl[2];
     float ex_ = bl[0] - tl[0], ey_ = bl[1] - tl[1], ez_ = bl[2] - tl[2];
@@ -167,10 +178,17 @@ int sim_tile_row(uint32_t W, uint32_t H, const float o[3], const float tl[3], co
     float fw = (float)W, fh = (float)H;
     float dx_ = tr[0] - tl[0], dy_ = tr[1] - tl[1], dz_ = tr[2] - tl[2];
     float ex_ = bl[0] - tl[0], ey_ = bl[1] - tl[1], ez_ = bl[2] - tl[2];
-    long long uniq = 0, tests = 0, interior = 0;
+    long long uniq = 0, tests = 0, interior = 0, ties_all = 0;
     for (uint32_t tx = 0; tx < (W + 7) / 8; ++tx) {
         memset(set, 0, (size_t)cap * 8);
-        ctrav_t tv = { child, lut, 0, 0, 0, 0, margin, mode, set, cap - 1, 0 };
+        ctrav_t tv = { child, lut, 0, 0, 0, 0, 0, margin, mode, {0, 0, 0}, set, cap - 1, 0 };
+        {
+            float u = (float)(tx * 8 + 4) / fw, v = (float)(ty * 8 + 4) / fh;
+            tv.axis[0] = ((tl[0] + dx_ * u) + ex_ * v) - o[0];
+            tv.axis[1] = ((tl[1] + dy_ * u) + ey_ * v) - o[1];
+            tv.axis[2] = ((tl[2] + dz_ * u) + ez_ * v) - o[2];
+            normalize3(tv.axis, lut);
+        }
         for (uint32_t y = ty * 8; y < ty * 8 + 8 && y < H; ++y)
             for (uint32_t x = tx * 8; x < tx * 8 + 8 && x < W; ++x) {
                 float u = (float)x / fw, v = (float)y / fh, D[3];
@@ -188,9 +206,9 @@ int sim_tile_row(uint32_t W, uint32_t H, const float o[3], const float tl[3], co
                     intersect_cull(&tv, D, root, &h, 1.0f, 0, 0);
                 }
             }
-        uniq += tv.uniq; tests += tv.tests; interior += tv.interior;
+        uniq += tv.uniq; tests += tv.tests; interior += tv.interior; ties_all += tv.ties;
     }
     free(set);
-    stats[0] = uniq; stats[1] = interior; stats[2] = tests;
+    stats[0] = uniq; stats[1] = interior; stats[2] = ties_all;
     return 0;
 }

@@ -110,7 +110,7 @@ struct sf_ctx {
     uint32_t* hit_index = nullptr;
     int32_t* stats = nullptr;          // [0] max depth, [1] closest key, [2] unrecoverable overflow
     uint32_t* ovf_counters = nullptr;  // [0,1] overflow counts, then the tile queues (SF_QUEUE_WORD); alternating per render
-    uint32_t* ovf_list = nullptr;      // tiles_x * tiles_y entries
+    uint32_t* ovf_list = nullptr;      // 4 x tiles_x * tiles_y entries (one per work unit)
     DeviceConsts* consts = nullptr;
     DeviceConsts host_consts;
     float child[9][16];
@@ -479,7 +479,8 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if ((e = hipMalloc(&c->hit_index, npx * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->stats, 16)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->ovf_counters, SF_COUNTER_WORDS * 4)) != hipSuccess) return fail(e);
-    if ((e = hipMalloc(&c->ovf_list, ntiles * 4)) != hipSuccess) return fail(e);
+    // each work unit pushes its tile at most once and a tile has <= 4 units: 4 entries per tile
+    if ((e = hipMalloc(&c->ovf_list, 4 * ntiles * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->tile_cost, ntiles * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->tile_order, 4 * ntiles * 4)) != hipSuccess) return fail(e);   // <= 4 units per tile
     if ((e = hipMalloc(&c->order_meta, 4 * 4)) != hipSuccess) return fail(e);
@@ -753,11 +754,14 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             else hipLaunchKernelGGL(sf_trace_wave4, grid, block, 4 * lds, s, a, c->ovf_list, cnt);
         }
         SF_HIP(c, hipGetLastError());
-        // Re-trace of overflowed tiles, unless the levels are proven sufficient (persistent kernel;
-        // it also zeroes the next render's overflow counter itself).
-        if (!(bounded && c->persistent)) {
+        // Re-trace of overflowed tiles (it also zeroes the next render's overflow counter itself). With the
+        // levels proven sufficient (persistent kernel) only an exact tie under the front-first child order can
+        // flag a tile -- never seen on the BASELINE views --: then a small grid suffices.
+        const bool front_first = (c->flags & (SF_FLAG_NO_OCCL_CULL | SF_FLAG_NO_FRONT_FIRST)) == 0u;
+        if (!(bounded && c->persistent) || front_first) {
             const size_t lds_fix = (size_t)SF_LDS_WAVE_FLOATS(SF_MAX_DEPTH_LIMIT) * 4;
-            hipLaunchKernelGGL(sf_fixup_wave, dim3(4 * c->fixup_blocks), dim3(64), lds_fix, s, a,
+            const uint32_t fb = (bounded && c->persistent) ? 8u : 4u * (uint32_t)c->fixup_blocks;
+            hipLaunchKernelGGL(sf_fixup_wave, dim3(fb), dim3(64), lds_fix, s, a,
                                (const uint32_t*)c->ovf_list, c->ovf_counters, c->parity);
             SF_HIP(c, hipGetLastError());
         }

@@ -73,6 +73,11 @@
 #define SF_FLAG_PRIO_FLAT 0x80u
 // disable the occlusion cull of the per-ray traversal (A/B only; results identical)
 #define SF_FLAG_NO_OCCL_CULL 0x100u
+// children in index order only (A/B; results identical): by default the per-ray traversal enters the children
+// nearer than their parent's centre along the tile's cone axis first
+#define SF_FLAG_NO_FRONT_FIRST 0x200u
+// tests only: every tile of the main kernels takes the tie fallback (re-traced by sf_fixup_wave in index order)
+#define SF_FLAG_DIAG_FORCE_RETRACE 0x400u
 
 struct DepthTables {
     float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)

@@ -29,7 +29,8 @@
 //   sf_order_scan / sf_order_scatter -- the next render's unit order from this render's tile costs.
 //   sf_trace_wave{1,2,4} -- the same traversal, one workgroup per tile group (non-persistent A/B path).
 //   sf_fixup_wave   -- re-traces the tiles flagged as needing more LDS levels than provisioned, with
-//                      SF_MAX_LEVELS levels.
+//                      SF_MAX_LEVELS levels, and those with an exact tie under the front-first child order,
+//                      in index order.
 //   sf_trace_ray    -- one thread per ray with a private traversal stack (the straightforward
 //                      formulation; cross-check and comparison point).
 //   sf_band_unpack  -- packed band slabs of a multi-GPU frame -> the G-buffer at frame positions.
@@ -342,6 +343,10 @@ __device__ __forceinline__ float depth_cull(const DeviceConsts* K, uint32_t d)
 #endif
 }
 
+// traverse's status bits: the tile needs more levels than provisioned; an exact tie under the front-first order
+#define SF_STATUS_OVERFLOW 1u
+#define SF_STATUS_TIE 2u
+
 // Root transform -> the wave's LDS image in the transform layout (Sphereflake.cpp:83). The same for
 // every tile of a frame: kernels stage it once per wave, before any tile loop.
 __device__ __forceinline__ void stage_root(float* __restrict__ Lbase, const float* root)
@@ -367,7 +372,7 @@ __device__ __forceinline__ void stage_root(float* __restrict__ Lbase, const floa
 template <int PW, bool PIPE = false>
 __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ Lbase,
                                          uint32_t levels, float dx, float dy, float dz, bool valid, HitState& h,
-                                         int32_t& maxd, bool& overflowed, uint32_t K_flags,
+                                         int32_t& maxd, uint32_t& status, uint32_t K_flags,
                                          uint64_t* phase_sums = nullptr, uint32_t axl = 36u,
                                          uint64_t* tile_counts = nullptr)
 {
@@ -376,6 +381,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     const TraverseLds L{ Lbase };
     const bool cone_cull = (K_flags & SF_FLAG_NO_CONE_CULL) == 0u;
     const bool occl_cull = (K_flags & SF_FLAG_NO_OCCL_CULL) == 0u;
+    // front-first child order (per-ray semantics, with the occlusion cull)
+    const bool front_first = !PACKET && (K_flags & (SF_FLAG_NO_OCCL_CULL | SF_FLAG_NO_FRONT_FIRST)) == 0u;
     SF_STAMP_DECL;
 
     h.minT = FLT_MAX;
@@ -480,7 +487,12 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         else hsm = wave_ballot(__builtin_fminf(__builtin_fminf(tca, R2s - d2), actv) >= 0.0f);   // f0 && in (child loop)
         if (hsm) {
             const float ts = near_root(tca, d2, R2s);
-            const uint64_t accm = hsm & (wave_ballot(ts < h.minT) | (wave_ballot(ts == h.minT) & ancm));
+            const uint64_t eqm = wave_ballot(ts == h.minT);
+            const uint64_t accm = hsm & (wave_ballot(ts < h.minT) | (eqm & ancm));
+            // an exact tie with a best sphere that is not an ancestor: in index order that sphere came first in
+            // the reference's post-order too (rejecting is right); with the front-first order it may not have,
+            // so the caller re-traces the tile in index order (never seen on the BASELINE views)
+            if (front_first && (hsm & eqm & ~ancm) != 0ull) status |= SF_STATUS_TIE;
             sel_in_place(h.minT, ts, accm);
             sel_in_place(h.cx, pc.x, accm);
             sel_in_place(h.cy, pc.y, accm);
@@ -679,7 +691,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 // children of a node at the deepest provisioned level (no table) would need a level that does
                 // not exist: flag the tile for the deeper re-trace instead of entering them
                 if constexpr (!decltype(tab)::value) {
-                    if (pm != 0u) overflowed = true;
+                    if (pm != 0u) status |= SF_STATUS_OVERFLOW;
                     pm = 0u;
                 }
             };
@@ -725,7 +737,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             if (d + 1u < levels) packet_loop(BoolC<true>{});
             else packet_loop(BoolC<false>{});
             if (d + 1u >= levels) {   // (as in the per-ray loop without a table)
-                if (pm != 0u) overflowed = true;
+                if (pm != 0u) status |= SF_STATUS_OVERFLOW;
                 pm = 0u;
             }
         }
@@ -733,14 +745,23 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         // children none of whose own children can pass LOD for any ray (sfhost::leaf_threshold of their depth;
         // |c|^2 of child i is w on lane 31 + i): entered as inline leaves
         leafm = (uint32_t)(wave_ballot(w > leafc) >> 31) & 0x1ffu;
+        // front-first order (per-ray, occlusion cull on): bits 9..17 = the children whose centre lies nearer
+        // than this node's along the cone axis; they are entered first, so their hits cull the far ones more
+        if constexpr (!PACKET) {
+            if (front_first) {
+                const float kp = (pc.x * ax + pc.y * ay) + pc.z * az;
+                leafm |= ((uint32_t)(wave_ballot(ca < kp) >> 31) & 0x1ffu) << 9;
+            }
+        }
         return e;
     };
 
-    // DFS stack in VGPR lanes (lane L = level L): {pending children | cursor << 16}, heap index.
+    // DFS stack in VGPR lanes (lane L = level L): {pending children | leaf and front bits << 9}, heap index.
     // Lane selects: no LDS traffic and no lane-0-only region in the loop.
     uint32_t stk_pc = 0u, stk_ix = 0u;
     uint32_t pend = 0u, eN = 0u;
-    uint32_t leafN = 0u;            // uniform: the open node's children that are inline leaves (bit i: child i)
+    uint32_t leafN = 0u;            // uniform: the open node's children that are inline leaves (bit i: child i),
+                                    // its front children at bits 9..17 (see expand)
     {
         // the root: its own sphere, then -- unless no child of it can pass LOD for any ray
         // (sfhost::leaf_threshold; per-ray semantics only) -- its children
@@ -758,7 +779,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         d = __builtin_amdgcn_readfirstlane(d);
         SF_STAMP(0);
         if (pend) {
-            const uint32_t c = __builtin_ctz(pend);
+            const uint32_t fp = pend & (leafN >> 9);   // front children still pending first
+            const uint32_t c = __builtin_ctz(fp ? fp : pend);
             const uint32_t cbit = 1u << c;
             pend &= ~cbit;
             // (d + 1 < levels here: expand never leaves children pending at the deepest provisioned level)
@@ -805,7 +827,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 continue;
             }
             // save the open node's state, enter child c
-            stk_pc = writelane_u(pend | (leafN << 16), d, stk_pc);
+            stk_pc = writelane_u(pend | (leafN << 9), d, stk_pc);
             stk_ix = writelane_u(idxB, d, stk_ix);
             L.E(d)[lane] = (uint16_t)eN;
             idxB = 9u * (idxB + c) + 1u;
@@ -824,8 +846,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         lds_fence();
         {
             const uint32_t pc = __builtin_amdgcn_readlane(stk_pc, d);
-            pend = pc & 0xffffu;
-            leafN = pc >> 16;
+            pend = pc & 0x1ffu;
+            leafN = pc >> 9;
             idxB = (uint32_t)__builtin_amdgcn_readlane(stk_ix, d);
         }
         eN = L.E(d)[lane];
@@ -1000,10 +1022,16 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
 
     HitState h;
     int32_t maxd = -1;
-    bool overflowed = false;
+    uint32_t status = 0u;
     uint64_t tile_counts = 0;
-    traverse<0, PIPE>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, overflowed, a.flags,
-                    FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
+    // The main kernels enter children front-first (with the occlusion cull); an exact non-ancestor tie under
+    // that order flags the tile like an overflow, and the fixup re-traces it in index order -- the reference's
+    // tie rule (see traverse). The fixup kernel always traces in index order.
+    traverse<0, PIPE>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, status,
+                      FIXUP ? (a.flags | SF_FLAG_NO_FRONT_FIRST) : a.flags,
+                      FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
+    if (!FIXUP && (a.flags & SF_FLAG_DIAG_FORCE_RETRACE)) status |= SF_STATUS_TIE;
+    const bool overflowed = status != 0u;
     pre();
     if (!FIXUP && a.tile_trace) {
         // diagnostics only: never read by the kernel, never feeds an output value. Every lane stores
@@ -1050,7 +1078,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
         }
     }
     if (!FIXUP && overflowed) {
-        // a deeper re-trace (sf_fixup_wave) rewrites this whole tile
+        // a deeper (or index-order) re-trace (sf_fixup_wave) rewrites this whole tile
         const uint32_t slot = wave_fetch_add(overflow_count, 1u);
         overflow_list[slot] = tile;   // uniform value and address
     }
@@ -2029,9 +2057,10 @@ __device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint
 
     HitState h;
     int32_t maxd = -1;
-    bool overflowed = false;
+    uint32_t status = 0u;
     stage_root(lds, a.root);
-    traverse<PW>(K, a.root, lds, levels, dx, dy, dz, valid, h, maxd, overflowed, a.flags);
+    traverse<PW>(K, a.root, lds, levels, dx, dy, dz, valid, h, maxd, status, a.flags);
+    const bool overflowed = (status & SF_STATUS_OVERFLOW) != 0u;
 
     PacketLane out;
     shade(dx, dy, dz, h, K->lut, out.px, out.py, out.pz, out.nx, out.ny, out.nz);

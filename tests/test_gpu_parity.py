@@ -699,3 +699,25 @@ def test_parallel_mt_draws_equal_sequential(sizes, monkeypatch):
     assert np.array_equal(pos.view(np.uint32), epos.view(np.uint32))
     assert np.array_equal(nrm.view(np.uint32), enrm.view(np.uint32))
     assert (st.max_depth, st.closest, st.rays) == (est.max_depth, est.closest, est.rays)
+
+
+@pytest.mark.parametrize("flags", ["0x200", "0x400"])
+@pytest.mark.parametrize("name", ["t3", "c2"])
+def test_front_first_order_and_tie_fallback(name, flags, monkeypatch):
+    """Children entered in index order only (SF_FLAG_NO_FRONT_FIRST), and every tile forced through the tie
+    fallback of the front-first order (SF_FLAG_DIAG_FORCE_RETRACE: the tile is queued like an overflow and
+    sf_fixup_wave re-traces it in index order, its small grid when the levels are proven): golden frames and
+    stats either way."""
+    monkeypatch.setenv("SF_FLAGS", flags)
+    fx = load_frame(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for _ in range(2):
+            s.Render(emit_aux=True)
+            pos, nrm, mint, idx = s.download(aux=True)
+            assert frame_digest(pos, nrm) == fx["frame_digest"], flags
+        st = s.stats()
+    assert st.max_depth == fx["stats"]["max_depth"]
+    assert np.float32(st.closest) == np.float32(float.fromhex(fx["stats"]["closest"]))
+    assert st.overflow_tiles == 0
