@@ -42,8 +42,8 @@ def main():
               f"{ph[6] / it:.2f}; active lanes/expanded node {ph[7] / max(ph[0], 1):.2f}; inline leaf tests "
               f"{ph[8] / per:.0f} with {ph[9] / max(ph[8], 1):.2f} active lanes")
         print(f"  iterations at depth >= 4: {ph[10] / it:.3f} of all, {ph[11] / max(ph[10], 1):.2f} active lanes; "
-              f"iterations with <= 4 / 16 / 32 active lanes: {ph[12] / it:.3f} / {ph[13] / it:.3f} / {ph[14] / it:.3f}; "
-              f"waves {ph[15] / per:.0f}")
+              f"iterations with <= 32 active lanes: {ph[14] / it:.3f}; occlusion-checked entries {ph[13] / per:.0f}, "
+              f"wholly culled {ph[12] / per:.0f}; waves {ph[15] / per:.0f}")
     elif ph.sum() > 0:
         names = {1: "push", 6: "expand: node read + build", 2: "expand: child tests", 3: "head->self",
                  4: "self test", 5: "pop"}

@@ -610,8 +610,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 SF_COUNT(6, __builtin_popcountll(hbm));
                 SF_COUNT(10, d >= 4u ? 1 : 0);
                 SF_COUNT(11, d >= 4u ? __builtin_popcountll(actm) : 0);
-                SF_COUNT(12, __builtin_popcountll(actm) <= 4 ? 1 : 0);
-                SF_COUNT(13, __builtin_popcountll(actm) <= 16 ? 1 : 0);
+                SF_COUNT(12, 0);
+                SF_COUNT(13, 0);
                 SF_COUNT(14, __builtin_popcountll(actm) <= 32 ? 1 : 0);
                 if (hbm == 0ull) {
                     SF_COUNT(2, 1);
@@ -811,6 +811,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                     const float te = depth_consts(K, (uint32_t)maxd + 1u).w;
                     const uint64_t cm = wave_ballot(__builtin_fminf(tca - h.minT, tca - te) > rho);
                     amx = am & ~cm;
+                    SF_COUNT(13, 1);
+                    SF_COUNT(12, amx == 0ull ? 1 : 0);
                     if (amx == 0ull) continue;
                     avx = sel_mask(av, -1.0f, cm);
                 }
