@@ -21,9 +21,11 @@ tail -1 $OUT/bench.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-extras > $OUT/stats.log 2>&1 || { tail -20 $OUT/stats.log; exit 5; }
 cat $(find $OUT/stats -name "*kernel_stats.csv") | head -12
-# timed loop of the default bench: 1 first render + 30 warmup, then 200 timed dispatches of the trace kernel
-python3 $R/scripts/trace_avg.py $(find $OUT/stats -name "*kernel_trace.csv") sf_trace_queue2 200 31 | tee $OUT/trace_avg.txt
 grep '^{' $OUT/stats.log | tail -1 > $OUT/bench_under_rocprof.json
+# timed loop of the default bench: 1 code-object warm-up + 1 first render + 30 warmup + the settle frames,
+# then 200 timed dispatches
+SKIP=$(python3 -c "import json; print(32 + json.load(open('$OUT/bench_under_rocprof.json'))['settle']['frames'])")
+python3 $R/scripts/trace_avg.py $(find $OUT/stats -name "*kernel_trace.csv") sf_trace_queue2 200 $SKIP | tee $OUT/trace_avg.txt
 cd $R
 scripts/prof_pmc.sh $TAG/pmc || exit 6
 python3 scripts/pmc_summary.py --json $OUT/pmc_traffic.json --config "1920x1080 K=0.25 moving" $OUT/pmc/*/ > $OUT/pmc_summary.txt

@@ -3,8 +3,8 @@
 bench run, after its warmup), to compare with bench.py's HIP-event roofline timing.
 Usage: trace_avg.py <run_kernel_trace.csv> <kernel> <N> [<skip>]
   the N dispatches after the first <skip> (default: the last N). The default bench (moving camera) runs
-  1 code-object warm-up render (64x64) + 1 first render + W warmup + S timed + W + S fixed-camera
-  renders: its timed loop is skip = 2 + W."""
+  1 code-object warm-up render (64x64) + 1 first render + W warmup + the settle frames (`settle.frames` of
+  the bench line) + S timed + ... renders: its timed loop is skip = 2 + W + settle frames."""
 import csv
 import sys
 
