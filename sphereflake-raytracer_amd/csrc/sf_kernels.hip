@@ -369,9 +369,25 @@ __device__ __forceinline__ void stage_root(float* __restrict__ Lbase, const floa
 
 // PW: packet width of the semantics (0 per ray, 8 (AVX) or 4 (SSE) frame-less packets); PIPE: the latency
 // variant of the per-ray child loop (small frames, whose heaviest tiles' serial DFS is the frame)
+// This lane's column of the cooperative child build (see traverse): unit child frame bi = lane % 9 (lanes
+// 0..26; centre lanes 31 + i: child i), column bc. Loaded once per wave, before any tile loop: a global load
+// in every traversal would wait (vmcnt, in order on this ISA) for the previous tile's G-buffer stores.
+__device__ __forceinline__ float4 build_column(const DeviceConsts* __restrict__ K)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 0u : 1u + ((lane - 32u) & 7u);
+    const uint32_t bc = lane < 27u ? lane / 9u : 3u;
+    const float4 r = make_float4(K->child[bi][4u * bc + 0u], K->child[bi][4u * bc + 1u], K->child[bi][4u * bc + 2u],
+                                 K->child[bi][4u * bc + 3u]);
+    // retire the loads here (vmcnt(0)): otherwise the wait is placed at the first use inside the traversal,
+    // where it would also wait for every tile's G-buffer stores
+    __builtin_amdgcn_s_waitcnt(0x0f70);
+    return r;
+}
+
 template <int PW, bool PIPE = false>
 __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ Lbase,
-                                         uint32_t levels, float dx, float dy, float dz, bool valid, HitState& h,
+                                         const float4 bcol, uint32_t levels, float dx, float dy, float dz, bool valid, HitState& h,
                                          int32_t& maxd, uint32_t& status, uint32_t K_flags,
                                          uint64_t* phase_sums = nullptr, uint32_t axl = 36u,
                                          uint64_t* tile_counts = nullptr)
@@ -458,9 +474,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
         return wave_ballot(!(tca >= 0.0f && tca * tca >= R2b * (1.0f + 0x1p-6f))) == 0ull;
     };
-    float b[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = K->child[bi][4u * bc + j];
+    const float b[4] = { bcol.x, bcol.y, bcol.z, bcol.w };   // (build_column)
     // where this lane's column goes in a level table: centre lanes (bc = 3) xyz + cc at plane 0, the others
     // xyz in their column plane; the centre lanes' cc store goes to plane 0, the others' to one junk word of
     // the cone block (so both stores are unconditional: no divergent region; one address, no conflict)
@@ -505,18 +519,17 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         }
     };
 
-    // ---- expand the node at `node` (depth d, transform in LDS): build its 9 child transforms into
+    // ---- expand the node with centre/|c|^2 `pc` (depth d, columns in LDS): build its 9 child transforms into
     // table(d), then test the children (depth d+1) for the lanes in `act`. Returns this lane's 9-bit
     // "child expands" vector; *pend = the wave's mask of children some lane expands.
-    // (node: {centre, cc} float4 at node; its columns j = 0..2 (xyz) at col + j * cs: col = node + 4,
+    // (pc: the node's {centre, cc}, read by the caller; its columns j = 0..2 (xyz) at col + j * cs: col = node + 4,
     // cs = 4 for the root image; col = the table's column planes + 3 c, cs = SF_LDS_COLS for child c of a level)
     // (the node's own sphere is tested by the caller when the node is entered, before this)
     // (act: the lanes visiting the node, as a per-lane bool for the packet semantics and as the wave mask actm)
-    auto expand = [&](const float* node, const float* col, uint32_t cs, uint32_t d, bool act, uint64_t actm,
+    auto expand = [&](const float4 pc, const float* col, uint32_t cs, uint32_t d, bool act, uint64_t actm,
                       float actv, uint32_t& pend, uint32_t& leafm) -> uint32_t {
         d = __builtin_amdgcn_readfirstlane(d);   // wave-uniform: depth constants come by scalar loads
         lds_fence();
-        const float4 pc = *reinterpret_cast<const float4*>(node);
         const float3 p0 = *reinterpret_cast<const float3*>(col);
         const float3 p1 = *reinterpret_cast<const float3*>(col + cs);
         const float3 p2 = *reinterpret_cast<const float3*>(col + 2u * cs);
@@ -771,7 +784,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         self_test(pc, 0u, wave_ballot(ex0), av0, 0u, depth_consts(K, 0u).y);
         if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u))) &&
               leaf_front(pc, depth_consts(K, 0u).x)))
-            eN = expand(L.root(), L.root() + 4u, 4u, 0u, ex0, wave_ballot(ex0), av0, pend, leafN);
+            eN = expand(pc, L.root() + 4u, 4u, 0u, ex0, wave_ballot(ex0), av0, pend, leafN);
         else SF_COUNT(4, 1);
     }
 
@@ -789,10 +802,14 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             const float av = a ? __builtin_inff() : -1.0f;
             const float* node = L.table(d) + c * 4u;
             // enter child c: its own sphere first (pre-order, see self_test), in one place for every child
+            maxd = (int32_t)d + 1 > maxd ? (int32_t)d + 1 : maxd;   // Sphereflake.h:157-160
+            // (the cull's scalar loads first, so that they are in flight with the LDS read below)
+            const float cull_r = depth_cull(K, d + 1u);
+            const float cull_t = depth_consts(K, (uint32_t)maxd + 1u).w;
             lds_fence();
             const float4 pc = *reinterpret_cast<const float4*>(node);
             const float4 dc1 = depth_consts(K, d + 1u);
-            maxd = (int32_t)d + 1 > maxd ? (int32_t)d + 1 : maxd;   // Sphereflake.h:157-160
+            if constexpr (!PACKET) __asm__ volatile("" ::"s"(cull_r), "s"(cull_t));   // (issued here, not in the branch)
             // Occlusion cull (per-ray semantics): every sphere of the child's subtree, and every bounding sphere
             // the subtree's LOD tests use, lies in the child's bounding ball (radius R = 2r around c). A lane
             // whose float test of any of them accepts has t >= c.d - rho, rho = R + m (|c| + R), m =
@@ -807,9 +824,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             if constexpr (!PACKET) {
                 if (occl_cull) {
                     const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
-                    const float rho = depth_cull(K, d + 1u) + SF_OCCL_MARGIN * __builtin_amdgcn_sqrtf(pc.w);
-                    const float te = depth_consts(K, (uint32_t)maxd + 1u).w;
-                    const uint64_t cm = wave_ballot(__builtin_fminf(tca - h.minT, tca - te) > rho);
+                    const float rho = cull_r + SF_OCCL_MARGIN * __builtin_amdgcn_sqrtf(pc.w);
+                    const uint64_t cm = wave_ballot(__builtin_fminf(tca - h.minT, tca - cull_t) > rho);
                     amx = am & ~cm;
                     SF_COUNT(13, 1);
                     SF_COUNT(12, amx == 0ull ? 1 : 0);
@@ -835,7 +851,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
             idxB = 9u * (idxB + c) + 1u;
             d += 1u;
             SF_STAMP(1);
-            eN = expand(node, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, a, amx, avx, pend, leafN);
+            eN = expand(pc, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, a, amx, avx, pend, leafN);
             SF_STAMP(2);
             continue;
         }
@@ -1009,7 +1025,7 @@ struct NoPrefetch {
 // its next queue ticket there, so the atomic's round trip overlaps the shading instead of following the
 // G-buffer stores (whose completion a later wait would otherwise include: vmcnt counts in order).
 template <bool FIXUP, bool PIPE = false, class Prefetch = NoPrefetch>
-__device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __restrict__ L, uint32_t tile,
+__device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __restrict__ L, const float4 bcol, uint32_t tile,
                                                 uint32_t levels, uint32_t* overflow_list, uint32_t* overflow_count,
                                                 uint32_t part = 0u, const Prefetch& pre = Prefetch())
 {
@@ -1029,7 +1045,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     // The main kernels enter children front-first (with the occlusion cull); an exact non-ancestor tie under
     // that order flags the tile like an overflow, and the fixup re-traces it in index order -- the reference's
     // tie rule (see traverse). The fixup kernel always traces in index order.
-    traverse<0, PIPE>(K, a.root, L, levels, dx, dy, dz, t.valid, h, maxd, status,
+    traverse<0, PIPE>(K, a.root, L, bcol, levels, dx, dy, dz, t.valid, h, maxd, status,
                       FIXUP ? (a.flags | SF_FLAG_NO_FRONT_FIRST) : a.flags,
                       FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
     if (!FIXUP && (a.flags & SF_FLAG_DIAG_FORCE_RETRACE)) status |= SF_STATUS_TIE;
@@ -1124,7 +1140,7 @@ __device__ __forceinline__ void trace_wave_body(const FrameArgs& a, uint32_t* ov
     if (tile >= a.tiles_x * a.tile_rows) return;
     float* const L = lds + wv * SF_LDS_WAVE_FLOATS(a.max_depth);
     stage_root(L, a.root);
-    const TileStats st = trace_tile<false>(a, L, tile, a.max_depth, overflow_list, overflow_count);
+    const TileStats st = trace_tile<false>(a, L, build_column(a.consts), tile, a.max_depth, overflow_list, overflow_count);
     publish_stats(a, st.maxd, st.closest, 0u);
 }
 
@@ -1180,6 +1196,7 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 #endif
     }
     stage_root(L, a.root);
+    const float4 bcol = build_column(a.consts);
     // One queue per XCD (a.queues of them); a wave drains its own group's queue and then exits. Stealing
     // from the other queues once the own one ran dry cost every wave up to 7 more atomics on queue words
     // contended chip-wide at the end of the frame: the last wave exited ~60 us after the last tile
@@ -1249,7 +1266,7 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
         auto ticket = [&]() {
             first = nwaves + wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u) * nq + k;   // uniform
         };
-        const TileStats st = trace_tile<false, PIPE>(at, L, t, at.max_depth, at.overflow_list, at.counters + at.parity, part,
+        const TileStats st = trace_tile<false, PIPE>(at, L, bcol, t, at.max_depth, at.overflow_list, at.counters + at.parity, part,
                                                ticket);
         if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace) {   // diagnostics only (uniform words)
             uint64_t* ut = at.tile_trace + 3u * (at.tiles_x * at.tile_rows) + SF_DIAG_SLOTS + 3u * g;
@@ -1526,8 +1543,9 @@ extern "C" __global__ __launch_bounds__(64) void sf_fixup_wave(FrameArgs a, cons
     float closest = FLT_MAX;
     uint32_t unresolved = 0u;
     stage_root(lds, a.root);
+    const float4 bcol = build_column(a.consts);
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        const TileStats st = trace_tile<true>(a, lds, overflow_list[i], SF_MAX_LEVELS, nullptr, nullptr);
+        const TileStats st = trace_tile<true>(a, lds, bcol, overflow_list[i], SF_MAX_LEVELS, nullptr, nullptr);
         maxd = st.maxd > maxd ? st.maxd : maxd;
         closest = fminf(closest, st.closest);
         unresolved += st.overflowed ? 1u : 0u;
@@ -2061,7 +2079,7 @@ __device__ __forceinline__ void progressive_trace(const FrameArgs& a, const uint
     int32_t maxd = -1;
     uint32_t status = 0u;
     stage_root(lds, a.root);
-    traverse<PW>(K, a.root, lds, levels, dx, dy, dz, valid, h, maxd, status, a.flags);
+    traverse<PW>(K, a.root, lds, build_column(K), levels, dx, dy, dz, valid, h, maxd, status, a.flags);
     const bool overflowed = (status & SF_STATUS_OVERFLOW) != 0u;
 
     PacketLane out;
