@@ -12,13 +12,14 @@
  * hit index and the max depth agree on every pixel, and counts bounding tests and expansions of both.
  * Built against oracle/sf_oracle.c (included) by scripts/experiments/occl_sim.py.
  */
+#include <stdlib.h>
 #include "../../oracle/sf_oracle.c"
 
 typedef struct {
     const float* child;
     const uint32_t* lut;
     int max_depth;
-    long long tests, interior, culled, ties;
+    long long tests, interior, culled, ties, fast_bad, band, hits;
     float margin;     /* relative margin (x |c|) */
     int mode;         /* 1: lb = tca - rho, 2: lb = tca - sqrt(rho^2 - d2); +4: children front to back */
     float axis[3];    /* mode & 8: children ordered along this direction (the tile's centre ray) for every lane */
@@ -90,6 +91,15 @@ static void intersect_cull(ctrav_t* tv, const float D[3], const float* node_m, h
         tv->tests++;
         float tb;
         if (!ray_sphere(D, Cc, R2b, &tb)) continue;
+        {   /* fast LOD decisions of the kernel (tca < T expands; tca (1 - 2^-8) >= Tfar does not): check */
+            const float Tt = lod_T(rc);
+            const float Tfar = nextafterf((float)((double)Tt + sqrt((double)R2b) * (1.0 + 0x1p-18)), FLT_MAX);
+            const float tca = (Cc[0] * D[0] + Cc[1] * D[1]) + Cc[2] * D[2];
+            if (tca < Tt && !(tb < Tt)) tv->fast_bad++;
+            if (tca * (1.0f - 0x1p-8f) >= Tfar && tb < Tt) tv->fast_bad++;
+            if (!(tca < Tt) && !(tca * (1.0f - 0x1p-8f) >= Tfar)) tv->band++;
+            tv->hits++;
+        }
         int expands = sqrtf(tb / rc) < g_lod_constant || tb < 0.0f;
         /* child's own sphere is tested by the reference even when it does not expand? No: the reference
            returns before the children and the self test when LOD fails (Sphereflake.h:146-153). */
@@ -135,7 +145,7 @@ int sim_rows(uint32_t W, uint32_t H, const float o[3], const float tl[3], const 
              const float root[16], const float child[9 * 16], const uint32_t* lut, uint32_t y0, uint32_t y1,
              float margin, int mode, float* minT, uint32_t* index, long long* stats)
 {
-    ctrav_t tv = { child, lut, 0, 0, 0, 0, 0, margin, mode, {0, 0, 0}, NULL, 0, 0 };
+    ctrav_t tv = { child, lut, 0, 0, 0, 0, 0, 0, 0, 0, margin, mode, {0, 0, 0}, NULL, 0, 0 };
     float fw = (float)W, fh = (float)H;
     float dx_ = tr[0] - tl[0], dy_ = tr[1] - tl[1], dz_ = tr[2] - tl[2];
     float ex_ = bl[0] - tl[0], ey_ = bl[1] - tl[1], ez_ = bl[2] - tl[2];
@@ -163,7 +173,7 @@ int sim_rows(uint32_t W, uint32_t H, const float o[3], const float tl[3], const 
             minT[p] = h.minT;
             index[p] = (uint32_t)h.index;
         }
-    stats[0] = tv.max_depth; stats[1] = tv.tests; stats[2] = tv.interior; stats[3] = tv.culled;
+    stats[0] = tv.max_depth; stats[1] = tv.fast_bad; stats[2] = tv.band; stats[3] = tv.hits;
     return 0;
 }
 
@@ -181,7 +191,7 @@ int sim_tile_row(uint32_t W, uint32_t H, const float o[3], const float tl[3], co
     long long uniq = 0, tests = 0, interior = 0, ties_all = 0;
     for (uint32_t tx = 0; tx < (W + 7) / 8; ++tx) {
         memset(set, 0, (size_t)cap * 8);
-        ctrav_t tv = { child, lut, 0, 0, 0, 0, 0, margin, mode, {0, 0, 0}, set, cap - 1, 0 };
+        ctrav_t tv = { child, lut, 0, 0, 0, 0, 0, 0, 0, 0, margin, mode, {0, 0, 0}, set, cap - 1, 0 };
         {
             float u = (float)(tx * 8 + 4) / fw, v = (float)(ty * 8 + 4) / fh;
             tv.axis[0] = ((tl[0] + dx_ * u) + ex_ * v) - o[0];

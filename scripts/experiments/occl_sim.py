@@ -52,6 +52,7 @@ def run(margin, mode):
 
 
 m0, i0, s0 = run(-1.0, 0)
+print(f"fast LOD decisions: violations {s0[:, 1].sum()}, band lanes {s0[:, 2].sum()} of {s0[:, 3].sum()} bounding hits")
 same_plain = np.array_equal(m0.view(np.uint32), ref["minT"].view(np.uint32)) and np.array_equal(i0, ref["index"])
 print(f"{name} {W}x{H} rows/{step}: pre-order plain == oracle: {same_plain}; max depth {s0[:, 0].max()} "
       f"(oracle {ref['stats']['max_depth']}); tests {s0[:, 1].sum()} expansions {s0[:, 2].sum()}")

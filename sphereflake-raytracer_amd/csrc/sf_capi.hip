@@ -345,7 +345,8 @@ static int upload_consts(sf_ctx* c)
         e[3] = c->host_consts.dt.lod[d];
         e[4] = sfhost::leaf_threshold(&c->host_consts.dt, (uint32_t)d);
         e[5] = std::nextafter((float)(std::sqrt((double)e[0]) * (1.0 + (double)SF_OCCL_MARGIN)), FLT_MAX);
-        e[6] = e[7] = 0.0f;
+        e[6] = std::nextafter((float)((double)e[3] + std::sqrt((double)e[0]) * (1.0 + 0x1p-18)), FLT_MAX);
+        e[7] = 0.0f;
     }
     std::memcpy(c->host_consts.lut, kLut, sizeof kLut);
     sfhost::sobol_matrices(c->host_consts.sobol);

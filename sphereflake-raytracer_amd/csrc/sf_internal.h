@@ -91,9 +91,10 @@ struct DeviceConsts {
     float child[9][16];               // unit child frames, glm column-major (Sphereflake.cpp:216-249)
     DepthTables dt;
     // the same interleaved per depth d, one scalar load: {r2_bound, r2_self, scale, lod,
-    // leaf, cull, 0, 0}; leaf = |c|^2 threshold beyond which no child of a depth-d node centred at c can
+    // leaf, cull, far, 0}; leaf = |c|^2 threshold beyond which no child of a depth-d node centred at c can
     // pass the LOD test for any ray (sfhost::leaf_threshold); cull = 2 r_d (1 + SF_OCCL_MARGIN), rounded
-    // up: the occlusion cull's fattened bounding radius without its |c| term (see traverse)
+    // up: the occlusion cull's fattened bounding radius without its |c| term (see traverse); far =
+    // T_d + 2 r_d (1 + 2^-18), rounded up: a bounding hit with tca (1 - 2^-8) >= far cannot pass LOD
     float depth8[SF_DEPTH_TABLE][8];
     uint32_t lut[2048];               // x86 rsqrtps table (rsqrtps_lut.inc)
     uint32_t sobol[2][52];            // Sobol direction numbers, dims 0 and 1 (Sobol.cpp:34-39, 57-162)

@@ -347,6 +347,18 @@ __device__ __forceinline__ float depth_cull(const DeviceConsts* K, uint32_t d)
 #define SF_STATUS_OVERFLOW 1u
 #define SF_STATUS_TIE 2u
 
+// {.., far} of depth d: T_d + 2 r_d (1 + 2^-18), rounded up (see DeviceConsts::depth8)
+__device__ __forceinline__ float depth_far(const DeviceConsts* K, uint32_t d)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) float* ConstF;
+    typedef const __attribute__((address_space(4))) char* ConstC;
+    return *(ConstF)((ConstC)(const void*)K->depth8 + (d << 5) + 24u);
+#else
+    return reinterpret_cast<const float4*>(K->depth8)[2u * d + 1u].z;
+#endif
+}
+
 // Root transform -> the wave's LDS image in the transform layout (Sphereflake.cpp:83). The same for
 // every tile of a frame: kernels stage it once per wave, before any tile loop.
 __device__ __forceinline__ void stage_root(float* __restrict__ Lbase, const float* root)
@@ -559,6 +571,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         }
         const float R2b = dtc.x;
         const float T = dtc.w;
+        const float Tfar = depth_far(K, d + 1u);
         // Cone cull of child bi (centre c in lanes 31..39): no ray of the wave's cone can hit its bounding
         // sphere. With ca = c.a, q = c - ca a, every lane's angle phi to c is >= alpha - theta, so its
         // line passes at distance |c| sin(phi) >= |q| cosT - ca sinT from c. A float hit
@@ -628,6 +641,20 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                 SF_COUNT(14, __builtin_popcountll(actm) <= 32 ? 1 : 0);
                 if (hbm == 0ull) {
                     SF_COUNT(2, 1);
+                    return;
+                }
+                // Most bounding hits are decided without the root: t = fl(tca - s) <= tca (s >= 0, rounding is
+                // monotone), so tca < T expands. And on a bounding hit s <= 2r (1 + 2^-19) + 2^-9.7 tca (d2 can be
+                // negative by rounding, down to -2^-19.4 |c|^2, |c|^2 <= tca^2 + R2b), so tca (1 - 2^-8) >= T + 2r
+                // (1 + 2^-18) (`Tfar`, rounded up) means t >= T: no expansion. Only lanes in between take the
+                // bracket below (rare: a band of width ~2r + 2^-8 tca around T).
+                const uint64_t nearm = wave_ballot(tca < T);
+                const uint64_t farm = wave_ballot(tca * (1.0f - 0x1p-8f) >= Tfar);
+                if ((hbm & ~(nearm | farm)) == 0ull) {
+                    const uint64_t exf = hbm & nearm;
+                    sel_in_place(e, e | (1u << i), exf);
+                    if (exf != 0ull) pm |= 1u << i;
+                    SF_COUNT(3, exf != 0ull ? 1 : 0);
                     return;
                 }
                 // LOD on t = fl(tca - sqrt_rn(R2b - d2)) (SIMD_AVX.h:260-267; t0 <= t1 picks t1 for
