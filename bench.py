@@ -75,12 +75,19 @@ def parse():
                     help="skip the post-process, transfer, frame-less and c4 sections (profiling runs of the timed loop only)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--check", action="store_true", help="verify the last frame against the oracle rows")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="dist mode with more ranks than GPUs (ranks share devices): every leg but the RCCL gather, "
+                         "which RCCL refuses on a shared device")
+    ap.add_argument("--gather-timeout", type=float, default=GATHER_TIMEOUT_S,
+                    help="seconds the RCCL-gathered leg may take before the line is printed without it")
     return ap.parse_args()
 
 
 DEFAULT_SLOTS = 3                    # frames in flight: 1080p 0.149 / 0.140 / 0.136 / 0.133 ms per frame at 1-4
                                      # (profiles/r3/overlap_1080.txt); 3 keeps the latency at ~3 frames
 
+
+GATHER_TIMEOUT_S = 180.0             # the RCCL-gathered leg (multi-GPU) runs last, under a watchdog
 
 SETTLE_MS = 150.0                    # the shader clock ramps from ~2075 to ~2370 MHz over the first ~60 ms of load
                                      # (profiles/r3/ramp.txt): warm-up lasts at least this long
@@ -450,9 +457,47 @@ class Control:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t[0])
 
+    def combine_stats(self, st):
+        """This rank's sf_stats combined over the ranks in place (max depth max, closest min, rays and overflow
+        tiles summed) -- for a distributed G-buffer made without RCCL communicators."""
+        if not self.dist:
+            return st
+        import torch
+        t = torch.tensor([float(st.max_depth), -float(st.closest)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        u = torch.tensor([int(st.rays), int(st.overflow_tiles)], dtype=torch.int64)
+        self.dist.all_reduce(u, op=self.dist.ReduceOp.SUM)
+        st.max_depth, st.closest = int(t[0]), float(-t[1])
+        st.rays, st.overflow_tiles = int(u[0]), int(u[1])
+        return st
+
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
+
+
+class Watchdog:
+    """Deadline for a leg that may hang (the RCCL gather on a node never seen before): past it, `on_timeout`
+    runs (rank 0 prints the line without that leg) and the process exits 0 -- every rank arms the same deadline,
+    so no rank is left waiting in a collective."""
+
+    def __init__(self, seconds, on_timeout):
+        import threading
+        self._done = threading.Event()
+        self._fire = on_timeout
+        self._t = threading.Thread(target=self._run, args=(seconds,), daemon=True)
+        self._t.start()
+
+    def _run(self, seconds):
+        if not self._done.wait(seconds):
+            try:
+                self._fire()
+            finally:
+                sys.stdout.flush()
+                os._exit(0)
+
+    def cancel(self):
+        self._done.set()
 
 
 def slot_period(steps, slots):
@@ -512,7 +557,9 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
     out["trace_ms"] = float(np.mean(tk)) if tk else None
     out["kernel_samples"] = len(tk)
     out["clock_mhz"] = float(np.median(clk)) if clk else None
-    st = d.stats()   # (collective over the ranks)
+    st = d.stats()   # (collective over the ranks with RCCL communicators; else combined over gloo)
+    if nranks > 1 and ids is None:
+        st = ctl.combine_stats(st)
     if st.overflow_tiles:
         raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
     out["stats"] = st
@@ -556,9 +603,9 @@ def main():
     n = world
     ndev = torch.cuda.device_count()
     gpu = local % max(1, ndev) if world > 1 else 0
-    if args.mode == "dist" and world > 1 and ndev < world:
+    if args.mode == "dist" and world > 1 and ndev < world and not args.rehearse:
         raise SystemExit(f"dist mode needs one GPU per rank (RCCL refuses two ranks on one device): {world} ranks, "
-                         f"{ndev} GPU(s); rehearse with --mode frames")
+                         f"{ndev} GPU(s); rehearse with --rehearse (every leg but the RCCL gather)")
     torch.cuda.set_device(gpu)
     ctl = Control(world, rank)
     dev = torch.device("cuda", gpu)
@@ -586,24 +633,11 @@ def main():
         return
 
     slots = max(1, min(8, args.slots))
-    gathered = None
     if args.mode == "dist":
         # the frame split over the ranks, each rank's bands into its own HBM (the distributed G-buffer)
         r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
                       lambda i: i, fixed=True, latency=True, first=True, settle_ms=args.settle_ms)
         rays_step = width * height
-        if n > 1:   # the same frames also assembled on rank 0: RCCL gather of the packed slabs + unpack
-            rg = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
-                           lambda i: i, latency=True, gather=True, settle_ms=args.settle_ms)
-            rg["dist"].close()
-            gathered = {"value": round(rays_step / rg["t_step"] / 1e6, 2), "frame_ms": round(rg["t_step"] * 1e3, 4),
-                        "frame_latency_ms": round(rg["latency_ms"], 4),
-                        "bytes_per_frame": sum(sf.lib().sf_slab_rows(height, args.band_rows, n, kk)
-                                               for kk in range(1, n)) * width * 16,
-                        "format": "packed float4 (nx, ny, nz, minT) per pixel; rank 0 rebuilds pos = dir * minT",
-                        "transport": "RCCL grouped ncclSend/ncclRecv to rank 0 over xGMI, one communicator per slot",
-                        "note": "every frame complete in rank 0's G-buffer (reference layout): the rate a consumer "
-                                "on rank 0 sees; bound by the peers' links into rank 0"}
     else:   # frames: every rank its own frames (frame i * N + rank), one GPU each, slots in flight
         r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, 1,
                       lambda i: i * n + rank, fixed=True, latency=True, first=True, settle_ms=args.settle_ms)
@@ -724,8 +758,9 @@ def main():
             "build": build,
         }
         if n > 1 and args.mode == "dist":
-            out["gathered_on_rank0"] = gathered
             out["independent_frames"] = indep
+            if args.rehearse:
+                out["config"]["parallelism"] += f" [rehearsal: {n} ranks on {ndev} GPU(s), no RCCL gather]"
         if c4 is not None:
             out["configs"] = {"c4": c4}
         if post is not None:
@@ -748,6 +783,32 @@ def main():
                 out["cpu_baseline"] = cb
             except Exception as e:  # never lose the GPU number over the baseline leg
                 out["cpu_baseline"] = {"error": str(e)}
+
+    # Last, the same frames assembled on rank 0 (RCCL gather of the packed slabs + unpack). It is the only leg
+    # with a data-path collective, so it runs after every other number is in hand, under a watchdog: an RCCL
+    # error is recorded in the line, a hang past --gather-timeout prints the line without it.
+    if n > 1 and args.mode == "dist" and not args.rehearse:
+        if rank == 0:
+            out["gathered_on_rank0"] = {"error": f"not finished within {args.gather_timeout:g} s"}
+        wd = Watchdog(args.gather_timeout, (lambda: print(json.dumps(out), flush=True)) if rank == 0 else (lambda: None))
+        try:
+            rg = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
+                           lambda i: i, latency=True, gather=True, settle_ms=args.settle_ms)
+            rg["dist"].close()
+            gathered = {"value": round(rays_step / rg["t_step"] / 1e6, 2), "frame_ms": round(rg["t_step"] * 1e3, 4),
+                        "frame_latency_ms": round(rg["latency_ms"], 4),
+                        "bytes_per_frame": sum(sf.lib().sf_slab_rows(height, args.band_rows, n, kk)
+                                               for kk in range(1, n)) * width * 16,
+                        "format": "packed float4 (nx, ny, nz, minT) per pixel; rank 0 rebuilds pos = dir * minT",
+                        "transport": "RCCL grouped ncclSend/ncclRecv to rank 0 over xGMI, one communicator per slot",
+                        "note": "every frame complete in rank 0's G-buffer (reference layout): the rate a consumer "
+                                "on rank 0 sees; bound by the peers' links into rank 0"}
+        except Exception as e:   # (an RCCL error on one rank: the others fail or the watchdog ends them)
+            gathered = {"error": f"{type(e).__name__}: {e}"}
+        wd.cancel()
+        if rank == 0:
+            out["gathered_on_rank0"] = gathered
+    if rank == 0:
         print(json.dumps(out), flush=True)
     ctl.close()
 

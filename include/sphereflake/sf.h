@@ -334,15 +334,17 @@ int sf_group_last_hip_error(const sf_group* group);
    others' (sf_unpack_bands) into its G-buffer, bit for bit the single-GPU frame.
    `slots` frames may be in flight: frame i runs on slot i % slots (its own context, stream, communicator and
    buffers), so a frame's trace fills the GPU while the previous frame's heaviest tiles and gather finish.
-   With nranks = 1 there is no communicator (frames in flight on one GPU). Every rank must issue the same calls
-   in the same order (set_view, render, get_stats) with the same views. */
+   Without ids there is no communicator, whatever nranks: frames in flight on one GPU (nranks = 1), or this rank's
+   bands of a distributed G-buffer (sf_dist_render_bands; sf_dist_render returns SF_ESTATE, sf_dist_get_stats this
+   rank's stats alone). Every rank must issue the same calls in the same order (set_view, render, get_stats) with
+   the same views. */
 #define SF_DIST_ID_BYTES 128   /* ncclUniqueId */
 #define SF_DIST_MAX_SLOTS 8
 typedef struct sf_dist sf_dist;
 /* Rank 0 makes one id per slot and hands them to every rank (any channel: MPI, a torch.distributed broadcast). */
 int sf_dist_unique_id(uint8_t id[SF_DIST_ID_BYTES]);
-/* Collective over the ranks (RCCL communicator init per slot). ids: slots x SF_DIST_ID_BYTES (may be NULL when
-   nranks = 1: no communicator at all; with ids a one-rank communicator is made).
+/* Collective over the ranks when ids are given (RCCL communicator init per slot). ids: slots x SF_DIST_ID_BYTES,
+   or NULL: no communicator at all (bands only, see above); nranks = 1 with ids makes a one-rank communicator.
    band_rows: a multiple of 8 (8 = one tile row). */
 int sf_dist_create(int device, uint32_t width, uint32_t height, uint32_t band_rows, int rank, int nranks, int slots,
                    const uint8_t* ids, sf_dist** out);
@@ -352,13 +354,15 @@ sf_ctx* sf_dist_context(sf_dist* dist, int slot);     /* slot's context; on rank
 int sf_dist_last_slot(const sf_dist* dist);           /* slot of the last frame issued (SF_ESTATE before any) */
 int sf_dist_set_view(sf_dist* dist, const float origin[3], const float top_left[3], const float top_right[3],
                      const float bottom_left[3]);     /* the view of the next frames */
-int sf_dist_render(sf_dist* dist);                    /* one frame, asynchronous (this rank's share + gather) */
+int sf_dist_render(sf_dist* dist);                    /* one frame, asynchronous (this rank's share + gather;
+                                                         SF_ESTATE for nranks > 1 without communicators) */
 /* One frame as a distributed G-buffer: this rank's bands into its slot's G-buffer at frame positions (reference
    layout), no gather -- every rank holds its own rows in its own HBM. Asynchronous; no collective. */
 int sf_dist_render_bands(sf_dist* dist);
 int sf_dist_synchronize(sf_dist* dist);               /* every slot of this rank done */
 int sf_dist_download(sf_dist* dist, float* pos4, float* nrm4);   /* rank 0: D2H of the last frame (synchronises) */
-int sf_dist_get_stats(sf_dist* dist, sf_stats* out);  /* collective: over slots and ranks (synchronises) */
+int sf_dist_get_stats(sf_dist* dist, sf_stats* out);  /* over slots, and over ranks when made with ids
+                                                         (then collective); synchronises */
 int sf_dist_reset_stats(sf_dist* dist);
 int sf_dist_last_error(const sf_dist* dist, int* hip_error, int* rccl_error);
 

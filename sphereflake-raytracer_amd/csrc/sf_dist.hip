@@ -15,7 +15,8 @@
 // i % slots. A frame's persistent trace grid then fills the wave slots the previous frame's heaviest tiles
 // leave idle, and its trace overlaps the previous frame's gather. Every slot has its own communicator, so
 // operations of different slots never share one; all ranks issue frames in the same order.
-// With nranks = 1 there is no communicator unless ids are given: the slots alone (frames in flight on one GPU).
+// Without ids there is no communicator (any nranks): the slots alone -- frames in flight on one GPU, or this rank's
+// bands of a distributed G-buffer (sf_dist_render_bands, no collective; sf_dist_render then refuses).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -108,7 +109,7 @@ extern "C" int sf_dist_create(int device, uint32_t width, uint32_t height, uint3
                               int slots, const uint8_t* ids, sf_dist** out)
 {
     if (!out || width == 0 || height == 0 || nranks < 1 || rank < 0 || rank >= nranks || slots < 1 ||
-        slots > SF_DIST_MAX_SLOTS || band_rows == 0 || band_rows % 8 != 0 || (nranks > 1 && !ids))
+        slots > SF_DIST_MAX_SLOTS || band_rows == 0 || band_rows % 8 != 0)
         return SF_EINVAL;
     *out = nullptr;
     sf_dist* d = new (std::nothrow) sf_dist();
@@ -189,6 +190,7 @@ extern "C" int sf_dist_render(sf_dist* d)
     if (!d) return SF_EINVAL;
     const uint32_t n = (uint32_t)d->nranks, W = d->W;
     auto& s = d->slot[d->frames % d->slot.size()];
+    if (n > 1 && !s.comm) return SF_ESTATE;   // made without ids: bands only (sf_dist_render_bands)
     hipStream_t st = (hipStream_t)sf_context_stream(s.ctx);
     sf_render_params p;
     std::memset(&p, 0, sizeof p);
@@ -258,7 +260,8 @@ extern "C" int sf_dist_download(sf_dist* d, float* pos4, float* nrm4)
     return sf_download(d->slot[(d->frames - 1) % d->slot.size()].ctx, pos4, nrm4, nullptr, nullptr);
 }
 
-// Collective: every rank calls it. Stats of this rank's slots combined, then over the ranks on the device
+// Collective when the dist has communicators (every rank calls it; without ids: this rank's slots only, the caller
+// combines the ranks). Stats of this rank's slots combined, then over the ranks on the device
 // (max depth max, closest min, rays and overflow tiles summed: Sphereflake.h:30-58 over the whole frame).
 extern "C" int sf_dist_get_stats(sf_dist* d, sf_stats* out)
 {

@@ -801,7 +801,8 @@ def dist_unique_id() -> bytes:
 class SphereflakeDist:
     """One process per GPU (sf_dist_*): this rank's share of every frame (interleaved
     `band_rows`-row bands), gathered to rank 0 over RCCL as packed slabs; `slots` frames in flight. `ids`:
-    slots x 128 bytes of dist_unique_id() from rank 0 (None when nranks = 1)."""
+    slots x 128 bytes of dist_unique_id() from rank 0, or None: no communicator (nranks = 1, or this rank's bands
+    of a distributed G-buffer via RenderBands only -- Render then raises SF_ESTATE)."""
 
     def __init__(self, device: int, width: int, height: int, rank: int = 0, nranks: int = 1, slots: int = 2,
                  ids: bytes | None = None, band_rows: int = 8):
@@ -883,7 +884,8 @@ class SphereflakeDist:
         return pos, nrm
 
     def stats(self) -> sf_stats:
-        """Collective over the ranks."""
+        """Over this rank's slots, and over the ranks when made with ids (then collective: every rank calls it);
+        without ids the caller combines the ranks' stats."""
         s = sf_stats()
         self._check(lib().sf_dist_get_stats(self._d, ctypes.byref(s)), "sf_dist_get_stats")
         return s

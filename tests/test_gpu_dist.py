@@ -118,3 +118,38 @@ def test_dist_render_bands_one_rank_is_the_frame():
         for slot in (0, 1):
             pos, nrm = d.download_slot(slot)
             assert frame_digest(pos, nrm) == fx["frame_digest"], slot
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_dist_bands_without_communicators(n):
+    """nranks > 1 made without ids (no RCCL: the multi-GPU bench's `value` leg): rank k's RenderBands writes the
+    bands b = k (mod n) of each frame into its slot G-buffer at frame positions; the ranks' bands together are the
+    golden frame bit for bit, the per-rank stats sum to one frame's rays, and the gathering Render refuses
+    (SF_ESTATE). Ranks here are n objects on device 0 (the driver's 8-GPU node puts each on its own GPU)."""
+    fx = load_frame("c2")
+    W, H, K, band = fx["W"], fx["H"], float.fromhex(fx["K"]), 8
+    owner = (np.arange(H) // band) % n
+    ranks = [sf.SphereflakeDist(0, W, H, rank=k, nranks=n, slots=2, band_rows=band) for k in range(n)]
+    try:
+        pos = np.full((H, W, 4), np.nan, np.float32)
+        nrm = pos.copy()
+        rays = 0
+        for k, d in enumerate(ranks):
+            d.SetCamera(sf.config_camera(W, H, K))
+            d.reset_stats()
+            for _ in range(2):   # row-major, then the heavy-first order of the rank's own bands
+                d.RenderBands()
+            d.Synchronize()
+            p, q = d.download_slot(1)
+            pos[owner == k], nrm[owner == k] = p[owner == k], q[owner == k]
+            st = d.stats()
+            rays += st.rays
+            assert st.max_depth <= fx["stats"]["max_depth"]
+            with pytest.raises(sf.SphereflakeError) as e:
+                d.Render()
+            assert e.value.code == sf.SF_ESTATE
+        assert frame_digest(pos, nrm) == fx["frame_digest"]
+        assert rays == 2 * W * H
+    finally:
+        for d in ranks:
+            d.close()
