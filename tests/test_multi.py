@@ -12,7 +12,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import load_frame, load_npz
+from conftest import REPO, load_frame, load_npz
 from sphereflake_amd import shard
 
 
@@ -170,3 +170,56 @@ def test_dist_ids_reach_every_rank(world, slots):
     assert all(v == first for v in got.values())
     chunks = {first[k * 128:(k + 1) * 128] for k in range(slots)}
     assert len(chunks) == slots
+
+
+def _stats_worker(rank, world, port, errq, outq):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        import bench
+        import sphereflake_amd as sf
+        ctl = bench.Control(world, rank)
+        st = sf.sf_stats()
+        st.max_depth, st.closest, st.rays, st.overflow_tiles = 5 + rank, 1.5 - 0.25 * rank, 1000 * (rank + 1), rank
+        got = ctl.combine_stats(st)
+        outq.put((rank, got.max_depth, float(got.closest), int(got.rays), int(got.overflow_tiles), ctl.max(rank * 0.5)))
+        ctl.close()
+    except BaseException as e:
+        errq.put(f"rank {rank}: {type(e).__name__}: {e}")
+        raise
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_control_combines_rank_stats(world):
+    """The multi-GPU bench's value leg renders without RCCL communicators, so each rank's sf_stats are combined
+    over the gloo control plane (bench.Control.combine_stats): max depth max, closest min, rays and overflow tiles
+    summed -- the same reduction sf_dist_get_stats does over RCCL; the timed region is the max over ranks."""
+    ctx = mp.get_context("spawn")
+    errq, outq = ctx.SimpleQueue(), ctx.SimpleQueue()
+    mp.start_processes(_stats_worker, args=(world, _free_port(), errq, outq), nprocs=world, start_method="spawn",
+                       join=True)
+    assert errq.empty(), errq.get()
+    got = [outq.get() for _ in range(world)]
+    for _, md, cl, rays, ovf, tmax in got:
+        assert md == 5 + world - 1
+        assert cl == 1.5 - 0.25 * (world - 1)
+        assert rays == 1000 * world * (world + 1) // 2
+        assert ovf == world * (world - 1) // 2
+        assert tmax == 0.5 * (world - 1)
+
+
+def test_bench_watchdog_prints_line_and_exits():
+    """A leg past its deadline (the RCCL gather hanging on an unseen node): the watchdog runs its callback (rank 0
+    prints the line without that leg) and ends the process with status 0."""
+    import subprocess
+    import sys
+    code = ("import sys, time; sys.path.insert(0, %r); import bench\n"
+            "bench.Watchdog(0.5, lambda: print('LINE', flush=True))\n"
+            "time.sleep(30)\nprint('NOT REACHED')\n") % REPO
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "LINE"
+    code2 = ("import sys, time; sys.path.insert(0, %r); import bench\n"
+             "w = bench.Watchdog(1.0, lambda: print('LINE', flush=True))\nw.cancel()\ntime.sleep(1.5)\n"
+             "print('DONE')\n") % REPO
+    r = subprocess.run([sys.executable, "-c", code2], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip() == "DONE", r.stderr
