@@ -23,6 +23,7 @@ typedef struct {
     float margin;     /* relative margin (x |c|) */
     int mode;         /* 1: lb = tca - rho, 2: lb = tca - sqrt(rho^2 - d2); +4: children front to back */
     float axis[3];    /* mode & 8: children ordered along this direction (the tile's centre ray) for every lane */
+    float seed;       /* mode & 32: cull bound min(minT, seed) */
     uint64_t* set;    /* per-tile set of expanded heap indices (open addressing, 0 = empty: stores idx + 1) */
     uint32_t set_mask;
     long long uniq;
@@ -119,7 +120,8 @@ static void intersect_cull(ctrav_t* tv, const float D[3], const float* node_m, h
                 lb = tca - sqrtf(a > 0.0f ? a : 0.0f) - M;
             }
             float Tn = lod_T(1.0f / powf(3.0f, (float)(tv->max_depth + 1)));
-            if (lb > h->minT && lb >= Tn && lb >= 0.0f) {
+            float mb = h->minT; if ((tv->mode & 32) && tv->seed < mb) mb = tv->seed;
+            if (lb > mb && lb >= Tn && lb >= 0.0f) {
                 tv->culled++;
                 continue;
             }
@@ -145,7 +147,7 @@ int sim_rows(uint32_t W, uint32_t H, const float o[3], const float tl[3], const 
              const float root[16], const float child[9 * 16], const uint32_t* lut, uint32_t y0, uint32_t y1,
              float margin, int mode, float* minT, uint32_t* index, long long* stats)
 {
-    ctrav_t tv = { child, lut, 0, 0, 0, 0, 0, 0, 0, 0, margin, mode, {0, 0, 0}, NULL, 0, 0 };
+    ctrav_t tv = { child, lut, 0, 0, 0, 0, 0, 0, 0, 0, margin, mode, {0, 0, 0}, 0.0f, NULL, 0, 0 };
     float fw = (float)W, fh = (float)H;
     float dx_ = tr[0] - tl[0], dy_ = tr[1] - tl[1], dz_ = tr[2] - tl[2];
     float ex_ = bl[0] - tl[0], ey_ = bl[1] - tl[1], ez_ = bl[2] - tl[2];
@@ -191,7 +193,7 @@ int sim_tile_row(uint32_t W, uint32_t H, const float o[3], const float tl[3], co
     long long uniq = 0, tests = 0, interior = 0, ties_all = 0;
     for (uint32_t tx = 0; tx < (W + 7) / 8; ++tx) {
         memset(set, 0, (size_t)cap * 8);
-        ctrav_t tv = { child, lut, 0, 0, 0, 0, 0, 0, 0, 0, margin, mode, {0, 0, 0}, set, cap - 1, 0 };
+        ctrav_t tv = { child, lut, 0, 0, 0, 0, 0, 0, 0, 0, margin, mode, {0, 0, 0}, 0.0f, set, cap - 1, 0 };
         {
             float u = (float)(tx * 8 + 4) / fw, v = (float)(ty * 8 + 4) / fh;
             tv.axis[0] = ((tl[0] + dx_ * u) + ex_ * v) - o[0];
@@ -210,6 +212,16 @@ int sim_tile_row(uint32_t W, uint32_t H, const float o[3], const float tl[3], co
                 h.minT = FLT_MAX; h.index = 0xffffffffu; h.depth = -1;
                 const float* C = root + 12;
                 float tb;
+                if (mode & 32) {
+                    ctrav_t t2 = { child, lut, 0, 0, 0, 0, 0, 0, 0, 0, -1.0f, 0, {0, 0, 0}, 0.0f, NULL, 0, 0 };
+                    hit_t h2; h2.minT = FLT_MAX; h2.index = 0xffffffffu; h2.depth = -1;
+                    if (ray_sphere(D, C, 4.0f, &tb) && (sqrtf(tb) < g_lod_constant || tb < 0.0f)) {
+                        float ts;
+                        if (ray_sphere(D, C, 1.0f, &ts) && ts < h2.minT) { h2.minT = ts; h2.index = 0; h2.depth = 0; }
+                        intersect_cull(&t2, D, root, &h2, 1.0f, 0, 0);
+                    }
+                    tv.seed = h2.minT;
+                }
                 if (ray_sphere(D, C, 4.0f, &tb) && (sqrtf(tb) < g_lod_constant || tb < 0.0f)) {
                     float ts;
                     if (ray_sphere(D, C, 1.0f, &ts) && ts < h.minT) { h.minT = ts; h.index = 0; h.depth = 0; }

@@ -82,6 +82,6 @@ def tiles(margin, mode):
 
 t0 = tiles(-1.0, 0)
 print(f"tiles (every {max(1, step // 2)}th tile row): wave expansions (union over the tile) {t0[0]}, per-lane {t0[1]}")
-for mode, lg in ((1, 7), (9, 7), (17, 7)):
+for mode, lg in ((17, 7), (17, 8.415), (17, 9)):
     t = tiles(2.0 ** -lg, mode)
     print(f"  mode {mode} margin 2^-{lg}: wave expansions {t[0] / t0[0]:.3f}  per-lane {t[1] / t0[1]:.3f}  non-ancestor ties {t[2]}")

@@ -12,8 +12,12 @@
 
 #define SF_DEPTH_TABLE 33      // depths 0..32 (SF_MAX_DEPTH_LIMIT)
 // relative margin of the occlusion cull: a subtree's bounding ball (radius R around c) is fattened to
-// R + SF_OCCL_MARGIN (|c| + R), about 4.6x the worst-case rounding of the float tests inside it
-#define SF_OCCL_MARGIN 0x1p-7f
+// R + SF_OCCL_MARGIN (|c| + R). The float tests inside it can start at most sqrt(28 u) (|c| + R) = 2^-9.6 (|c| + R)
+// (u = 2^-24; the d2 cancellation, tca and |d| != 1) plus ~25 u (|c| + R) before the ball:
+// 3 x 2^-10 is 2.2x that (round 3 started at 2^-7; the wider margin culls fewer deep subtrees)
+#ifndef SF_OCCL_MARGIN
+#define SF_OCCL_MARGIN 0x1.8p-9f
+#endif
 #define SF_TILE 8              // a wave64 traces one 8x8 pixel tile
 #define SF_WAVES_PER_BLOCK 4   // 256-thread workgroups (per-ray kernel)
 #ifndef SF_WAVES_PER_EU
