@@ -159,6 +159,23 @@ __device__ __forceinline__ void sel_in_place(uint32_t& dst, uint32_t src, uint64
     __asm__("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(dst) : "v"(src), "s"(m));
 }
 
+// Near root with sqrt_rn(x) for x = R2 - d2 >= 2^-96 (finite): the hardware estimate and its +-1 ulp correction
+// by two fma residuals -- the sequence the compiler emits for a correctly rounded sqrtf, without the scaling of
+// tiny arguments and the zero/inf class fix-up that x >= 2^-96 never needs, so bit for bit its result there.
+__device__ __forceinline__ float near_root_big(float tca, float x)
+{
+    const float s0 = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __uint_as_float(__float_as_uint(s0) - 1u);
+    const float sup = __uint_as_float(__float_as_uint(s0) + 1u);
+    const float rdn = __builtin_fmaf(-sdn, s0, x);
+    const float rup = __builtin_fmaf(-sup, s0, x);
+    float thc = rdn <= 0.0f ? sdn : s0;
+    thc = rup > 0.0f ? sup : thc;
+    const float t0 = tca + thc;
+    const float t1 = tca - thc;
+    return (t0 <= t1) ? t0 : t1;
+}
+
 // Exact near root for the rare undecided lanes of the LOD bracket. Inlined: its uniform branch stays a
 // real branch (the structurizer leaves wave-uniform regions alone), and without a call no SGPRs are saved
 // around it (round 1 kept it out of line so it would not be if-converted into every child test).
@@ -512,7 +529,15 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         if constexpr (PACKET) hsm = actm & wave_ballot(group_any<PW>(f0) && group_any<PW>(in));
         else hsm = wave_ballot(__builtin_fminf(__builtin_fminf(tca, R2s - d2), actv) >= 0.0f);   // f0 && in (child loop)
         if (hsm) {
+#ifndef SF_NO_FAST_SQRT
+            // (the general correctly rounded path only when a hitting lane's argument is tiny: a uniform branch)
+            const float xs = R2s - d2;
+            float ts;
+            if ((wave_ballot(!(xs >= 0x1p-96f)) & hsm) != 0ull) ts = near_root_exact(tca, d2, R2s);
+            else ts = near_root_big(tca, xs);
+#else
             const float ts = near_root(tca, d2, R2s);
+#endif
             const uint64_t eqm = wave_ballot(ts == h.minT);
             const uint64_t accm = hsm & (wave_ballot(ts < h.minT) | (eqm & ancm));
             // an exact tie with a best sphere that is not an ancestor: in index order that sphere came first in
@@ -583,6 +608,19 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         const float ax = cn.x, ay = cn.y, az = cn.z, cosT = cn.w;
         const float dl = w * 0x1p-18f;
         const float ca = (x * ax + y * ay) + z * az;
+#ifndef SF_OLD_CONE
+        // In squares, with |q| from |c|^2 - ca^2 (no q vector, one hardware sqrt): X = |q| cosT - ca sinT bounds
+        // |c| sin(phi) from below; skip when X > 0 and X^2 > R^2 + dl + 2^-19 |c|^2. The added 32 u |c|^2 covers
+        // this test's own rounding: |q|^2 = |c|^2 - ca^2 is off by <= 10 u |c|^2 (cancellation), which moves X^2 by
+        // <= 2 X dq <= 10 u |c|^2; the sqrt, X and X^2 add <= 7 u |c|^2. (w - ca^2 clamped at 0: no NaN, which
+        // the min below would drop.)
+        const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaxf(w - ca * ca, 0.0f));
+        const float X = sq * cosT - ca * sinT;
+        const float Y = X * X - (R2b + w * (0x1p-18f + 0x1p-19f));
+        // skip = ca > 0 && w > 2 (R2b + dl) && X > 0 && Y > 0, as compares of a v_min3 and a v_min (with
+        // denormals kept, a > b exactly when fl(a - b) > 0; every operand is finite): the kept children from a ballot
+        const float mk = __builtin_fminf(__builtin_fminf(ca, w - 2.0f * (R2b + dl)), __builtin_fminf(X, Y));
+#else
         const float qx = x - ca * ax, qy = y - ca * ay, qz = z - ca * az;
         const float sq = __builtin_amdgcn_sqrtf((qx * qx + qy * qy) + qz * qz);
         const float lhs = sq * cosT - ca * sinT;
@@ -590,6 +628,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         // skip = ca > 0 && w > 2 (R2b + dl) && lhs > rhs, as ONE compare of a v_min3 (with denormals kept,
         // a > b exactly when fl(a - b) > 0; every operand is finite): the kept children straight from a ballot
         const float mk = __builtin_fminf(__builtin_fminf(ca, w - 2.0f * (R2b + dl)), lhs - rhs);
+#endif
         uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 31) & 0x1ffu;
         M = __builtin_amdgcn_readfirstlane(M);
         SF_STAMP(6);
