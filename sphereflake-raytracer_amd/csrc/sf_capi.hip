@@ -81,9 +81,9 @@ namespace {
 
 constexpr uint32_t kDefaultLevels = 12;   // depths 0..11 expand; every BASELINE camera stays <= 10
 // parallel mt19937 draws (sf_mtjump.cpp, sf_kernels.hip): from this many draws per call, in K <= kMtSegMax
-// segments of >= kMtSegMin draws, each jumped to by a convolution split over SF_MT_PARTS (8) workgroups
+// segments of >= kMtSegMin draws, each jumped to by a convolution split over SF_MT_PARTS workgroups
 constexpr uint32_t kMtParMin = 32768, kMtSegMin = 8192, kMtSegMax = 32;
-constexpr uint32_t kMtParts = 8, kMtRawBlocks = 33;   // raw words x_0..x_20559 (19937 + 623 + 1)
+constexpr uint32_t kMtParts = SF_MT_PARTS, kMtRawBlocks = 33;   // raw words x_0..x_20559 (19937 + 623 + 1)
 
 struct DevGuard {
     int prev = -1;
@@ -156,6 +156,11 @@ struct sf_ctx {
     // generated on pf_stream while this batch traces -- the generator is one sequential workgroup.
     // A call that does not continue the stream restores the state saved before the prefetch.
     uint32_t* draws_pf = nullptr;      // the prefetched draws (prog_cap x 2)
+    // ... and, where the batch is binned in index order, its binned trace order (the bins depend on the draws,
+    // the Sobol index and the frame size only, not on the view): the next batch starts with its trace
+    uint32_t* perm_pf = nullptr;       // prog_cap
+    uint32_t* bin_cnt_pf = nullptr;    // SF_PROG_MAX_BINS
+    uint32_t pf_bin_pl = 0;            // packet lanes the prefetched order was binned for (0: not binned)
     uint32_t* mt_saved = nullptr;      // MT state before the pending prefetch
     hipStream_t pf_stream = nullptr;
     hipEvent_t pf_done = nullptr;      // prefetch written (pf_stream)
@@ -163,6 +168,7 @@ struct sf_ctx {
     hipEvent_t traced = nullptr;       // the last batch's trace done reading its draws
     // parallel draws (env SF_MT_PARALLEL=0: the single-workgroup generator only)
     bool mt_parallel = true;
+    uint32_t mt_seg_max = kMtSegMax;   // env SF_MT_SEGMENTS: at most this many segments per call (2..kMtSegMax)
     uint32_t* mt_raw = nullptr;        // kMtRawBlocks x 624 raw words from the state's buffer
     uint32_t* mt_partial = nullptr;    // (kMtSegMax - 1) x kMtParts partial windows
     uint32_t* mt_state2 = nullptr;     // the state after the batch (copied back into mt_state)
@@ -301,6 +307,8 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->prog_ovf);
     (void)hipFree(c->prog_ovf_cnt);
     (void)hipFree(c->draws_pf);
+    (void)hipFree(c->perm_pf);
+    (void)hipFree(c->bin_cnt_pf);
     (void)hipFree(c->mt_saved);
     (void)hipFree(c->mt_raw);
     (void)hipFree(c->mt_partial);
@@ -445,6 +453,10 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if (const char* ev = std::getenv("SF_PROG_ADAPT")) c->prog_adapt = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_ORDER")) c->prog_order = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_MT_PARALLEL")) c->mt_parallel = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_MT_SEGMENTS")) {
+        const int k = std::atoi(ev);
+        c->mt_seg_max = k < 2 ? 2u : k > (int)kMtSegMax ? kMtSegMax : (uint32_t)k;
+    }
     if (const char* ev = std::getenv("SF_SPLIT_BUCKETS"))
         c->split_buckets = std::strcmp(ev, "model") == 0 ? SF_SPLIT_MODEL : (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_SPLIT_PARTS")) c->split_parts = std::atoi(ev) == 4 ? 4u : 2u;
@@ -826,7 +838,7 @@ static int gen_draws(sf_ctx* c, hipStream_t s, uint32_t* out, uint32_t n)
         return SF_OK;
     }
     uint32_t K = n / kMtSegMin;
-    K = K < 2u ? 2u : K > kMtSegMax ? kMtSegMax : K;
+    K = K < 2u ? 2u : K > c->mt_seg_max ? c->mt_seg_max : K;
     const uint32_t L = (n + K - 1u) / K;
     const uint32_t pw = (uint32_t)sfhost::mt_poly_words();
     if (!c->mt_raw) {
@@ -847,6 +859,34 @@ static int gen_draws(sf_ctx* c, hipStream_t s, uint32_t* out, uint32_t n)
                        (const uint32_t*)c->mt_partial, L, n, out, c->mt_state2);
     SF_HIP(c, hipGetLastError());
     SF_HIP(c, hipMemcpyAsync(c->mt_state, c->mt_state2, 625 * 4, hipMemcpyDeviceToDevice, s));
+    return SF_OK;
+}
+
+// Packet bins of a frame-less batch: squares of 2^shift pixels, about 8 packets per bin (a wave's worth of AVX
+// packets), at most SF_PROG_MAX_BINS.
+static void bin_geometry(const sf_ctx* c, uint32_t packets, uint32_t& shift, uint32_t& bx, uint32_t& by)
+{
+    for (shift = 2u;; ++shift) {
+        bx = (c->W + (1u << shift) - 1u) >> shift;
+        by = (c->H + (1u << shift) - 1u) >> shift;
+        const uint64_t nb = (uint64_t)bx * by;
+        if (nb <= SF_PROG_MAX_BINS && 8ull * nb <= packets) break;
+        if (shift == 30u) break;
+    }
+}
+
+// Binned trace order of `packets` packets (counting sort by bin, index order of the bins) into perm, on stream s.
+static int bin_packets(sf_ctx* c, hipStream_t s, const FrameArgs& a, const uint32_t* draws, uint64_t counter0,
+                       uint32_t packets, uint32_t pl, uint32_t* cnt, uint32_t* perm)
+{
+    uint32_t shift, bx, by;
+    bin_geometry(c, packets, shift, bx, by);
+    const uint32_t nbins = bx * by, pb = (packets + 255u) / 256u;
+    SF_HIP(c, hipMemsetAsync(cnt, 0, (size_t)nbins * 4, s));
+    hipLaunchKernelGGL(sf_packet_bin, dim3(pb), dim3(256), 0, s, a, draws, counter0, packets, pl, shift, bx, cnt);
+    hipLaunchKernelGGL(sf_packet_scan, dim3(1), dim3(1024), 0, s, cnt, nbins, (const uint32_t*)nullptr);
+    hipLaunchKernelGGL(sf_packet_place, dim3(pb), dim3(256), 0, s, a, draws, counter0, packets, pl, shift, bx, cnt, perm);
+    SF_HIP(c, hipGetLastError());
     return SF_OK;
 }
 
@@ -872,12 +912,17 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
         SF_HIP(c, hipMemsetAsync(c->owner, 0, (size_t)c->W * c->H * 8, s));
     }
     // a pending prefetch either is this batch's draws, or is undone (MT state restored)
-    bool prefetched = false;
+    bool prefetched = false, prebinned = false;
+    const bool binned = c->prog_bin && packets >= SF_PROG_BIN_MIN;
     if (c->pf_packets) {
         SF_HIP(c, hipStreamWaitEvent(s, c->pf_done, 0));
         if (c->pf_packets == packets && c->prog_seeded && seed == c->prog_seed && counter0 == c->prog_next) {
             std::swap(c->draws, c->draws_pf);
             prefetched = true;
+            if (binned && !c->prog_order && c->pf_bin_pl == pl) {
+                std::swap(c->perm, c->perm_pf);
+                prebinned = true;
+            }
         } else {
             SF_HIP(c, hipMemcpyAsync(c->mt_state, c->mt_saved, 625 * 4, hipMemcpyDeviceToDevice, s));
         }
@@ -889,6 +934,8 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
         (void)hipFree(c->draws_pf);
         (void)hipFree(c->lanes);
         (void)hipFree(c->perm);
+        (void)hipFree(c->perm_pf);
+        c->perm_pf = nullptr;
         (void)hipFree(c->prog_ovf);
         c->draws = c->draws_pf = nullptr;
         c->lanes = nullptr;
@@ -936,22 +983,28 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
         if (c->traced_valid) SF_HIP(c, hipStreamWaitEvent(c->pf_stream, c->traced, 0));   // draws_pf free
         SF_HIP(c, hipMemcpyAsync(c->mt_saved, c->mt_state, 625 * 4, hipMemcpyDeviceToDevice, c->pf_stream));
         if (int rc = gen_draws(c, c->pf_stream, c->draws_pf, 2 * packets)) return rc;
+        // the next batch's binned order too (index-ordered bins only: a cost-ranked order needs this batch's costs)
+        c->pf_bin_pl = 0;
+        if (binned && !c->prog_order) {
+            if (!c->perm_pf) SF_HIP(c, hipMalloc(&c->perm_pf, (size_t)c->prog_cap * 4));
+            if (!c->bin_cnt_pf) SF_HIP(c, hipMalloc(&c->bin_cnt_pf, SF_PROG_MAX_BINS * 4));
+            if (int rc = bin_packets(c, c->pf_stream, a, c->draws_pf, counter0 + packets, packets, pl, c->bin_cnt_pf,
+                                     c->perm_pf))
+                return rc;
+            c->pf_bin_pl = pl;
+        }
         SF_HIP(c, hipEventRecord(c->pf_done, c->pf_stream));
         c->pf_packets = packets;
     }
     // Trace order: packets binned by a square of 2^shift pixels (about 8 per bin, a wave's worth of
     // AVX packets), so a wave's packets share their traversal. Small batches: draw order.
     const uint32_t* perm = nullptr;
-    if (c->prog_bin && packets >= SF_PROG_BIN_MIN) {
+    if (prebinned) {   // (binned on pf_stream with the draws)
+        perm = c->perm;
+    } else if (binned) {
         if (!c->bin_cnt) SF_HIP(c, hipMalloc(&c->bin_cnt, SF_PROG_MAX_BINS * 4));
-        uint32_t shift = 2u, bx = 0, by = 0;
-        for (;; ++shift) {
-            bx = (c->W + (1u << shift) - 1u) >> shift;
-            by = (c->H + (1u << shift) - 1u) >> shift;
-            const uint64_t nb = (uint64_t)bx * by;
-            if (nb <= SF_PROG_MAX_BINS && 8ull * nb <= packets) break;
-            if (shift == 30u) break;
-        }
+        uint32_t shift, bx, by;
+        bin_geometry(c, packets, shift, bx, by);
         const uint32_t nbins = bx * by;
         const uint32_t pb = (packets + 255u) / 256u;
         // Heavy-first: bins ranked by the cycles their waves took in the previous batch of the same

@@ -177,6 +177,9 @@ struct PostArgs {
 #define SF_PROGRESSIVE_LEVELS 16        // frame-less mode: LDS traversal levels
 #endif
 #define SF_PROG_FIXUP_BLOCKS 256u      // grid of sf_progressive_fixup (grid-stride over the overflow list)
+#ifndef SF_MT_PARTS
+#define SF_MT_PARTS 32u                // frame-less mode: workgroups per jump-ahead window (sf_mt_jump_partial)
+#endif
 #define SF_PROG_MAX_BINS 32768u        // frame-less mode: packet bins (counting sort in one workgroup's LDS)
 #define SF_PROG_PREFETCH_MIN 65536u    // frame-less batches from this many packets prefetch the next draws
 #define SF_PROG_BIN_MIN 65536u         // frame-less batches below this many packets trace in draw order

@@ -1865,7 +1865,6 @@ extern "C" __global__ __launch_bounds__(SF_MT_PAR_THREADS) void sf_mt_raw(const 
 
 // Partial jumped windows: workgroup (s, p) XORs x_{i+k} (k < 624) over the set coefficients i of segment
 // s + 1's polynomial within [p C, (p + 1) C), C = ceil(19937 / P); the raw words it needs are staged in LDS.
-#define SF_MT_PARTS 8u
 #define SF_MT_CHUNK ((19937u + SF_MT_PARTS - 1u) / SF_MT_PARTS)
 extern "C" __global__ __launch_bounds__(SF_MT_PAR_THREADS) void sf_mt_jump_partial(const uint32_t* __restrict__ raw,
                                                                                     const uint64_t* __restrict__ polys,

@@ -265,6 +265,32 @@ def test_progressive_draw_prefetch_paths(calls, monkeypatch):
         assert st.max_depth == fx["stats"]["max_depth"]
 
 
+def test_progressive_prefetched_bins_follow_the_variant(monkeypatch):
+    """The next batch's binned order is prefetched with its draws for the variant of the batch that issued the
+    prefetch (packet width 8 or 4); a continuing batch of the other variant bins afresh. Frames and stats equal
+    the same calls with the prefetch off."""
+    fx = load_progressive("p3")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+
+    def run():
+        with sf.Sphereflake(W, H) as s:
+            s.SetCamera(sf.config_camera(W, H, K))
+            done = 0
+            for variant in ("avx", "sse", "sse", "avx"):
+                s.SetVariant(variant)
+                s.Progressive(fx["seed"], 70000, counter0=done)
+                done += 70000
+            pos, nrm, _, _ = s.download()
+            return pos, nrm, s.stats()
+
+    pos, nrm, st = run()
+    monkeypatch.setenv("SF_PROG_PREFETCH", "0")
+    epos, enrm, est = run()
+    assert np.array_equal(pos.view(np.uint32), epos.view(np.uint32))
+    assert np.array_equal(nrm.view(np.uint32), enrm.view(np.uint32))
+    assert (st.max_depth, st.closest, st.rays) == (est.max_depth, est.closest, est.rays)
+
+
 def test_repeat_renders_heavy_first_order_bit_exact():
     """From the second render on, the persistent kernel takes its tiles heaviest-first (costs of the
     previous render, sf_tile_order). The image must not depend on the order: renders 2 and 3 of c3
