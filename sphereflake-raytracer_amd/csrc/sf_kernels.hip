@@ -952,6 +952,305 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
 #endif
 }
 
+// ------------------------------------------------------------------------------------------
+// Per-ray semantics (full frames), round 3: a child is entered as soon as its own test passes. The reference
+// itself recurses into child i before testing child i + 1 (Sphereflake.h:162-172); `traverse` above tests all
+// children of a node first, keeps each lane's 9 "expands" bits in LDS and enters the pending children after.
+// Per-ray, the tests of child i + 1 do not depend on anything child i's subtree does (bounding and LOD involve
+// only the ray and the child; acceptance is the self test's, at entry), so entering at once gives the same
+// visits, and the child test's values carry into the entry: its centre and |c|^2 (no second LDS read), tca and
+// d2 (the self test's own, not recomputed), the expanding lanes (no per-lane E bits in LDS: no store at the
+// push, no load at the pop). A node keeps on the VGPR stack its untested children (the cone-culled mask,
+// front children first, as before) instead of its pending ones, and its visiting lanes as one bit per level
+// (`actbits`).
+template <bool PIPE = false>
+__device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ Lbase,
+                                             const float4 bcol, uint32_t levels, float dx, float dy, float dz, bool valid,
+                                             HitState& h, int32_t& maxd, uint32_t& status, uint32_t K_flags,
+                                             uint64_t* phase_sums = nullptr, uint32_t axl = 36u,
+                                             uint64_t* tile_counts = nullptr)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const TraverseLds L{ Lbase };
+    const bool cone_cull = (K_flags & SF_FLAG_NO_CONE_CULL) == 0u;
+    const bool occl_cull = (K_flags & SF_FLAG_NO_OCCL_CULL) == 0u;
+    const bool front_first = (K_flags & (SF_FLAG_NO_OCCL_CULL | SF_FLAG_NO_FRONT_FIRST)) == 0u;
+    const bool lod_cull = (K_flags & SF_FLAG_NO_LOD_CULL) == 0u;
+    SF_STAMP_DECL;
+
+    h.minT = FLT_MAX;
+    h.cx = h.cy = h.cz = 0.f;
+    h.index = 0xffffffffu;
+    h.depth = -1;
+    h.hit = false;
+    uint64_t ancm = 0ull;   // lanes whose current best sphere is an ancestor of the open node (see self_test)
+
+    // ---- root node (depth 0): bounding sphere + LOD
+    const float rcx = root[9], rcy = root[10], rcz = root[11];
+    const float rcc = (rcx * rcx + rcy * rcy) + rcz * rcz;
+    bool ex0;
+    {
+        const float4 dt0 = depth_consts(K, 0u);
+        const float tca = (rcx * dx + rcy * dy) + rcz * dz;
+        const float d2 = rcc - tca * tca;
+        const bool hb = valid && tca >= 0.0f && d2 <= dt0.x;
+        ex0 = hb && near_root(tca, d2, dt0.x) < dt0.w;
+    }
+    if (!wave_ballot(ex0)) return;
+    maxd = 0;
+
+    // ---- the wave's ray cone (as in traverse)
+    {
+        const float ax = readlane_f(dx, axl), ay = readlane_f(dy, axl), az = readlane_f(dz, axl);
+        float cosT = 0.0f, sinT = 1.0f;
+        if (cone_cull) {
+            const float cx_ = dy * az - dz * ay, cy_ = dz * ax - dx * az, cz_ = dx * ay - dy * ax;
+            const float s2 = (cx_ * cx_ + cy_ * cy_) + cz_ * cz_;
+            const bool fwd = (dx * ax + dy * ay) + dz * az > 0.0f;
+            const float s2m = fwd ? s2 : 1.0f;
+            const float sm = __builtin_amdgcn_sqrtf(wave_max_pos(s2m)) * (1.0f + 0x1p-16f) + 0x1p-16f;
+            if (sm < 0.5f) {
+                sinT = sm;
+                cosT = __builtin_amdgcn_sqrtf(1.0f - sm * sm) * (1.0f - 0x1p-16f);
+            }
+        }
+        if (lane < 5u) L.cone()[lane] = lane == 0u ? ax : lane == 1u ? ay : lane == 2u ? az : lane == 3u ? cosT : sinT;
+    }
+
+    // this lane's column of the cooperative child build (see traverse)
+    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 0u : 1u + ((lane - 32u) & 7u);
+    const uint32_t bc = lane < 27u ? lane / 9u : 3u;
+    const float b[4] = { bcol.x, bcol.y, bcol.z, bcol.w };
+    const uint32_t slot = bc == 3u ? bi * 4u : SF_LDS_PLANE + bc * SF_LDS_COLS + bi * 3u;
+
+    uint32_t d = 0;      // uniform: depth of the open node
+    uint32_t idxB = 1;   // uniform: the heap index of the open node's child 0 (9 n + 1)
+
+    // ---- the own sphere of a node entered for the lanes of actv (+inf on them, -1 elsewhere), with its tca and
+    // d2 already formed by its child test (the same operations: Sphereflake.h:174-224, SIMD_AVX.h:236-270).
+    // Pre-order with the ancestor tie rule (see traverse's self_test).
+    auto self_test = [&](const float4 pc, float tca, float d2, uint32_t dd, float actv, uint32_t idx, float R2s) {
+        const uint64_t hsm = wave_ballot(__builtin_fminf(__builtin_fminf(tca, R2s - d2), actv) >= 0.0f);
+        if (hsm) {
+            const float xs = R2s - d2;
+            float ts;
+            if ((wave_ballot(!(xs >= 0x1p-96f)) & hsm) != 0ull) ts = near_root_exact(tca, d2, R2s);
+            else ts = near_root_big(tca, xs);
+            const uint64_t eqm = wave_ballot(ts == h.minT);
+            const uint64_t accm = hsm & (wave_ballot(ts < h.minT) | (eqm & ancm));
+            if (front_first && (hsm & eqm & ~ancm) != 0ull) status |= SF_STATUS_TIE;
+            sel_in_place(h.minT, ts, accm);
+            sel_in_place(h.cx, pc.x, accm);
+            sel_in_place(h.cy, pc.y, accm);
+            sel_in_place(h.cz, pc.z, accm);
+            sel_in_place(h.index, idx, accm);
+            uint32_t hd = (uint32_t)h.depth;
+            sel_in_place(hd, dd, accm);
+            h.depth = (int32_t)hd;
+            ancm |= accm;
+        }
+    };
+
+    // ---- bounding + LOD of one child (centre c, |c|^2 cc, depth constants R2b, T, Tfar) for the lanes of actv:
+    // the lanes that expand it (see traverse's test_child for the fast decisions and the certified bracket)
+    auto child_test = [&](float tca, float d2, float actv, float R2b, float T, float Tfar) -> uint64_t {
+        SF_COUNT(1, 1);
+        const float xs = R2b - d2;
+        const bool hb = __builtin_fminf(__builtin_fminf(tca, xs), actv) >= 0.0f;
+        const uint64_t hbm = wave_ballot(hb);
+        if (hbm == 0ull) {
+            SF_COUNT(2, 1);
+            return 0ull;
+        }
+        const uint64_t nearm = wave_ballot(tca < T);
+        const uint64_t farm = wave_ballot(tca * (1.0f - 0x1p-8f) >= Tfar);
+        if ((hbm & ~(nearm | farm)) == 0ull) return hbm & nearm;
+        const float sq = __builtin_amdgcn_sqrtf(xs);
+        const float s_lo = __uint_as_float((uint32_t)max((int32_t)__float_as_uint(sq) - 2, 0));
+        const float s_hi = __uint_as_float(__float_as_uint(sq) + 2u);
+        const float t_hi = tca - s_lo;
+        const float t_lo = tca - s_hi;
+        const uint64_t tinym = wave_ballot(xs < 0x1p-96f);
+        const float thx = sel_mask(t_hi, __builtin_inff(), tinym);
+        const float tlx = sel_mask(t_lo, -__builtin_inff(), tinym);
+        const float th = hb ? thx : __builtin_inff();
+        const float tl = hb ? tlx : __builtin_inff();
+        uint64_t exm = wave_ballot(th < T);
+        const uint64_t undm = wave_ballot(sel_mask(tl, __builtin_inff(), exm) < T);
+        if (undm) {
+            const float te = near_root_exact(tca, d2, R2b);
+            exm |= undm & wave_ballot(te < T);
+        }
+        return exm;
+    };
+
+    // ---- expand the node with centre/|c|^2 pc at depth d (axis columns at col + j cs): build its 9 child
+    // transforms into table(d) and cull the children no ray of the tile's cone can reach. Returns the children
+    // left to test; leafm = its inline-leaf children | its front children << 9. At the deepest provisioned level
+    // (no table for the children's children) the children are tested here, from the centre lanes: any that some
+    // lane expands flags the tile for the deeper re-trace, and none is entered.
+    auto expand = [&](const float4 pc, const float* col, uint32_t cs, uint32_t d, float actv, uint32_t& leafm) -> uint32_t {
+        d = __builtin_amdgcn_readfirstlane(d);
+        SF_COUNT(0, 1);
+        lds_fence();
+        const float3 p0 = *reinterpret_cast<const float3*>(col);
+        const float3 p1 = *reinterpret_cast<const float3*>(col + cs);
+        const float3 p2 = *reinterpret_cast<const float3*>(col + 2u * cs);
+        const float4 cn = *reinterpret_cast<const float4*>(L.cone());
+        const float sinT = L.cone()[4];
+        const float4 dtn = depth_consts(K, d);
+        const float4 dtc = depth_consts(K, d + 1u);
+        const float leaf1 = depth_leaf(K, d + 1u);
+        const float leafc = lod_cull ? leaf1 : __builtin_inff();
+        const float sm = bc == 3u ? dtn.z : 1.0f;
+        const float b0 = b[0] * sm, b1 = b[1] * sm, b2 = b[2] * sm;
+        const float x = ((p0.x * b0 + p1.x * b1) + p2.x * b2) + pc.x * b[3];
+        const float y = ((p0.y * b0 + p1.y * b1) + p2.y * b2) + pc.y * b[3];
+        const float z = ((p0.z * b0 + p1.z * b1) + p2.z * b2) + pc.z * b[3];
+        const float w = (x * x + y * y) + z * z;
+        if (d + 1u < levels) {
+            float* const tb = L.table(d);
+            *reinterpret_cast<float3*>(tb + slot) = make_float3(x, y, z);
+            *(bc == 3u ? tb + slot + 3u : L.cone() + 5u) = w;
+        }
+        const float R2b = dtc.x;
+        // cone cull of child bi (centre lanes 31..39), in squares (see traverse)
+        const float ax = cn.x, ay = cn.y, az = cn.z, cosT = cn.w;
+        const float dl = w * 0x1p-18f;
+        const float ca = (x * ax + y * ay) + z * az;
+        const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaxf(w - ca * ca, 0.0f));
+        const float X = sq * cosT - ca * sinT;
+        const float Y = X * X - (R2b + w * (0x1p-18f + 0x1p-19f));
+        const float mk = __builtin_fminf(__builtin_fminf(ca, w - 2.0f * (R2b + dl)), __builtin_fminf(X, Y));
+        uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 31) & 0x1ffu;
+        M = __builtin_amdgcn_readfirstlane(M);
+        leafm = (uint32_t)(wave_ballot(w > leafc) >> 31) & 0x1ffu;
+        if (front_first) {
+            const float kp = (pc.x * ax + pc.y * ay) + pc.z * az;
+            leafm |= ((uint32_t)(wave_ballot(ca < kp) >> 31) & 0x1ffu) << 9;
+        }
+        if (d + 1u >= levels) {
+            const float T = dtc.w, Tfar = depth_far(K, d + 1u);
+            while (M) {
+                const uint32_t i = __builtin_ctz(M);
+                M &= ~(1u << i);
+                const float cx = readlane_f(x, 31u + i), cy = readlane_f(y, 31u + i);
+                const float cz = readlane_f(z, 31u + i), cc = readlane_f(w, 31u + i);
+                const float tca = (cx * dx + cy * dy) + cz * dz;
+                const float d2 = cc - tca * tca;
+                if (child_test(tca, d2, actv, R2b, T, Tfar) != 0ull) {
+                    status |= SF_STATUS_OVERFLOW;
+                    break;
+                }
+            }
+            return 0u;
+        }
+        return M;
+    };
+
+    uint32_t stk_pc = 0u, stk_ix = 0u;   // VGPR stack, lane k = level k: {untested | leaf << 9 | front << 18}, idxB
+    uint32_t M = 0u, leafN = 0u;         // uniform: the open node's untested children; its leaf | front << 9 bits
+    float actv;                          // per lane: +inf if the lane visits the open node, -1 otherwise
+    uint32_t actbits;                    // per lane: bit k set if the lane visits the open node's level-k ancestor
+    {
+        lds_fence();
+        const float4 pc = *reinterpret_cast<const float4*>(L.root());
+        actv = ex0 ? __builtin_inff() : -1.0f;
+        actbits = ex0 ? 1u : 0u;
+        const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
+        const float d2 = pc.w - tca * tca;
+        self_test(pc, tca, d2, 0u, actv, 0u, depth_consts(K, 0u).y);
+        if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u)))))
+            M = expand(pc, L.root() + 4u, 4u, 0u, actv, leafN);
+        else SF_COUNT(4, 1);
+    }
+
+    for (;;) {
+        d = __builtin_amdgcn_readfirstlane(d);
+        SF_STAMP(0);
+        if (M) {
+            const uint32_t fp = M & (leafN >> 9);   // front children first
+            const uint32_t c = __builtin_ctz(fp ? fp : M);
+            const uint32_t cbit = 1u << c;
+            M &= ~cbit;
+            // the children's depth constants (scalar loads, in flight with the centre's LDS read)
+            const float4 dc = depth_consts(K, d + 1u);
+            const float Tfar = depth_far(K, d + 1u);
+            const float cull_r = depth_cull(K, d + 1u);
+            lds_fence();
+            const float4 pc = *reinterpret_cast<const float4*>(L.table(d) + c * 4u);
+            const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
+            const float d2 = pc.w - tca * tca;
+            const uint64_t exm = child_test(tca, d2, actv, dc.x, dc.w, Tfar);
+            SF_STAMP(2);
+            if (exm == 0ull) continue;
+            // ---- child c passed bounding + LOD for the lanes of exm: enter it
+            SF_COUNT(3, 1);
+            maxd = (int32_t)d + 1 > maxd ? (int32_t)d + 1 : maxd;   // Sphereflake.h:157-160
+            // occlusion cull (see traverse): lanes for which no sphere of the child's subtree can be accepted or
+            // pass LOD deeper than the depth already reached do not enter
+            uint64_t amx = exm;
+            if (occl_cull) {
+                const float cull_t = depth_consts(K, (uint32_t)maxd + 1u).w;
+                const float rho = cull_r + SF_OCCL_MARGIN * __builtin_amdgcn_sqrtf(pc.w);
+                const uint64_t cm = wave_ballot(__builtin_fminf(tca - h.minT, tca - cull_t) > rho);
+                amx = exm & ~cm;
+                SF_COUNT(13, 1);
+                SF_COUNT(12, amx == 0ull ? 1 : 0);
+                if (amx == 0ull) continue;
+            }
+            const float avx = sel_mask(-1.0f, __builtin_inff(), amx);
+            self_test(pc, tca, d2, d + 1u, avx, idxB + c, dc.y);
+            SF_STAMP(4);
+            if ((leafN & cbit) != 0u) {   // an inline leaf: its own sphere only (sfhost::leaf_threshold)
+                SF_COUNT(4, 1);
+                SF_COUNT(8, 1);
+                SF_COUNT(9, __builtin_popcountll(amx));
+                ancm &= wave_ballot(h.depth != (int32_t)d + 1);   // the child is finished
+                continue;
+            }
+            // push the open node, open child c
+            stk_pc = writelane_u(M | (leafN << 9), d, stk_pc);
+            stk_ix = writelane_u(idxB, d, stk_ix);
+            {
+                const uint32_t bit = 2u << d;   // level d + 1
+                uint32_t ab = actbits & ~bit;
+                sel_in_place(ab, ab | bit, amx);
+                actbits = ab;
+            }
+            idxB = 9u * (idxB + c) + 1u;
+            d += 1u;
+            actv = avx;
+            SF_STAMP(1);
+            M = expand(pc, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, avx, leafN);
+            SF_STAMP(6);
+            continue;
+        }
+        // ---- the node at depth d is finished: a best sphere at depth d is no longer an ancestor
+        ancm &= wave_ballot(h.depth != (int32_t)d);
+        if (d == 0u) break;
+        d -= 1u;
+        {
+            const uint32_t pw = __builtin_amdgcn_readlane(stk_pc, d);
+            M = pw & 0x1ffu;
+            leafN = pw >> 9;
+            idxB = (uint32_t)__builtin_amdgcn_readlane(stk_ix, d);
+        }
+        actv = ((actbits >> d) & 1u) ? __builtin_inff() : -1.0f;
+        SF_STAMP(5);
+    }
+    h.hit = h.depth >= 0;
+    SF_STAMP_FLUSH(phase_sums);
+#ifdef SF_COUNTS
+    if (tile_counts) {
+        auto sat = [](uint64_t v) { return v > 0xffffull ? 0xffffull : v; };
+        *tile_counts = sat(ph_sum[0]) | (sat(ph_sum[1]) << 16) | (sat(ph_sum[1] - ph_sum[2]) << 32) | (sat(ph_sum[8]) << 48);
+    }
+#else
+    (void)tile_counts;
+#endif
+}
+
 struct Tile {
     uint32_t x, y, orow;
     bool valid;
@@ -1111,9 +1410,15 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     // The main kernels enter children front-first (with the occlusion cull); an exact non-ancestor tie under
     // that order flags the tile like an overflow, and the fixup re-traces it in index order -- the reference's
     // tie rule (see traverse). The fixup kernel always traces in index order.
+#ifndef SF_OLD_TRAVERSE
+    traverse_ray<PIPE>(K, a.root, L, bcol, levels, dx, dy, dz, t.valid, h, maxd, status,
+                       FIXUP ? (a.flags | SF_FLAG_NO_FRONT_FIRST) : a.flags,
+                       FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
+#else
     traverse<0, PIPE>(K, a.root, L, bcol, levels, dx, dy, dz, t.valid, h, maxd, status,
                       FIXUP ? (a.flags | SF_FLAG_NO_FRONT_FIRST) : a.flags,
                       FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
+#endif
     if (!FIXUP && (a.flags & SF_FLAG_DIAG_FORCE_RETRACE)) status |= SF_STATUS_TIE;
     const bool overflowed = status != 0u;
     pre();
