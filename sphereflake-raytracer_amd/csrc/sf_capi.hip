@@ -352,7 +352,7 @@ static int upload_consts(sf_ctx* c)
         e[2] = c->host_consts.dt.scale[d];
         e[3] = c->host_consts.dt.lod[d];
         e[4] = sfhost::leaf_threshold(&c->host_consts.dt, (uint32_t)d);
-        e[5] = std::nextafter((float)(std::sqrt((double)e[0]) * (1.0 + (double)SF_OCCL_MARGIN)), FLT_MAX);
+        e[5] = std::nextafter((float)(std::sqrt((double)e[0]) * (1.0 + 2.0 * (double)SF_OCCL_MARGIN)), FLT_MAX);
         e[6] = std::nextafter((float)((double)e[3] + std::sqrt((double)e[0]) * (1.0 + 0x1p-18)), FLT_MAX);
         e[7] = 0.0f;
     }

@@ -96,7 +96,7 @@ struct DeviceConsts {
     DepthTables dt;
     // the same interleaved per depth d, one scalar load: {r2_bound, r2_self, scale, lod,
     // leaf, cull, far, 0}; leaf = |c|^2 threshold beyond which no child of a depth-d node centred at c can
-    // pass the LOD test for any ray (sfhost::leaf_threshold); cull = 2 r_d (1 + SF_OCCL_MARGIN), rounded
+    // pass the LOD test for any ray (sfhost::leaf_threshold); cull = 2 r_d (1 + 2 SF_OCCL_MARGIN), rounded
     // up: the occlusion cull's fattened bounding radius without its |c| term (see traverse); far =
     // T_d + 2 r_d (1 + 2^-18), rounded up: a bounding hit with tca (1 - 2^-8) >= far cannot pass LOD
     float depth8[SF_DEPTH_TABLE][8];

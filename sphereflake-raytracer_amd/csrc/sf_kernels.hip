@@ -348,7 +348,7 @@ __device__ __forceinline__ float depth_leaf(const DeviceConsts* K, uint32_t d)
 #endif
 }
 
-// {.., cull} of depth d: 2 r_d (1 + SF_OCCL_MARGIN), rounded up (see DeviceConsts::depth8)
+// {.., cull} of depth d: 2 r_d (1 + 2 SF_OCCL_MARGIN), rounded up (see DeviceConsts::depth8)
 __device__ __forceinline__ float depth_cull(const DeviceConsts* K, uint32_t d)
 {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1189,11 +1189,15 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             maxd = (int32_t)d + 1 > maxd ? (int32_t)d + 1 : maxd;   // Sphereflake.h:157-160
             // occlusion cull (see traverse): lanes for which no sphere of the child's subtree can be accepted or
             // pass LOD deeper than the depth already reached do not enter
+            // The fattened radius rho = R (1 + m) + m |c| (see traverse) without |c|: a lane of exm hit the bounding
+            // sphere, so |c|^2 = d2 + tca^2 <= R^2 + tca^2 (+ the float test's slack, 2^-9.6 |c|) and
+            // |c| <= tca + R (+ 2^-9.6 |c|, whose m multiple is far inside m's safety factor): rho <= R (1 + 2 m) +
+            // m tca = cull_r + m tca per lane, no square root.
             uint64_t amx = exm;
             if (occl_cull) {
                 const float cull_t = depth_consts(K, (uint32_t)maxd + 1u).w;
-                const float rho = cull_r + SF_OCCL_MARGIN * __builtin_amdgcn_sqrtf(pc.w);
-                const uint64_t cm = wave_ballot(__builtin_fminf(tca - h.minT, tca - cull_t) > rho);
+                const float v = __builtin_fminf(tca - h.minT, tca - cull_t);
+                const uint64_t cm = wave_ballot(v - SF_OCCL_MARGIN * tca > cull_r);
                 amx = exm & ~cm;
                 SF_COUNT(13, 1);
                 SF_COUNT(12, amx == 0ull ? 1 : 0);
