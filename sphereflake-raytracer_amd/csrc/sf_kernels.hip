@@ -1051,17 +1051,9 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         }
     };
 
-    // ---- bounding + LOD of one child (centre c, |c|^2 cc, depth constants R2b, T, Tfar) for the lanes of actv:
+    // ---- LOD of one child whose bounding sphere the lanes of hbm hit (xs = R2b - d2, depth constants R2b, T, Tfar):
     // the lanes that expand it (see traverse's test_child for the fast decisions and the certified bracket)
-    auto child_test = [&](float tca, float d2, float actv, float R2b, float T, float Tfar) -> uint64_t {
-        SF_COUNT(1, 1);
-        const float xs = R2b - d2;
-        const bool hb = __builtin_fminf(__builtin_fminf(tca, xs), actv) >= 0.0f;
-        const uint64_t hbm = wave_ballot(hb);
-        if (hbm == 0ull) {
-            SF_COUNT(2, 1);
-            return 0ull;
-        }
+    auto child_lod = [&](float tca, float d2, float xs, bool hb, uint64_t hbm, float R2b, float T, float Tfar) -> uint64_t {
         const uint64_t nearm = wave_ballot(tca < T);
         const uint64_t farm = wave_ballot(tca * (1.0f - 0x1p-8f) >= Tfar);
         if ((hbm & ~(nearm | farm)) == 0ull) return hbm & nearm;
@@ -1125,9 +1117,12 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 31) & 0x1ffu;
         M = __builtin_amdgcn_readfirstlane(M);
         leafm = (uint32_t)(wave_ballot(w > leafc) >> 31) & 0x1ffu;
+        // entry order as bit order: the front children (nearer than this node's centre along the cone axis) at
+        // bits 0..8, the others at 9..17 -- one find-first-set per child picks the next
+        uint32_t front = 0x1ffu;
         if (front_first) {
             const float kp = (pc.x * ax + pc.y * ay) + pc.z * az;
-            leafm |= ((uint32_t)(wave_ballot(ca < kp) >> 31) & 0x1ffu) << 9;
+            front = (uint32_t)(wave_ballot(ca < kp) >> 31) & 0x1ffu;
         }
         if (d + 1u >= levels) {
             const float T = dtc.w, Tfar = depth_far(K, d + 1u);
@@ -1138,18 +1133,22 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
                 const float cz = readlane_f(z, 31u + i), cc = readlane_f(w, 31u + i);
                 const float tca = (cx * dx + cy * dy) + cz * dz;
                 const float d2 = cc - tca * tca;
-                if (child_test(tca, d2, actv, R2b, T, Tfar) != 0ull) {
+                const float xs = R2b - d2;
+                const bool hb = __builtin_fminf(__builtin_fminf(tca, xs), actv) >= 0.0f;
+                const uint64_t hbm = wave_ballot(hb);
+                if (hbm != 0ull && child_lod(tca, d2, xs, hb, hbm, R2b, T, Tfar) != 0ull) {
                     status |= SF_STATUS_OVERFLOW;
                     break;
                 }
             }
             return 0u;
         }
-        return M;
+        return (M & front) | ((M & ~front) << 9);
     };
 
-    uint32_t stk_pc = 0u, stk_ix = 0u;   // VGPR stack, lane k = level k: {untested | leaf << 9 | front << 18}, idxB
-    uint32_t M = 0u, leafN = 0u;         // uniform: the open node's untested children; its leaf | front << 9 bits
+    uint32_t stk_pc = 0u, stk_ix = 0u;   // VGPR stack, lane k = level k: {untested | leaf << 18}, idxB
+    uint32_t C = 0u, leafN = 0u;         // uniform: the open node's untested children in entry order (child i at bit
+                                         // i if it is a front child, else at bit 9 + i); its inline-leaf children
     float actv;                          // per lane: +inf if the lane visits the open node, -1 otherwise
     uint32_t actbits;                    // per lane: bit k set if the lane visits the open node's level-k ancestor
     {
@@ -1161,27 +1160,37 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float d2 = pc.w - tca * tca;
         self_test(pc, tca, d2, 0u, actv, 0u, depth_consts(K, 0u).y);
         if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u)))))
-            M = expand(pc, L.root() + 4u, 4u, 0u, actv, leafN);
+            C = expand(pc, L.root() + 4u, 4u, 0u, actv, leafN);
         else SF_COUNT(4, 1);
     }
 
+    // (the scalar unit is shared by the CU's four SIMDs and measured ~3x a VALU op per instruction here: the child
+    // loop keeps its scalar bookkeeping to a find-first-set, a clear-lowest and the index)
     for (;;) {
         d = __builtin_amdgcn_readfirstlane(d);
         SF_STAMP(0);
-        if (M) {
-            const uint32_t fp = M & (leafN >> 9);   // front children first
-            const uint32_t c = __builtin_ctz(fp ? fp : M);
-            const uint32_t cbit = 1u << c;
-            M &= ~cbit;
+        if (C) {
+            const uint32_t p = __builtin_ctz(C);
+            C &= C - 1u;
+            const uint32_t c = min(p, p - 9u);   // (p < 9: front child p; else child p - 9)
             // the children's depth constants (scalar loads, in flight with the centre's LDS read)
             const float4 dc = depth_consts(K, d + 1u);
-            const float Tfar = depth_far(K, d + 1u);
-            const float cull_r = depth_cull(K, d + 1u);
             lds_fence();
             const float4 pc = *reinterpret_cast<const float4*>(L.table(d) + c * 4u);
             const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
             const float d2 = pc.w - tca * tca;
-            const uint64_t exm = child_test(tca, d2, actv, dc.x, dc.w, Tfar);
+            // bounding (SIMD_AVX.h:247-258) for the visiting lanes: one v_min3 compare, its VCC the branch
+            const float xs = dc.x - d2;
+            const bool hb = __builtin_fminf(__builtin_fminf(tca, xs), actv) >= 0.0f;
+            const uint64_t hbm = wave_ballot(hb);
+            SF_COUNT(1, 1);
+            if (hbm == 0ull) {
+                SF_COUNT(2, 1);
+                continue;
+            }
+            const float Tfar = depth_far(K, d + 1u);
+            const float cull_r = depth_cull(K, d + 1u);
+            const uint64_t exm = child_lod(tca, d2, xs, hb, hbm, dc.x, dc.w, Tfar);
             SF_STAMP(2);
             if (exm == 0ull) continue;
             // ---- child c passed bounding + LOD for the lanes of exm: enter it
@@ -1206,7 +1215,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             const float avx = sel_mask(-1.0f, __builtin_inff(), amx);
             self_test(pc, tca, d2, d + 1u, avx, idxB + c, dc.y);
             SF_STAMP(4);
-            if ((leafN & cbit) != 0u) {   // an inline leaf: its own sphere only (sfhost::leaf_threshold)
+            if ((leafN >> c) & 1u) {   // an inline leaf: its own sphere only (sfhost::leaf_threshold)
                 SF_COUNT(4, 1);
                 SF_COUNT(8, 1);
                 SF_COUNT(9, __builtin_popcountll(amx));
@@ -1214,7 +1223,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
                 continue;
             }
             // push the open node, open child c
-            stk_pc = writelane_u(M | (leafN << 9), d, stk_pc);
+            stk_pc = writelane_u(C | (leafN << 18), d, stk_pc);
             stk_ix = writelane_u(idxB, d, stk_ix);
             {
                 const uint32_t bit = 2u << d;   // level d + 1
@@ -1226,7 +1235,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             d += 1u;
             actv = avx;
             SF_STAMP(1);
-            M = expand(pc, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, avx, leafN);
+            C = expand(pc, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, avx, leafN);
             SF_STAMP(6);
             continue;
         }
@@ -1236,8 +1245,8 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         d -= 1u;
         {
             const uint32_t pw = __builtin_amdgcn_readlane(stk_pc, d);
-            M = pw & 0x1ffu;
-            leafN = pw >> 9;
+            C = pw & 0x3ffffu;
+            leafN = pw >> 18;
             idxB = (uint32_t)__builtin_amdgcn_readlane(stk_ix, d);
         }
         actv = ((actbits >> d) & 1u) ? __builtin_inff() : -1.0f;
