@@ -1036,9 +1036,14 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             float ts;
             if ((wave_ballot(!(xs >= 0x1p-96f)) & hsm) != 0ull) ts = near_root_exact(tca, d2, R2s);
             else ts = near_root_big(tca, xs);
-            const uint64_t eqm = wave_ballot(ts == h.minT);
-            const uint64_t accm = hsm & (wave_ballot(ts < h.minT) | (eqm & ancm));
-            if (front_first && (hsm & eqm & ~ancm) != 0ull) status |= SF_STATUS_TIE;
+            // strictly nearer lanes accept; exact ties (rare) take a branch of their own: a tie is accepted where
+            // the best is an ancestor, and one with a non-ancestor flags the tile (front-first order, see traverse)
+            uint64_t accm = hsm & wave_ballot(ts < h.minT);
+            const uint64_t tie = hsm & wave_ballot(ts == h.minT);
+            if (tie != 0ull) {
+                accm |= tie & ancm;
+                if (front_first && (tie & ~ancm) != 0ull) status |= SF_STATUS_TIE;
+            }
             sel_in_place(h.minT, ts, accm);
             sel_in_place(h.cx, pc.x, accm);
             sel_in_place(h.cy, pc.y, accm);
