@@ -164,6 +164,10 @@ int sf_set_variant(sf_ctx* ctx, int variant);
 int sf_get_variant(const sf_ctx* ctx);   /* SF_VARIANT_* or SF_EINVAL */
 /* Exact threshold T: sqrtf(t / r) < lod_constant || t < 0  <=>  t < T (Sphereflake.h:129,146). Host only. */
 int sf_lod_threshold(float r, float lod_constant, float* T);
+/* 1 when ray generation's u = x / n (Sphereflake.cpp:149-150) may be formed as q0 = RN(x RN(1/n)) corrected by one
+   fma residual (RN(q0 + (x - q0 n) RN(1/n))) with the same bits as the division for every integer x in [0, n];
+   a context uses the shortcut only for a frame size where this holds (checked at sf_create). Host only. */
+int sf_division_by_reciprocal_exact(uint32_t n);
 
 /* --- SSAO post-process ---------------------------------- */
 /* The reference's GL passes over the G-buffer (SSAO.cpp:106-142: SSAO, blur x, blur y;

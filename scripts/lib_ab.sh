@@ -11,7 +11,7 @@ mkdir -p $OUT
 for rep in $(seq 1 ${REPS:-3}); do
   for LF in "$@"; do
     L=${LF%@*}; F=0; [ "$L" != "$LF" ] && F=${LF#*@}
-    SF_FLAGS=$F SF_LIB=$R/$L timeout -k 10 120 python3 -u bench.py --no-cpu-baseline --no-extras --steps 200 --warmup 30 $ARGS > $OUT/b.json
+    SF_LIB_PARTIAL=1 SF_FLAGS=$F SF_LIB=$R/$L timeout -k 10 120 python3 -u bench.py --no-cpu-baseline --no-extras --steps 200 --warmup 30 $ARGS > $OUT/b.json
     python3 -c "import json; j=json.loads(open('$OUT/b.json').read().strip().split(chr(10))[-1]); print('$LF', 'frame', j['frame_ms'], 'trace', j['roofline']['kernel_ms'], 'clk', j['roofline'].get('clock_mhz_live'), 'Mrays', j['value'], 'fixed', j['fixed_camera']['frame_ms'] if j.get('fixed_camera') else None)"
   done
 done
@@ -21,7 +21,7 @@ if [ "${PMC:-0}" = "1" ]; then
   for LF in "$@"; do
     L=${LF%@*}; F=0; [ "$L" != "$LF" ] && F=${LF#*@}
     i=$((i+1))
-    SF_FLAGS=$F SF_LIB=$R/$L timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $OUT/pmc$i -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras $ARGS > $OUT/pmc$i.log 2>&1
+    SF_LIB_PARTIAL=1 SF_FLAGS=$F SF_LIB=$R/$L timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $OUT/pmc$i -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras $ARGS > $OUT/pmc$i.log 2>&1
     echo "== $LF"
     python3 $R/scripts/pmc_summary.py $OUT/pmc$i | grep -A12 "sf_trace_queue2 " || true
   done

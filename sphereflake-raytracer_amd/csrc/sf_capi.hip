@@ -101,6 +101,7 @@ struct DevGuard {
 }  // namespace
 
 struct sf_ctx {
+    uint32_t fast_div = 0;             // ray generation's u = x / W by reciprocal + fma correction (host-verified)
     int device = 0;
     uint32_t W = 0, H = 0;
     hipStream_t stream = nullptr;
@@ -358,6 +359,10 @@ static int upload_consts(sf_ctx* c)
     }
     std::memcpy(c->host_consts.lut, kLut, sizeof kLut);
     sfhost::sobol_matrices(c->host_consts.sobol);
+    c->host_consts.rw = 1.0f / (float)c->W;
+    c->host_consts.rh = 1.0f / (float)c->H;
+    c->host_consts.fast_div = c->fast_div ? 1u : 0u;
+    c->host_consts.tx_magic = 0xffffffffu / ((c->W + 7) / 8);
     if (int rc_ = ctx_drain(c)) return rc_;   // no kernel of the context may still read the block
     SF_HIP(c, hipMemcpyAsync(c->consts, &c->host_consts, sizeof(DeviceConsts), hipMemcpyHostToDevice, c->stream));
     SF_HIP(c, hipStreamSynchronize(c->stream));
@@ -429,6 +434,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     c->device = device;
     c->W = width;
     c->H = height;
+    c->fast_div = sfhost::division_by_reciprocal_exact(width) && sfhost::division_by_reciprocal_exact(height);
     c->fixup_blocks = prop.multiProcessorCount;
     c->cus = prop.multiProcessorCount;
     {   // gfx950: 32 CUs per XCD; a compute partition of the chip exposes fewer XCDs (then fewer queues)
@@ -625,6 +631,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
     FrameArgs a = frame_args(c);
     a.tile_rows = tile_rows;
     a.tiles_per_band = tpb;
+    a.tpb_magic = 0xffffffffu / tpb;
     a.band_count = band_count;
     a.band_index = p.band_index;
     a.compact = p.compact ? 1u : 0u;
@@ -1461,6 +1468,11 @@ int sf_lod_threshold(float r, float lod_constant, float* T)
     if (!T || !(r > 0.0f) || !(lod_constant > 0.0f)) return SF_EINVAL;
     *T = sfhost::lod_threshold(r, lod_constant);
     return SF_OK;
+}
+
+int sf_division_by_reciprocal_exact(uint32_t n)
+{
+    return sfhost::division_by_reciprocal_exact(n) ? 1 : 0;
 }
 
 int sf_depth_constants(uint32_t depth, float* radius, float* lod)

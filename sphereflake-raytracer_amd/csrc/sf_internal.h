@@ -102,6 +102,11 @@ struct DeviceConsts {
     float depth8[SF_DEPTH_TABLE][8];
     uint32_t lut[2048];               // x86 rsqrtps table (rsqrtps_lut.inc)
     uint32_t sobol[2][52];            // Sobol direction numbers, dims 0 and 1 (Sobol.cpp:34-39, 57-162)
+    // per context (its frame size), read by scalar loads where used rather than carried in the launch arguments:
+    // {RN(1 / W), RN(1 / H)}: u = x / W as one product and one fma correction, where the host checked it equals
+    // x / W for every x in [0, W] and y in [0, H] (fast_div); floor((2^32 - 1) / tiles_x) (tile_of)
+    float rw, rh;
+    uint32_t fast_div, tx_magic;
 };
 
 // Frame-less progressive mode: one traced packet lane (staged between trace and scatter).
@@ -149,6 +154,7 @@ struct FrameArgs {
     uint32_t bin_shift, bins_x;       // frame-less mode: the batch's packet bins (squares of 2^bin_shift pixels)
     uint64_t* clock_probe;            // measurement (NULL = off): the first wave of blocks 0..SF_CLOCK_WAVES-1
                                       // writes {s_memtime, s_memrealtime} at its start and at its end
+    uint32_t tpb_magic;               // floor((2^32 - 1) / tiles_per_band) (tile_of)
 };
 #define SF_CLOCK_WAVES 8u             // live shader clock samples per timed render (one per XCD group)
 
@@ -217,6 +223,8 @@ void camera_corners(uint32_t W, uint32_t H, const float pos[3], float pitch, flo
                     float fov, float o[3], float tl[3], float tr[3], float bl[3]);
 float radius(uint32_t depth);
 float lod_threshold(float r, float lod_constant = 70.0f);
+// true when fma(fma(-q0, n, x), RN(1/n), q0), q0 = RN(x RN(1/n)), equals RN(x / n) for every integer x in [0, n]
+bool division_by_reciprocal_exact(uint32_t n);
 void depth_tables(DepthTables* t, float lod_constant = 70.0f);
 float leaf_threshold(const DepthTables* t, uint32_t depth);
 void sobol_matrices(uint32_t out[2][52]);

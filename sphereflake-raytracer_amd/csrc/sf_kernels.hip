@@ -79,8 +79,26 @@ __device__ __forceinline__ void normalize3(float& x, float& y, float& z, const u
 __device__ __forceinline__ void ray_dir(const FrameArgs& a, float x, float y, float& dx, float& dy, float& dz,
                                         const uint32_t* __restrict__ lut)
 {
-    const float u = x / a.fw;
-    const float v = y / a.fh;
+    float u, v;
+    // (uniform) RN(x / W) as one product and one fma correction (sfhost::division_by_reciprocal_exact); the
+    // context's reciprocals by scalar loads from the constant block
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) DeviceConsts* ConstK;
+    const ConstK kc = (ConstK)(const void*)a.consts;
+    const float rw = kc->rw, rh = kc->rh;
+    const uint32_t fast = kc->fast_div;
+#else
+    const float rw = a.consts->rw, rh = a.consts->rh;
+    const uint32_t fast = a.consts->fast_div;
+#endif
+    if (fast) {
+        const float qu = x * rw, qv = y * rh;
+        u = __builtin_fmaf(__builtin_fmaf(-qu, a.fw, x), rw, qu);
+        v = __builtin_fmaf(__builtin_fmaf(-qv, a.fh, y), rh, qv);
+    } else {
+        u = x / a.fw;
+        v = y / a.fh;
+    }
     dx = ((a.tl[0] + a.dh[0] * u) + a.dv[0] * v) - a.o[0];
     dy = ((a.tl[1] + a.dh[1] * u) + a.dv[1] * v) - a.o[1];
     dz = ((a.tl[2] + a.dh[2] * u) + a.dv[2] * v) - a.o[2];
@@ -1277,9 +1295,28 @@ struct Tile {
 // Tile of a wave: owned tile row k (band sharding) -> frame tile row.
 __device__ __forceinline__ Tile tile_of(const FrameArgs& a, uint32_t tile, uint32_t lane, uint32_t part = 0u)
 {
-    const uint32_t tx = tile % a.tiles_x, k = tile / a.tiles_x;
-    const uint32_t band = a.band_index + (k / a.tiles_per_band) * a.band_count;
-    const uint32_t ty = band * a.tiles_per_band + k % a.tiles_per_band;
+    // tile -> (k, tx) and k -> (band, row in band) by multiply-high with host magic numbers and one correction
+    // (m = floor((2^32 - 1) / D) underestimates n / D by less than 1 for n < 2^31: q or q + 1), scalar
+    auto divmod = [](uint32_t n, uint32_t D, uint32_t m, uint32_t& r) {
+        uint32_t q = __umulhi(n, m);
+        r = n - q * D;
+        if (r >= D) {
+            q += 1u;
+            r -= D;
+        }
+        return q;
+    };
+    uint32_t tx, kr;
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) DeviceConsts* ConstK;
+    const uint32_t txm = ((ConstK)(const void*)a.consts)->tx_magic;
+#else
+    const uint32_t txm = a.consts->tx_magic;
+#endif
+    const uint32_t k = divmod(tile, a.tiles_x, txm, tx);
+    const uint32_t kb = divmod(k, a.tiles_per_band, a.tpb_magic, kr);
+    const uint32_t band = a.band_index + kb * a.band_count;
+    const uint32_t ty = band * a.tiles_per_band + kr;
     // (opaque copy: recompute the lane's column/row per tile rather than keep them live, or spilled,
     // across a persistent loop)
     uint32_t l = lane;

@@ -320,4 +320,27 @@ bool post_centre_exact(uint32_t n)
     return true;
 }
 
+// Ray generation divides pixel coordinates by the frame size (u = x / W, v = y / H, Sphereflake.cpp:149-150): a
+// correctly rounded division, ~11 instructions on the device. With y = RN(1/n), q0 = RN(x y) and the exact
+// residual r = x - q0 n (one fma), q = RN(q0 + r y) is RN(x / n) for these operands (Markstein's correction;
+// exhaustively true for every n <= 16384 and x in [0, n]); the host checks the frame's own n before the kernels
+// use it, so the shortcut never changes a bit.
+bool division_by_reciprocal_exact(uint32_t n)
+{
+    if (n == 0u || n > (1u << 24)) return false;
+    const float fn = (float)n, y = 1.0f / fn;
+    for (uint32_t x = 0; x <= n; ++x) {
+        const float fx = (float)x;
+        const float q0 = fx * y;
+        const float r = std::fma(-q0, fn, fx);
+        const float q = std::fma(r, y, q0);
+        const float ref = fx / fn;
+        uint32_t a, b;
+        std::memcpy(&a, &q, 4);
+        std::memcpy(&b, &ref, 4);
+        if (a != b) return false;
+    }
+    return true;
+}
+
 }  // namespace sfhost

@@ -94,6 +94,7 @@ SIGNATURES = {
     "sf_set_variant": (ctypes.c_int, [_CTX, ctypes.c_int]),
     "sf_get_variant": (ctypes.c_int, [_CTX]),
     "sf_lod_threshold": (ctypes.c_int, [ctypes.c_float, ctypes.c_float, _F]),
+    "sf_division_by_reciprocal_exact": (ctypes.c_int, [ctypes.c_uint32]),
     "sf_post_defaults": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_post_params)]),
     "sf_post_process": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_post_params), ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p]),
@@ -190,7 +191,11 @@ def lib() -> ctypes.CDLL:
             except ImportError:
                 pass
             L = ctypes.CDLL(LIB_PATH)
+            # (SF_LIB_PARTIAL=1: an older build under A/B -- entry points it predates are left unbound)
+            partial = os.environ.get("SF_LIB_PARTIAL") == "1"
             for name, (res, args) in SIGNATURES.items():
+                if partial and not hasattr(L, name):
+                    continue
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args

@@ -252,3 +252,36 @@ def test_mt19937_jump_matches_generator(seed, advance, steps):
     else:
         half = jump(jump(s0, steps // 2), steps // 2)
         assert np.array_equal(gen(half).random_raw(1500), gen(out).random_raw(1500))
+
+
+def _rn32(fr):
+    """Fraction -> the nearest float32 (ties to even), exactly."""
+    from fractions import Fraction
+    f = np.float32(float(fr))
+    best = None
+    for c in (np.nextafter(f, np.float32(-np.inf)), f, np.nextafter(f, np.float32(np.inf))):
+        e = abs(Fraction(float(c)) - fr)
+        key = (e, int(np.array([c], np.float32).view(np.uint32)[0]) & 1)
+        if best is None or key < best[0]:
+            best = (key, c)
+    return np.float32(best[1])
+
+
+@pytest.mark.parametrize("n", [640, 360, 1280, 720, 1920, 1080, 3840, 2160, 16384, 96, 64, 37, 1, 2, 3])
+def test_division_by_reciprocal_exact(n):
+    """Ray generation forms u = x / W (Sphereflake.cpp:149-150) as q0 = RN(x y), y = RN(1/W), corrected by one fma
+    residual: q = RN(q0 + RN(x - q0 W) y). sf_division_by_reciprocal_exact(W) (the library's host check, run at
+    sf_create) says it equals RN(x / W) for every x in [0, W]; here an independent exact-rational restatement
+    agrees on a sample of x, and the library reports 1 for every BASELINE frame size."""
+    from fractions import Fraction
+    assert sf.lib().sf_division_by_reciprocal_exact(n) == 1
+    fn = np.float32(n)
+    y = np.float32(1.0) / fn
+    rng = np.random.default_rng(n)
+    xs = np.unique(np.concatenate([np.arange(0, min(n, 300) + 1), rng.integers(0, n + 1, 300), [n - 1, n]]))
+    for x in xs:
+        fx = np.float32(x)
+        q0 = np.float32(fx * y)
+        r = _rn32(Fraction(int(x)) - Fraction(float(q0)) * n)          # fma(-q0, n, x)
+        q = _rn32(Fraction(float(q0)) + Fraction(float(r)) * Fraction(float(y)))   # fma(r, y, q0)
+        assert q == np.float32(fx / fn), (n, x)
