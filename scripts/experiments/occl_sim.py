@@ -69,7 +69,7 @@ trows = np.arange(0, (H + 7) // 8, max(1, step // 2))
 
 
 def tiles(margin, mode):
-    st = np.zeros((len(trows), 3), np.int64)
+    st = np.zeros((len(trows), 80), np.int64)
 
     def work(k):
         L.sim_tile_row(W, H, o.ctypes.data_as(fp), tl.ctypes.data_as(fp), tr.ctypes.data_as(fp), bl.ctypes.data_as(fp),
@@ -77,10 +77,28 @@ def tiles(margin, mode):
                        ctypes.c_float(margin), mode, st[k].ctypes.data_as(ctypes.POINTER(ctypes.c_longlong)))
     with ThreadPoolExecutor(8) as ex:
         list(ex.map(work, range(len(trows))))
-    return st.sum(0)
+    return st.sum(0) if not (mode & 64) else st
 
 
 t0 = tiles(-1.0, 0)
+if len(sys.argv) > 3 and sys.argv[3] == "cone":
+    st = tiles(3 * 2.0 ** -10, 17 | 64).sum(0)
+    print("depth: children tested at unique expansions, cone-culled share; at |c| sinT > 4R: share of those children, culled share")
+    for k in range(12):
+        n, c = st[3 + k], st[19 + k]
+        if n:
+            print(f"  depth {k}: {n:9d} culled {c / n:.3f}")
+    names = ["<=2", "<=4", "<=8", "<=16", "<=32", ">32"]
+    tot = st[67:79].sum()
+    print("unique expanded nodes by lanes that expand them (cone useful | cone useless, |c| sinT >= R):")
+    for b in range(6):
+        print(f"  {names[b]:>5} lanes: {st[67 + 2 * b] / tot:.3f} | {st[67 + 2 * b + 1] / tot:.3f}")
+    print("by |c| sinT / r (the node's radius):")
+    for k in range(16):
+        wn, wc = st[35 + k], st[51 + k]
+        if wn:
+            print(f"  [2^{k - 8}, 2^{k - 7}): {wn:9d} children, culled {wc / wn:.3f}")
+    sys.exit(0)
 print(f"tiles (every {max(1, step // 2)}th tile row): wave expansions (union over the tile) {t0[0]}, per-lane {t0[1]}")
 for mode, lg in ((17, 7), (17, 8.415), (17, 9)):
     t = tiles(2.0 ** -lg, mode)
