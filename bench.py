@@ -263,16 +263,20 @@ def post_rates(ctx, torch, stream, width, height, reps=20):
     return out
 
 
-def progressive_rates(width, height, k, batch=1 << 18, reps=5):
+def progressive_rates(width, height, k, batch=1 << 18, reps=10):
     """the frame-less mode (the reference's Initialize() worker stream: mt19937 draws,
     Sobol pixel picks, 8-ray AVX / 4-ray SSE packets with packet early-outs, last-writer scatter) on a
-    fresh context with the same camera, in batches of `batch` packets continuing one stream."""
-    out = {"batch_packets": batch}
+    fresh context with the same camera, in batches of `batch` packets continuing one stream. Two untimed
+    batches first and a wait: the steady state of a running loop (the adaptive LDS levels follow the depth the
+    finished batches reached, the next batch's draws and bins are prefetched)."""
+    out = {"batch_packets": batch, "batches_timed": reps}
     with sf.Sphereflake(width, height) as s:
         s.SetCamera(sf.config_camera(width, height, k))
         for variant, lanes in (("avx", 8), ("sse", 4)):
             s.SetVariant(variant)
             s.Progressive(12345, batch, 0)
+            s.Synchronize()
+            s.Progressive(12345, batch)
             s.Synchronize()
             t = time.perf_counter()
             for _ in range(reps):
