@@ -43,8 +43,10 @@ def run(n, slots, split):
             c.close()
 
 
-for slots in (1, 3):
-    for split in ("auto", "model"):
+SLOTS = [int(v) for v in os.environ.get("PROBE_SLOTS", "1,3").split(",")]
+SPLITS = os.environ.get("PROBE_SPLITS", "auto,model").split(",")
+for slots in SLOTS:
+    for split in SPLITS:
         base = None
         row = []
         for n in (1, 2, 4, 8):

@@ -128,7 +128,7 @@ struct sf_ctx {
     uint32_t flags = 0;                          // SF_FLAG_* A/B switches: env SF_FLAGS
     int cus = 256;
     uint32_t queues = 8;                         // persistent trace: XCD queue groups, one per XCD (power of 2)
-    uint32_t queues_per_xcd = 1;                 // env SF_QUEUES_PER_XCD = 1 | 2 | 4: tile queues per XCD
+    uint32_t queues_per_xcd = 4;                 // env SF_QUEUES_PER_XCD = 1 | 2 | 4: tile queues per XCD (full grids)
     int pipe = -1;                               // env SF_PIPE = 0 | 1: latency variant of the trace (-1: auto)
     uint32_t prio_buckets = 8;                   // top cost buckets (3 octaves) traced at raised wave priority (env SF_PRIO_BUCKETS)
     int occ_key = -1, occ_blocks = 0;            // cached occupancy (waves per block, levels) -> blocks per CU
@@ -214,7 +214,12 @@ struct sf_ctx {
     // and downloads issued on different streams of one context run in call order, as on one stream.
     hipStream_t last_stream = nullptr; // stream of the latest enqueued work (nullptr: the context stream)
     hipEvent_t join_ev = nullptr;      // the point later calls order after (see ctx_join / StreamMark)
-    bool use_order = true;             // env SF_ORDER=0: row-major order always
+    // Heavy-first tile order: -1 (default) for frames whose tiles fill the persistent grid at most twice (small
+    // frames and multi-GPU shares, latency-bound: the heaviest tiles start first and may be split into parts),
+    // row-major on larger frames, where with frames in flight the order's kernels and per-tile cost recording
+    // cost more than the tail they shorten (round 3: 1080p 0.0816 -> 0.079 ms, 4K 0.382 -> 0.376 ms per frame);
+    // env SF_ORDER=0 never, SF_ORDER=1 always
+    int order_mode = -1;
     uint32_t order_every = 0;          // env SF_ORDER_EVERY = k: rebuild the order after every k-th render only
                                        // (0 = auto: 3 for small frames, 1 otherwise)
     uint32_t order_phase = 0;          // renders since the last rebuild
@@ -452,7 +457,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
         }
     }
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
-    if (const char* ev = std::getenv("SF_ORDER")) c->use_order = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_ORDER")) c->order_mode = std::atoi(ev) != 0 ? 1 : 0;
     if (const char* ev = std::getenv("SF_ORDER_EVERY")) c->order_every = std::atoi(ev) > 1 ? (uint32_t)std::atoi(ev) : 1u;   // (explicit)
     if (const char* ev = std::getenv("SF_PROG_BIN")) c->prog_bin = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_PREFETCH")) c->prog_prefetch = std::atoi(ev) != 0;
@@ -701,8 +706,10 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 c->occ_key = key;
             }
             uint32_t nblk = (uint32_t)c->occ_blocks * (uint32_t)c->cus;
+            const bool small = ntiles <= 2u * nblk * wpb;   // tiles fill the full persistent grid at most twice
+            const bool use_order = c->order_mode > 0 || (c->order_mode < 0 && small);
             // work units: tiles, or up to `split_parts` per tile when the schedule may split tiles
-            const uint32_t units_max = (c->use_order && c->split_buckets != 0u) ? c->split_parts * ntiles : ntiles;
+            const uint32_t units_max = (use_order && c->split_buckets != 0u) ? c->split_parts * ntiles : ntiles;
             const uint32_t need = (units_max + wpb - 1) / wpb;
             if (nblk > need) nblk = need;
             if (c->max_blocks && nblk > c->max_blocks) nblk = c->max_blocks;
@@ -721,11 +728,10 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             // order costs the trace nothing measurable while the two order kernels are ~5 us of a ~80 us
             // frame, so by default they are rebuilt after every 3rd render (640x360 -6 %, 1280x720 -4 %);
             // full grids are throughput-bound and a stale order costs more than the kernels (1080p).
-            const bool small = ntiles <= 2u * nblk * wpb;
             const uint32_t every = c->order_every ? c->order_every : (small ? 3u : 1u);
-            const bool rebuild = c->use_order && (c->order_n != ntiles || c->order_phase + 1u >= every);
-            if (c->use_order) c->order_phase = rebuild ? 0u : c->order_phase + 1u;
-            if (c->use_order) {
+            const bool rebuild = use_order && (c->order_n != ntiles || c->order_phase + 1u >= every);
+            if (use_order) c->order_phase = rebuild ? 0u : c->order_phase + 1u;
+            if (use_order) {
                 a.tile_cost = c->tile_cost;
                 a.chunk_cnt = rebuild ? c->chunk_cnt : nullptr;
                 a.part_cost = c->part_cost;

@@ -291,10 +291,12 @@ def test_progressive_prefetched_bins_follow_the_variant(monkeypatch):
     assert (st.max_depth, st.closest, st.rays) == (est.max_depth, est.closest, est.rays)
 
 
-def test_repeat_renders_heavy_first_order_bit_exact():
+def test_repeat_renders_heavy_first_order_bit_exact(monkeypatch):
     """From the second render on, the persistent kernel takes its tiles heaviest-first (costs of the
-    previous render, sf_tile_order). The image must not depend on the order: renders 2 and 3 of c3
-    equal the golden digests, and kernel timing reports one duration per render."""
+    previous render, sf_tile_order; SF_ORDER=1: on for this full-grid frame too). The image must not depend
+    on the order: renders 2 and 3 of c3 equal the golden digests, and kernel timing reports one duration per
+    render."""
+    monkeypatch.setenv("SF_ORDER", "1")
     fx = load_frame("c3")
     W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
     with sf.Sphereflake(W, H) as s:
@@ -504,7 +506,8 @@ def expected_units(cost, split_buckets, spare=0, parts=2, prio_buckets=8):
 def test_tile_order_is_stable_heavy_first_schedule(W, H, split, parts, monkeypatch):
     """The next render's work units (sf_order_scan + sf_order_scatter) are exactly the stable sort of
     the last render's tile costs by bucket, heaviest first, with the heaviest tiles as 2 or 4 part units:
-    every tile covered once (whole, or all its parts)."""
+    every tile covered once (whole, or all its parts). (SF_ORDER=1: the order on whatever the frame size.)"""
+    monkeypatch.setenv("SF_ORDER", "1")
     if split is not None:
         monkeypatch.setenv("SF_SPLIT_BUCKETS", str(split))
     monkeypatch.setenv("SF_SPLIT_PARTS", str(parts))
@@ -538,10 +541,11 @@ def test_tile_order_is_stable_heavy_first_schedule(W, H, split, parts, monkeypat
 def test_split_render_bit_exact_and_stable(parts, monkeypatch):
     """With part units in the schedule (renders 2+: halves or quarters), c3 stays bit-exact, splitting the
     heaviest bucket and with every tile split-eligible (SF_SPLIT_BUCKETS=32: the cap of one eighth of the
-    tiles applies)."""
+    tiles applies). (SF_ORDER=1: the order -- and with it the splits -- on for this full-grid frame.)"""
     fx = load_frame("c3")
     W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
     import os
+    monkeypatch.setenv("SF_ORDER", "1")
     monkeypatch.setenv("SF_SPLIT_PARTS", str(parts))
     for split in ("1", "32"):
         os.environ["SF_SPLIT_BUCKETS"] = split
@@ -634,7 +638,8 @@ def test_fewer_tile_queues_bit_exact(nq, monkeypatch):
 @pytest.mark.parametrize("prio", ["0", "1", "32"])
 def test_raised_priority_tiles_bit_exact(prio, monkeypatch):
     """The top SF_PRIO_BUCKETS cost buckets of the last render run at raised wave priority (none / the
-    top one / all): scheduling only, frames equal the golden."""
+    top one / all): scheduling only, frames equal the golden. (SF_ORDER=1: the order on for this full grid.)"""
+    monkeypatch.setenv("SF_ORDER", "1")
     monkeypatch.setenv("SF_PRIO_BUCKETS", prio)
     fx = load_frame("c3")
     W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
@@ -653,6 +658,22 @@ def test_raised_priority_tiles_bit_exact(prio, monkeypatch):
         assert lv.min() >= 1 and lv.max() == 2
     else:
         assert 0 < np.count_nonzero(lv) < len(units)
+
+
+@pytest.mark.parametrize("name,ordered", [("c1", True), ("c2", True), ("c3", False), ("c4", False)])
+def test_tile_order_auto_by_frame_size(name, ordered):
+    """Default tile order (sf_capi.hip order_mode -1): heavy-first for frames whose tiles fill the persistent
+    grid at most twice (c1, c2: latency-bound), row-major on larger ones (c3, c4: with frames in flight the order
+    costs more than it saves). Either way every render equals the golden frame."""
+    fx = load_frame(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for k in range(3):
+            s.Render()
+            pos, nrm, _, _ = s.download()
+            assert frame_digest(pos, nrm) == fx["frame_digest"], (name, k)
+        assert (s.tile_order() is not None) == ordered
 
 
 @pytest.mark.parametrize("name", ["c1", "c2", "c3", "c4"])
