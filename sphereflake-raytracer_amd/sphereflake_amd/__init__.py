@@ -248,6 +248,19 @@ def _fp(a: np.ndarray):
     return a.ctypes.data_as(_F)
 
 
+_F3 = ctypes.c_float * 3
+
+
+def _vec3(v):
+    """A view vector as a ctypes float[3] (the per-frame SetView path: a tuple or list of 3 numbers is converted
+    without numpy, ~6 us less host time per frame; float32 rounding as np.float32)."""
+    if isinstance(v, (tuple, list)) and len(v) == 3:
+        return _F3(*v)
+    if isinstance(v, np.ndarray) and v.dtype == np.float32 and v.shape == (3,):
+        return _F3(*v.tolist())
+    return _F3(*_f32(v, 3).ravel().tolist())
+
+
 # ----------------------------------------------------------------------------- host setup helpers
 
 def child_transforms() -> np.ndarray:
@@ -415,9 +428,9 @@ class Sphereflake:
 
     # view ------------------------------------------------------------------
     def SetView(self, origin, topLeft, topRight, bottomLeft):
-        o, tl, tr, bl = (_f32(v, 3) for v in (origin, topLeft, topRight, bottomLeft))
+        o, tl, tr, bl = (_vec3(v) for v in (origin, topLeft, topRight, bottomLeft))
         with self._mutex:   # (the frame-less loop's batches read the view)
-            _check(lib().sf_set_view(self._ctx, _fp(o), _fp(tl), _fp(tr), _fp(bl)), "SetView", self._ctx)
+            _check(lib().sf_set_view(self._ctx, o, tl, tr, bl), "SetView", self._ctx)
             self._view_change = self._counter
 
     def GetViewChangePacket(self) -> int:
@@ -749,8 +762,8 @@ class SphereflakeGroup:
         return lib().sf_group_member(self._g, k)
 
     def SetView(self, origin, topLeft, topRight, bottomLeft):
-        o, tl, tr, bl = (_f32(v, 3) for v in (origin, topLeft, topRight, bottomLeft))
-        self._check(lib().sf_group_set_view(self._g, _fp(o), _fp(tl), _fp(tr), _fp(bl)), "sf_group_set_view")
+        o, tl, tr, bl = (_vec3(v) for v in (origin, topLeft, topRight, bottomLeft))
+        self._check(lib().sf_group_set_view(self._g, o, tl, tr, bl), "sf_group_set_view")
 
     def SetCamera(self, cam: Camera):
         self.SetView(*cam.corners())
@@ -852,8 +865,8 @@ class SphereflakeDist:
         return lib().sf_dist_last_slot(self._d)
 
     def SetView(self, origin, topLeft, topRight, bottomLeft):
-        o, tl, tr, bl = (_f32(v, 3) for v in (origin, topLeft, topRight, bottomLeft))
-        self._check(lib().sf_dist_set_view(self._d, _fp(o), _fp(tl), _fp(tr), _fp(bl)), "sf_dist_set_view")
+        o, tl, tr, bl = (_vec3(v) for v in (origin, topLeft, topRight, bottomLeft))
+        self._check(lib().sf_dist_set_view(self._d, o, tl, tr, bl), "sf_dist_set_view")
 
     def SetCamera(self, cam: Camera):
         self.SetView(*cam.corners())
