@@ -29,7 +29,8 @@ for rep in range(2):
     for slots in SLOTS:
         row = []
         for n in NS:
-            r = bench.dist_loop(ctl, torch, dev, bench.W, bench.H, bench.K, 200, 30, slots, 8, n, lambda i: i)
+            r = bench.dist_loop(ctl, torch, dev, bench.W, bench.H, bench.K, 200, 30, slots, 8, n, lambda i: i,
+                                settle_ms=float(os.environ.get("SHARE_SETTLE_MS", bench.SETTLE_MS)))
             r["dist"].close()
             row.append(f"N={n} {r['t_step'] * 1e3:.4f} ms")
         print(f"slots={slots}: " + "  ".join(row), flush=True)

@@ -17,7 +17,7 @@ import sphereflake_amd as sf  # noqa: E402
 from bench import frame_camera  # noqa: E402
 
 W, H, K = (int(sys.argv[1]), int(sys.argv[2]), float(sys.argv[3])) if len(sys.argv) > 3 else (1920, 1080, 0.25)
-STEPS, WARM = 120, 30
+STEPS, WARM = int(os.environ.get("PROBE_STEPS", 120)), int(os.environ.get("PROBE_WARM", 30))
 if os.environ.get("PROBE_TORCH"):   # A/B: the HIP runtime as a torch process has it (bench.py)
     import torch
     torch.cuda.set_device(0)

@@ -25,10 +25,11 @@ extern "C" __global__ void sf_trace_queue1(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2(FrameArgs a);
 extern "C" __global__ void sf_trace_queue4(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2p(FrameArgs a);
-extern "C" __global__ void sf_order_scan(const uint32_t* chunk_cnt, uint32_t nc, uint32_t n_tiles,
+extern "C" __global__ void sf_order_scan(uint32_t* chunk_cnt, uint32_t nc, uint32_t n_tiles,
                                          uint32_t split_buckets, uint32_t parts, uint32_t spare, uint32_t waves,
                                          uint32_t prio_buckets,
-                                         uint32_t* chunk_off, uint32_t* order_meta);
+                                         uint32_t* chunk_off, uint32_t* order_meta, const uint32_t* fuse_cost,
+                                         uint32_t* fuse_order);
 extern "C" __global__ void sf_order_scatter(const uint32_t* cost, uint32_t n, uint32_t* chunk_cnt,
                                             const uint32_t* chunk_off, const uint32_t* order_meta, uint32_t* order,
                                             uint32_t* rank_out);
@@ -763,14 +764,20 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 const uint32_t nc = (ntiles + 63u) / 64u;
                 const uint32_t waves = nblk * wpb;   // resident waves of the persistent grid
                 const uint32_t spare = waves > ntiles ? waves - ntiles : 0u;
-                hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->chunk_cnt, nc, ntiles,
+                // few chunks: the scan's workgroup also scatters (one launch: ~3 us less host time and one
+                // dispatch less on the frame's stream); more: one wave per chunk in a launch of its own
+                const bool fuse = nc <= SF_ORDER_FUSE_CHUNKS;
+                hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, c->chunk_cnt, nc, ntiles,
                                    c->split_buckets, c->split_parts, spare, waves, c->prio_buckets, c->chunk_off,
-                                   c->order_meta);
+                                   c->order_meta, fuse ? (const uint32_t*)c->tile_cost : nullptr,
+                                   fuse ? c->tile_order : nullptr);
                 SF_HIP(c, hipGetLastError());
-                hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost, ntiles,
-                                   c->chunk_cnt, (const uint32_t*)c->chunk_off, (const uint32_t*)c->order_meta,
-                                   c->tile_order, nullptr);
-                SF_HIP(c, hipGetLastError());
+                if (!fuse) {
+                    hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost, ntiles,
+                                       c->chunk_cnt, (const uint32_t*)c->chunk_off, (const uint32_t*)c->order_meta,
+                                       c->tile_order, nullptr);
+                    SF_HIP(c, hipGetLastError());
+                }
                 c->order_n = ntiles;
             }
         } else {
@@ -1039,8 +1046,9 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
             if (c->bin_key == key) {
                 hipLaunchKernelGGL(sf_bin_hist, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->bin_cost, nbins,
                                    c->bin_chunk_cnt);
-                hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)c->bin_chunk_cnt, nc, nbins,
-                                   0u, 2u, 0u, 0u, 0u, c->bin_chunk_off, c->bin_meta);
+                hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, c->bin_chunk_cnt, nc, nbins,
+                                   0u, 2u, 0u, 0u, 0u, c->bin_chunk_off, c->bin_meta, (const uint32_t*)nullptr,
+                                   (uint32_t*)nullptr);
                 hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->bin_cost, nbins,
                                    c->bin_chunk_cnt, (const uint32_t*)c->bin_chunk_off, (const uint32_t*)c->bin_meta,
                                    c->bin_order, c->bin_rank);

@@ -209,6 +209,11 @@ struct PostArgs {
 // (1920x1080: 32400 tiles, 7168 waves) nothing is split -- measured: splitting there costs +1.5-3.5 %;
 // at 640x360 (3600 tiles) it takes the frame from 0.198 to 0.144 ms.
 #define SF_SPLIT_AUTO 0xffffffffu
+// tile orders of at most this many 64-tile chunks are scattered by sf_order_scan's own workgroup (8 chunks per
+// wave at most); larger ones by sf_order_scatter, one wave per chunk
+#ifndef SF_ORDER_FUSE_CHUNKS
+#define SF_ORDER_FUSE_CHUNKS 128u
+#endif
 // env SF_SPLIT_BUCKETS=model: split the buckets a makespan model of the last render's costs says shorten the
 // frame (sf_order_scan) -- also on full grids, where the heaviest tile exceeds the slots' fair share
 #define SF_SPLIT_MODEL 0xfffffffeu

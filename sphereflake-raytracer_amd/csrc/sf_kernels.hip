@@ -1757,14 +1757,52 @@ extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(
 // per-(chunk, bucket) output offsets, heaviest bucket first and chunks in order within a bucket;
 // sf_order_scatter (one wave per chunk) writes the permutation and clears the histograms. Stable and
 // deterministic. Any permutation gives the same image: only the schedule changes.
+// One 64-item chunk c of the scatter, one wave (lane = item within the chunk).
+// (rank_out, when not NULL: rank_out[i] = item i's position, the inverse permutation; unsplit orders only)
+__device__ __forceinline__ void order_scatter_chunk(uint32_t c, uint32_t lane, const uint32_t* __restrict__ cost,
+                                                    uint32_t n, uint32_t* __restrict__ chunk_cnt,
+                                                    const uint32_t* __restrict__ chunk_off, uint32_t split_from,
+                                                    uint32_t parts, uint32_t pb, uint32_t* __restrict__ order,
+                                                    uint32_t* __restrict__ rank_out)
+{
+    const uint32_t i = c * 64u + lane;
+    const uint32_t first = parts == 4u ? SF_PART_QUARTER0 : SF_PART_HALF0;
+    const uint32_t bk = i < n ? cost_bucket(cost[i]) : SF_ORDER_BUCKETS;   // sentinel: no tile
+    const uint32_t offs = chunk_off[c * SF_ORDER_BUCKETS + (lane & (SF_ORDER_BUCKETS - 1u))];   // lane b: bucket b
+    uint64_t pending = __builtin_amdgcn_ballot_w64(bk < SF_ORDER_BUCKETS);
+    while (pending) {   // one round per distinct bucket in the chunk
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)bk, (int)__builtin_ctzll(pending));
+        const uint64_t m = __builtin_amdgcn_ballot_w64(bk == b);
+        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)offs, (int)b);
+        if (bk == b) {
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            // the unit's wave priority next render (see SF_UNIT_PRIO_SHIFT)
+            const uint32_t u = i | ((b >= pb + 3u ? 2u : b >= pb ? 1u : 0u) << SF_UNIT_PRIO_SHIFT);
+            if (b >= split_from) {   // `parts` part units, adjacent
+                for (uint32_t p = 0; p < parts; ++p) order[off + parts * rank + p] = u | ((first + p) << SF_UNIT_PART_SHIFT);
+            } else {
+                order[off + rank] = u;
+                if (rank_out) rank_out[i] = off + rank;
+            }
+        }
+        pending &= ~m;
+    }
+    if (lane < SF_ORDER_BUCKETS) chunk_cnt[c * SF_ORDER_BUCKETS + lane] = 0u;   // for the next render
+}
+
 #define SF_SCAN_BATCH 16   // chunk counts a scan thread loads at once (independent loads, one wait)
 
-extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t* __restrict__ chunk_cnt, uint32_t nc,
+extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(uint32_t* __restrict__ chunk_cnt, uint32_t nc,
                                                                    uint32_t n_tiles, uint32_t split_buckets, uint32_t parts,
                                                                    uint32_t spare, uint32_t waves, uint32_t prio_buckets,
                                                                    uint32_t* __restrict__ chunk_off,
-                                                                   uint32_t* __restrict__ order_meta)
+                                                                   uint32_t* __restrict__ order_meta,
+                                                                   const uint32_t* __restrict__ fuse_cost,
+                                                                   uint32_t* __restrict__ fuse_order)
 {
+    // fuse_cost / fuse_order not NULL: this workgroup also does sf_order_scatter's work afterwards (its 16 waves
+    // over the chunks), one launch instead of two -- for frames of few chunks, where the second launch's host
+    // cost and dispatch latency exceed the scatter itself
     // (with frames in flight this one workgroup shares the CUs with other frames' trace waves, whose heavy
     // tiles run at raised priority: without its own it waited ~125 us instead of ~8 for issue slots)
     __builtin_amdgcn_s_setprio(3);
@@ -1894,6 +1932,14 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(const uint32_t*
             off += v[j] * mult;
         }
     }
+    if (fuse_order) {
+        // chunk_off and the counts were written / read by this workgroup only: a workgroup barrier orders them
+        __syncthreads();
+        const uint32_t pb = order_meta[3];
+        for (uint32_t c = tid >> 6; c < nc; c += blockDim.x >> 6)
+            order_scatter_chunk(c, tid & 63u, fuse_cost, n_tiles, chunk_cnt, chunk_off, split_from, parts, pb,
+                                fuse_order, nullptr);
+    }
 }
 
 extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t* __restrict__ cost, uint32_t n,
@@ -1903,32 +1949,9 @@ extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t
                                                                     uint32_t* __restrict__ order,
                                                                     uint32_t* __restrict__ rank_out)
 {
-    // (rank_out, when not NULL: rank_out[i] = item i's position, the inverse permutation; unsplit orders only)
     __builtin_amdgcn_s_setprio(3);   // (see sf_order_scan)
-    const uint32_t c = blockIdx.x, lane = threadIdx.x, i = c * 64u + lane;
-    const uint32_t split_from = order_meta[1], parts = order_meta[2], pb = order_meta[3];
-    const uint32_t first = parts == 4u ? SF_PART_QUARTER0 : SF_PART_HALF0;
-    const uint32_t bk = i < n ? cost_bucket(cost[i]) : SF_ORDER_BUCKETS;   // sentinel: no tile
-    const uint32_t offs = chunk_off[c * SF_ORDER_BUCKETS + (lane & (SF_ORDER_BUCKETS - 1u))];   // lane b: bucket b
-    uint64_t pending = __builtin_amdgcn_ballot_w64(bk < SF_ORDER_BUCKETS);
-    while (pending) {   // one round per distinct bucket in the chunk
-        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)bk, (int)__builtin_ctzll(pending));
-        const uint64_t m = __builtin_amdgcn_ballot_w64(bk == b);
-        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)offs, (int)b);
-        if (bk == b) {
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            // the unit's wave priority next render (see SF_UNIT_PRIO_SHIFT)
-            const uint32_t u = i | ((b >= pb + 3u ? 2u : b >= pb ? 1u : 0u) << SF_UNIT_PRIO_SHIFT);
-            if (b >= split_from) {   // `parts` part units, adjacent
-                for (uint32_t p = 0; p < parts; ++p) order[off + parts * rank + p] = u | ((first + p) << SF_UNIT_PART_SHIFT);
-            } else {
-                order[off + rank] = u;
-                if (rank_out) rank_out[i] = off + rank;
-            }
-        }
-        pending &= ~m;
-    }
-    if (lane < SF_ORDER_BUCKETS) chunk_cnt[c * SF_ORDER_BUCKETS + lane] = 0u;   // for the next render
+    order_scatter_chunk(blockIdx.x, threadIdx.x, cost, n, chunk_cnt, chunk_off, order_meta[1], order_meta[2],
+                        order_meta[3], order, rank_out);
 }
 
 // Packed band slabs -> the frame G-buffer (multi-GPU gather). `stage` holds `members` slabs

@@ -506,17 +506,24 @@ def expected_units(cost, split_buckets, spare=0, parts=2, prio_buckets=8):
 def test_tile_order_is_stable_heavy_first_schedule(W, H, split, parts, monkeypatch):
     """The next render's work units (sf_order_scan + sf_order_scatter) are exactly the stable sort of
     the last render's tile costs by bucket, heaviest first, with the heaviest tiles as 2 or 4 part units:
-    every tile covered once (whole, or all its parts). (SF_ORDER=1: the order on whatever the frame size.)"""
+    every tile covered once (whole, or all its parts). (SF_ORDER=1: the order on whatever the frame size.)
+    Three renders, each rebuilding the order (SF_ORDER_EVERY=1), so the cleared histograms are covered too, for
+    orders scattered by the scan's own workgroup (<= SF_ORDER_FUSE_CHUNKS chunks) and by sf_order_scatter."""
     monkeypatch.setenv("SF_ORDER", "1")
+    monkeypatch.setenv("SF_ORDER_EVERY", "1")
     if split is not None:
         monkeypatch.setenv("SF_SPLIT_BUCKETS", str(split))
     monkeypatch.setenv("SF_SPLIT_PARTS", str(parts))
-    n = ((W + 7) // 8) * ((H + 7) // 8)
     with sf.Sphereflake(W, H) as s:
         s.SetCamera(sf.config_camera(W, H, 0.25))
         assert s.tile_order() is None
-        s.Render()
-        units, cost = s.tile_order()
+        for _ in range(3):
+            s.Render()
+            check_tile_order(W, H, split, parts, *s.tile_order())
+
+
+def check_tile_order(W, H, split, parts, units, cost):
+    n = ((W + 7) // 8) * ((H + 7) // 8)
     if split is None:   # auto: recover the idle-wave count from the split made (<= spare < next bucket)
         n_extra = len(units) - n
         exp, nsplit = expected_units(cost, None, n_extra, parts)
