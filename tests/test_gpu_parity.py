@@ -358,7 +358,9 @@ def test_order_rebuilt_every_kth_render_bit_exact(monkeypatch, every):
     """SF_ORDER_EVERY=k: renders between two order rebuilds record tile costs without the histogram and
     keep the last order (sf_capi.hip `rebuild`). Every render still equals the golden c2 frame, the kept
     order stays a valid permutation of the tiles, and a rebuild after skipped renders gives the order of
-    the costs it was built from (no histogram counts carried over from the skipped renders)."""
+    the costs it was built from (no histogram counts carried over from the skipped renders). (SF_ORDER=1: c2
+    is not ordered by default.)"""
+    monkeypatch.setenv("SF_ORDER", "1")
     monkeypatch.setenv("SF_ORDER_EVERY", every)
     fx = load_frame("c2")
     W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
@@ -667,11 +669,11 @@ def test_raised_priority_tiles_bit_exact(prio, monkeypatch):
         assert 0 < np.count_nonzero(lv) < len(units)
 
 
-@pytest.mark.parametrize("name,ordered", [("c1", True), ("c2", True), ("c3", False), ("c4", False)])
+@pytest.mark.parametrize("name,ordered", [("c1", True), ("c2", False), ("c3", False), ("c4", False)])
 def test_tile_order_auto_by_frame_size(name, ordered):
-    """Default tile order (sf_capi.hip order_mode -1): heavy-first for frames whose tiles fill the persistent
-    grid at most twice (c1, c2: latency-bound), row-major on larger ones (c3, c4: with frames in flight the order
-    costs more than it saves). Either way every render equals the golden frame."""
+    """Default tile order (sf_capi.hip order_mode -1): heavy-first for frames whose tiles fill at most half the
+    persistent grid's waves (c1: 3 600 tiles for 8 192 waves), row-major on larger ones (c2..c4: with frames in
+    flight the order costs more than it saves). Either way every render equals the golden frame."""
     fx = load_frame(name)
     W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
     with sf.Sphereflake(W, H) as s:
