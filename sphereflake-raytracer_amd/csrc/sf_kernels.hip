@@ -1107,6 +1107,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
     auto expand = [&](const float4 pc, const float* col, uint32_t cs, uint32_t d, float actv, uint32_t& leafm) -> uint32_t {
         d = __builtin_amdgcn_readfirstlane(d);
         SF_COUNT(0, 1);
+        SF_COUNT(7, __builtin_popcountll(wave_ballot(actv >= 0.0f)));   // (COUNTS builds: lanes visiting the node)
         lds_fence();
         const float3 p0 = *reinterpret_cast<const float3*>(col);
         const float3 p1 = *reinterpret_cast<const float3*>(col + cs);
@@ -1207,6 +1208,16 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             const bool hb = __builtin_fminf(__builtin_fminf(tca, xs), actv) >= 0.0f;
             const uint64_t hbm = wave_ballot(hb);
             SF_COUNT(1, 1);
+#ifdef SF_COUNTS
+            {   // lane utilisation of the child loop (COUNTS builds only)
+                const uint32_t na = __builtin_popcountll(wave_ballot(actv >= 0.0f));
+                SF_COUNT(5, na);
+                SF_COUNT(6, __builtin_popcountll(hbm));
+                SF_COUNT(10, d >= 4u ? 1 : 0);
+                SF_COUNT(11, d >= 4u ? na : 0);
+                SF_COUNT(14, na <= 32u ? 1 : 0);
+            }
+#endif
             if (hbm == 0ull) {
                 SF_COUNT(2, 1);
                 continue;

@@ -285,3 +285,23 @@ def test_division_by_reciprocal_exact(n):
         r = _rn32(Fraction(int(x)) - Fraction(float(q0)) * n)          # fma(-q0, n, x)
         q = _rn32(Fraction(float(q0)) + Fraction(float(r)) * Fraction(float(y)))   # fma(r, y, q0)
         assert q == np.float32(fx / fn), (n, x)
+
+
+@pytest.mark.parametrize("v", [(0.1, -2.5, 3e38), [np.float32(1.1), 2, -0.0], np.array([1.1, 2.0, 3.0]),
+                               np.array([[1e39], [-1e-46], [7.0]]), np.array([0.3, 0.2, 0.1], np.float32),
+                               (float("nan"), float("inf"), -1.0)])
+def test_view_vector_conversion_matches_float32(v):
+    """SetView's ctypes float[3] (sphereflake_amd._vec3, no numpy on the per-frame path) holds exactly the
+    float32 values np.float32 conversion gives (round to nearest, overflow to inf, underflow to 0)."""
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        exp = np.asarray(v, np.float32).ravel()
+    got = np.array(list(sf._vec3(v)), np.float32)
+    assert np.array_equal(got.view(np.uint32), exp.view(np.uint32))
+
+
+@pytest.mark.parametrize("v", [(1.0, 2.0), [1.0, 2.0, 3.0, 4.0], np.zeros(4), np.zeros((2, 2))])
+def test_view_vector_conversion_rejects_wrong_size(v):
+    with pytest.raises(ValueError):
+        sf._vec3(v)
