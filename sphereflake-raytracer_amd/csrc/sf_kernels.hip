@@ -1999,6 +1999,9 @@ extern "C" __global__ __launch_bounds__(64) void sf_fixup_wave(FrameArgs a, cons
     extern __shared__ float lds[];
     if (blockIdx.x == 0 && threadIdx.x == 0) counters[parity ^ 1u] = 0u;
     const uint32_t n = counters[parity];
+    // workgroups without a tile leave at once (the usual case: no tile flagged), before the LDS setup: this
+    // kernel sits between a frame's trace and the next render of its slot
+    if (blockIdx.x >= n) return;
     int32_t maxd = -1;
     float closest = FLT_MAX;
     uint32_t unresolved = 0u;
