@@ -713,7 +713,10 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             // frames in flight, frames of more tiles are throughput-bound and the order costs more than it
             // gains: 1280x720 0.039 -> 0.036 ms, a 1080p member's share over 2 / 4 GPUs 0.045 -> 0.042 /
             // 0.028 -> 0.026 ms without it, while 640x360 keeps it (0.0203 vs 0.0232 ms on a fixed view).
-            const bool tiny = 2u * ntiles <= nblk * wpb;
+            // A member's share of a multi-GPU frame (band_count > 1) stays row-major too: its tiles are every N-th
+            // band row of the frame, and with frames in flight the order measured slower there at every N (1080p
+            // over 8 GPUs: 0.0212 vs 0.0204 ms per frame, `profiles/r3/share2/r3aw.txt`).
+            const bool tiny = 2u * ntiles <= nblk * wpb && band_count == 1u;
             const bool use_order = c->order_mode > 0 || (c->order_mode < 0 && tiny);
             // work units: tiles, or up to `split_parts` per tile when the schedule may split tiles
             const uint32_t units_max = (use_order && c->split_buckets != 0u) ? c->split_parts * ntiles : ntiles;
