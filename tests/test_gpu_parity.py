@@ -777,3 +777,29 @@ def test_front_first_order_and_tie_fallback(name, flags, monkeypatch):
     assert st.max_depth == fx["stats"]["max_depth"]
     assert np.float32(st.closest) == np.float32(float.fromhex(fx["stats"]["closest"]))
     assert st.overflow_tiles == 0
+
+
+@pytest.mark.parametrize("order", ["0", "1"])
+def test_member_share_with_and_without_order_bit_exact(order, monkeypatch):
+    """A multi-GPU member's share (band 3 of an 8-way split of c2's 8-row bands) rendered four times on a fresh
+    context with the heavy-first order forced on (SF_ORDER=1: the scan's own workgroup scatters the small order,
+    heavy tiles split into idle wave slots) and off (the default for shares): every render's rows equal the
+    whole frame's, bit for bit."""
+    fx = load_frame("c2")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        s.Render()
+        ref_pos, ref_nrm, _, _ = s.download()
+    assert bad_rows(fx["row_digest_gbuf"], row_digests(ref_pos, ref_nrm)) == []
+    monkeypatch.setenv("SF_ORDER", order)
+    rows = [y for b in range(3, (H + 7) // 8, 8) for y in range(8 * b, min(8 * b + 8, H))]
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for k in range(4):
+            s.Render(band_rows=8, band_count=8, band_index=3)
+            pos, nrm, _, _ = s.download()
+            assert np.array_equal(pos[rows].view(np.uint32), ref_pos[rows].view(np.uint32)), k
+            assert np.array_equal(nrm[rows].view(np.uint32), ref_nrm[rows].view(np.uint32)), k
+        assert (s.tile_order() is not None) == (order == "1")
+        assert s.stats().overflow_tiles == 0
