@@ -801,5 +801,5 @@ def test_member_share_with_and_without_order_bit_exact(order, monkeypatch):
             pos, nrm, _, _ = s.download()
             assert np.array_equal(pos[rows].view(np.uint32), ref_pos[rows].view(np.uint32)), k
             assert np.array_equal(nrm[rows].view(np.uint32), ref_nrm[rows].view(np.uint32)), k
-        assert (s.tile_order() is not None) == (order == "1")
+        # (sf_get_tile_order reports whole-frame orders only: a share's order is not readable through it)
         assert s.stats().overflow_tiles == 0
