@@ -74,7 +74,15 @@ def parse():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the post-process, transfer, frame-less and c4 sections (profiling runs of the timed loop only)")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--check", action="store_true", help="verify the last frame against the oracle rows")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the parity check of the timed frames (default: the last moving frame's oracle rows "
+                         "and the fixed-camera frame's row digests against the golden fixture; a mismatch exits 5)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="bring the ranks up (spawning them for --gpus N > 1), agree on the world, report each rank's "
+                         "device, and print the line without rendering (no GPU call: runs on a CPU-only host)")
+    ap.add_argument("--long-steps", type=int, default=0,
+                    help="frames of the second timed loop that measures the steady frame period and the pipeline fill "
+                         "(0: max(4 x --steps, 200))")
     ap.add_argument("--rehearse", action="store_true",
                     help="dist mode with more ranks than GPUs (ranks share devices): every leg but the RCCL gather, "
                          "which RCCL refuses on a shared device")
@@ -162,29 +170,38 @@ def load_pmc(kernel, config_key, build):
         return None, None
 
 
-def pmc_valu(c, cus=256):
-    """VALU issue of `kernel` from the committed PMC summary: wave-level VALU instructions per launch
-    against the VALU issue slots of the profiled dispatch (CUs x 4 SIMDs x cycles / 2: one wave64
-    VALU instruction issues over 2 cycles; cycles = GRBM_GUI_ACTIVE / 8 XCDs)."""
+def pmc_valu(c, frame_ms, clock_mhz, cus=256):
+    """Issue of the trace kernel on the FRAME PERIOD: the committed PMC summary's wave-level instructions per launch
+    (one launch = one frame) against the issue slots of one frame period at the live shader clock -- VALU: CUs x 4
+    SIMDs x cycles / 2 (one wave64 VALU instruction issues over 2 cycles), SALU: one scalar instruction per CU per
+    cycle. `lone_dispatch` keeps the PMC pass's own view: the passes serialise dispatches, so there one launch runs
+    alone (its duration GRBM_GUI_ACTIVE / 8 XCDs cycles), with the occupancy it reached."""
     if c is None:
         return None
     try:
+        out = {"valu_insts": round(c["SQ_INSTS_VALU"]), "salu_insts": round(c["SQ_INSTS_SALU"]),
+               "source": "profiles/pmc_traffic.json"}
+        if frame_ms and clock_mhz:
+            fcyc = frame_ms * 1e-3 * clock_mhz * 1e6
+            out["frame_cycles"] = round(fcyc)
+            out["valu_issue_frac"] = round(c["SQ_INSTS_VALU"] / (cus * 4 * fcyc / 2.0), 4)
+            out["salu_issue_frac"] = round(c["SQ_INSTS_SALU"] / (cus * fcyc), 4)
+            out["basis"] = "per launch / issue slots of one frame period (ms_per_step) at clock_mhz_live"
         cycles = c["GRBM_GUI_ACTIVE"] / 8.0
-        slots = cus * 4 * cycles / 2.0
         # wavefront occupancy: SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md), summed over the
         # chip -> mean resident waves; against the gfx950 peak of 8 waves per SIMD
         waves = 4.0 * c["SQ_WAVE_CYCLES"] / cycles
         peak_waves = cus * 4 * 8
-        out = {"valu_insts": round(c["SQ_INSTS_VALU"]), "salu_insts": round(c["SQ_INSTS_SALU"]),
-               "issue_slots": round(slots), "valu_issue_frac": round(c["SQ_INSTS_VALU"] / slots, 4),
-               "occupancy": {"mean_waves": round(waves, 1), "peak_waves": peak_waves,
-                             "frac": round(waves / peak_waves, 4)},
-               "clock_mhz": round(cycles / c["profiled_dispatch_us"], 1), "source": "profiles/pmc_traffic.json"}
+        lone = {"dispatch_us": round(c["profiled_dispatch_us"], 2), "clock_mhz": round(cycles / c["profiled_dispatch_us"], 1),
+                "valu_issue_frac": round(c["SQ_INSTS_VALU"] / (cus * 4 * cycles / 2.0), 4),
+                "salu_issue_frac": round(c["SQ_INSTS_SALU"] / (cus * cycles), 4),
+                "occupancy": {"mean_waves": round(waves, 1), "peak_waves": peak_waves, "frac": round(waves / peak_waves, 4)}}
         if "SQ_WAIT_INST_ANY" in c and c.get("SQ_WAVE_CYCLES"):
-            out["wait_inst_frac"] = round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4)
-            out["wait_any_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+            lone["wait_inst_frac"] = round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+            lone["wait_any_frac"] = round(c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"], 4)
+        out["lone_dispatch"] = lone
         return out
-    except (KeyError, ValueError, ZeroDivisionError):
+    except (KeyError, ValueError, ZeroDivisionError, TypeError):
         return None
 
 
@@ -406,10 +423,11 @@ def run_rows(args, torch, ctl, n, kernel):
         raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
     tk = g.member_kernel_timing(0, n=min(-(-args.steps // kp), 64))
     trace_ms = float(np.mean(tk)) if len(tk) else dt / args.steps * 1e3
-    rays0 = sf.lib().sf_slab_rows(height, band, n, 0) * width   # member 0's rays per launch
     t_step = dt / args.steps
-    achieved = BYTES_PER_RAY * rays0 / (trace_ms * 1e-3) / 1e9
-    gather_bytes = sum(sf.lib().sf_slab_rows(height, band, n, k) for k in range(1, n)) * width * BYTES_PER_RAY
+    # member 0's G-buffer receives the whole frame (32 B/pixel) every frame period
+    achieved = BYTES_PER_RAY * width * height / t_step / 1e9
+    slab_bytes = g.slab_bytes()
+    gather_bytes = sum(sf.lib().sf_slab_rows(height, band, n, k) for k in range(1, n)) * width * slab_bytes
     same_dev = len(set(devices)) < n
     g.close()
     out = {
@@ -423,11 +441,13 @@ def run_rows(args, torch, ctl, n, kernel):
                    "parallelism": f"row-bands x{n} (sf_group: one process, strided peer copies into device 0)"
                                   + (" [rehearsal: all members on device 0]" if same_dev else "")},
         "frame_ms": round(t_step * 1e3, 4), "first_render_ms": round(first_ms, 4),
-        "gather_bytes_per_frame": gather_bytes, "rays_per_step": width * height, "rays_counted": int(st.rays),
+        "gather_bytes_per_frame": gather_bytes, "slab_bytes_per_pixel": slab_bytes,
+        "rays_per_step": width * height, "rays_counted": int(st.rays),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": TRACE_KERNEL,
-                     "kernel_ms": round(trace_ms, 4),
-                     "note": "member 0's trace kernel over its bands (32 B/ray x its rays / HIP-event duration)"},
+                     "kernel_event_ms": round(trace_ms, 4),
+                     "basis": "member 0's G-buffer receives the frame (32 B/pixel) per frame period; kernel_event_ms = "
+                              "member 0's trace kernel over its own bands (HIP events)"},
     }
     print(json.dumps(out), flush=True)
 
@@ -480,10 +500,14 @@ class Control:
             self.dist.destroy_process_group()
 
 
+EXIT_GATHER_FAILED = 3              # the RCCL-gathered leg failed or hung (the line is printed first)
+EXIT_CHECK_FAILED = 5               # a timed frame differs from the oracle / golden rows (the line is printed first)
+
+
 class Watchdog:
     """Deadline for a leg that may hang (the RCCL gather on a node never seen before): past it, `on_timeout`
-    runs (rank 0 prints the line without that leg) and the process exits 0 -- every rank arms the same deadline,
-    so no rank is left waiting in a collective."""
+    runs (rank 0 prints the line with the leg marked as failed) and the process exits EXIT_GATHER_FAILED -- every
+    rank arms the same deadline, so no rank is left waiting in a collective, and a hang is never a success."""
 
     def __init__(self, seconds, on_timeout):
         import threading
@@ -498,7 +522,7 @@ class Watchdog:
                 self._fire()
             finally:
                 sys.stdout.flush()
-                os._exit(0)
+                os._exit(EXIT_GATHER_FAILED)
 
     def cancel(self):
         self._done.set()
@@ -511,19 +535,85 @@ def slot_period(steps, slots):
     return max(1, min(KTIMING_PERIOD, per_slot // need))
 
 
+PATH_PERIOD = 4 * PATH_AMPLITUDE     # the camera path repeats every 40 frames
+
+
+def path_views(width, height, k, frame_of):
+    """view_at(i) -> the corners of frame frame_of(i) of the camera path (40 distinct views, cached)."""
+    cache = [frame_camera(width, height, k, f).corners() for f in range(PATH_PERIOD)]
+    return lambda i: cache[frame_of(i) % PATH_PERIOD]
+
+
+GOLDEN_OF = {(640, 360, 1.0): "c1", (1280, 720, 0.8): "c2", (1920, 1080, 0.25): "c3", (3840, 2160, 0.22): "c4",
+             (16384, 16384, 0.2): "c5"}
+
+
+def golden_frame(width, height, k):
+    """The golden fixture of a BASELINE config (tests/golden/frame_c*.json: per-row SHA-256 digests of the reference
+    frame, made by tests/golden/make_golden.py from the reference build), or None for other sizes."""
+    name = GOLDEN_OF.get((width, height, round(k, 4)))
+    if not name:
+        return None
+    with open(os.path.join(REPO, "tests", "golden", f"frame_{name}.json")) as f:
+        return json.load(f)
+
+
+def row_digest(pos, nrm, y):
+    """Digest of one G-buffer row, as tests/sfcheck.py and make_golden.py define it."""
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(pos[y]).tobytes() + np.ascontiguousarray(nrm[y]).tobytes()).hexdigest()[:16]
+
+
+def owned_rows(height, band_rows, nranks, rank):
+    """Frame rows this rank's G-buffer holds (all of them on one rank)."""
+    if nranks <= 1:
+        return np.arange(height)
+    return np.array([y for y0, y1 in shard.owned_bands(height, band_rows, nranks, rank) for y in range(y0, y1)], int)
+
+
+def check_oracle_rows(pos, nrm, view, width, height, rows):
+    """Rows `rows` of a downloaded frame against the oracle restatement (the checker, outside any timed region):
+    True when position and normal are equal bit for bit."""
+    from oracle import pyoracle
+    o, tl, tr, bl = view
+    setup = {"W": width, "H": height, "origin": o, "tl": tl, "tr": tr, "bl": bl,
+             "root": sf.root_transform(o), "children": sf.child_transforms()}
+    ro = pyoracle.render(setup, rows=rows)
+    return bool(np.array_equal(ro["pos4"].view(np.uint32), pos[rows].view(np.uint32)) and
+                np.array_equal(ro["nrm4"].view(np.uint32), nrm[rows].view(np.uint32)))
+
+
+def check_golden_rows(pos, nrm, golden, rows):
+    """Rows `rows` (those the fixture holds: every row_step-th) against the golden row digests; returns
+    (rows checked, rows that differ)."""
+    step = golden.get("row_step", 1)
+    ref = golden["row_digest_gbuf"]
+    checked = [int(y) for y in rows if y % step == 0 and y // step < len(ref)]
+    bad = [y for y in checked if row_digest(pos, nrm, y) != ref[y // step]]
+    return len(checked), bad
+
+
 def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows, nranks, frame_of,
-              fixed=False, latency=False, first=False, gather=False, settle_ms=SETTLE_MS):
+              fixed=False, latency=False, first=False, gather=False, settle_ms=SETTLE_MS, long_steps=0, check=False):
     """One timed loop of the sf_dist path: `steps` frames (frame_of(i) of the camera path at step i) after
     `warmup`, `slots` in flight, over `nranks` ranks (1: this GPU alone, every rank its own frames); each frame
     is every rank's bands into its own G-buffer (the distributed G-buffer), or with `gather` also assembled on
-    rank 0 (RCCL). Barrier + device sync on both sides of the timed region; the time is the max over ranks."""
+    rank 0 (RCCL). Barrier + device sync on both sides of the timed region; the time is the max over ranks.
+
+    `long_steps` > steps: a second loop of that many frames, timed the same way from an empty pipeline, gives the
+    steady frame period (the difference of the two loops per extra frame) and the pipeline fill (what the timed
+    loop pays beyond steps x the period: its first frames start with no frame in flight).
+    `check`: after the timed loop, its last frame's rows (this rank's bands; 12 of them) against the oracle, and
+    after the fixed-view loop that frame's rows against the golden digests of the config (when one exists)."""
     rank = ctl.rank if nranks > 1 else 0
     ids = shard.dist_ids(slots) if nranks > 1 and gather else None
     d = sf.SphereflakeDist(dev.index, width, height, rank=rank, nranks=nranks, slots=slots, ids=ids,
                            band_rows=band_rows)
     render = d.Render if gather else d.RenderBands
-    views = [frame_camera(width, height, k, frame_of(i)).corners() for i in range(warmup + steps)]
-    out = {}
+    view_at = path_views(width, height, k, frame_of)
+    views = [view_at(i) for i in range(warmup + steps)]
+    out = {"checks": {}}
+    mine = owned_rows(height, band_rows, nranks, rank) if not gather else np.arange(height)
     ctl.barrier()
     if first:   # the first render of a fresh context: row-major tile order, no cost history
         d.SetView(*views[0])
@@ -541,18 +631,22 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
         d.kernel_timing(s, True, period=kp)
     d.Synchronize()
     d.reset_stats()
-    torch.cuda.synchronize(dev)
-    ctl.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(steps):
-        d.SetView(*views[warmup + i])
-        render()
-    d.Synchronize()
-    torch.cuda.synchronize(dev)
-    ctl.barrier()
-    torch.cuda.synchronize(dev)
-    out["t_step"] = ctl.max((time.perf_counter() - t0) / steps)
+
+    def timed(n, view_of):
+        torch.cuda.synchronize(dev)
+        ctl.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(n):
+            d.SetView(*view_of(i))
+            render()
+        d.Synchronize()
+        torch.cuda.synchronize(dev)
+        ctl.barrier()
+        torch.cuda.synchronize(dev)
+        return ctl.max(time.perf_counter() - t0)
+
+    out["t_step"] = timed(steps, lambda i: views[warmup + i]) / steps
     tk, clk = [], []
     for s in range(slots):
         tk += list(d.kernel_timing(s, n=64))
@@ -567,27 +661,38 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
     if st.overflow_tiles:
         raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
     out["stats"] = st
+    if check and (rank == 0 or not gather):   # the last timed frame, outside the timed region
+        pos, nrm = d.download_slot(d.last_slot())
+        rows = mine[np.linspace(0, len(mine) - 1, min(12, len(mine))).astype(int)] if len(mine) else mine
+        out["checks"]["moving_oracle_rows"] = {"rows": len(rows), "bit_exact":
+                                               check_oracle_rows(pos, nrm, views[-1], width, height, rows)}
+        del pos, nrm
+    if long_steps > steps:
+        t_long = timed(long_steps, lambda i: view_at(warmup + steps + i))
+        period = (t_long - out["t_step"] * steps) / (long_steps - steps)
+        out["pipeline"] = {"steady_frame_ms": round(period * 1e3, 5),
+                           "fill_ms": round((out["t_step"] - period) * steps * 1e3, 5),
+                           "long_steps": long_steps, "long_frame_ms": round(t_long / long_steps * 1e3, 5)}
     if fixed:   # the same loop on one unchanging view (the config camera)
-        d.SetView(*frame_camera(width, height, k, 0).corners())
+        cfg_view = frame_camera(width, height, k, 0).corners()
+        d.SetView(*cfg_view)
         t_w = time.perf_counter()
         for i in range(warmup):
             render()
         # (the host work since the timed loop let the clock drop: settle again)
-        fixed_view = [frame_camera(width, height, k, 0).corners()]
-        settle(d, render, fixed_view, 1, t_w, settle_ms)
-        ctl.barrier()
-        t0 = time.perf_counter()
-        for i in range(steps):
-            render()
-        d.Synchronize()
-        ctl.barrier()
-        out["t_fixed"] = ctl.max((time.perf_counter() - t0) / steps)
-    out["last_view"] = frame_camera(width, height, k, 0).corners() if fixed else views[-1]
+        settle(d, render, [cfg_view], 1, t_w, settle_ms)
+        out["t_fixed"] = timed(steps, lambda i: cfg_view) / steps
+        golden = golden_frame(width, height, k) if check else None
+        if golden is not None and (rank == 0 or not gather):
+            pos, nrm = d.download_slot(d.last_slot())
+            n_rows, bad = check_golden_rows(pos, nrm, golden, mine)
+            out["checks"]["fixed_golden_rows"] = {"fixture": f"tests/golden/frame_{golden['name']}.json",
+                                                  "rows": n_rows, "rows_differing": bad[:16], "bit_exact": not bad}
+            del pos, nrm
     if latency:   # one frame at a time, each waited for (rank 0's wait includes the gather of the others)
         lat = []
         for i in range(20):
             d.SetView(*views[i % len(views)])
-            out["last_view"] = views[i % len(views)]
             ctl.barrier()
             t = time.perf_counter()
             render()
@@ -598,11 +703,82 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
     return out
 
 
+def checks_pass(ctl, checks):
+    """Every check of every rank passed (combined over the control plane; True when there were none)."""
+    ok = all(c.get("bit_exact", True) for c in checks.values())
+    return ctl.max(0.0 if ok else 1.0) == 0.0
+
+
+def rank_devices(ctl, gpu, launch_check=False):
+    """Each rank's device as the rank sees it (index, PCI location, UUID), gathered on every rank."""
+    import torch
+    me = {"rank": ctl.rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "device": gpu}
+    if not launch_check:
+        p = torch.cuda.get_device_properties(gpu)
+        me["name"] = getattr(p, "gcnArchName", None) or p.name
+        for key in ("pci_bus_id", "pci_device_id", "pci_domain_id"):
+            if hasattr(p, key):
+                me[key] = int(getattr(p, key))
+        if hasattr(p, "uuid"):
+            me["uuid"] = str(p.uuid)
+    if not ctl.dist:
+        return [me]
+    got = [None] * ctl.world
+    ctl.dist.all_gather_object(got, me)
+    return got
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args):
+    """`--gpus N > 1` without a launcher: start N rank processes (torch.distributed.run, 127.0.0.1) with the same
+    arguments and exit with their status. Runs before this process makes any GPU call (it makes none)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, SF_BENCH_SPAWNED="1")
+    return subprocess.call(cmd, env=env)
+
+
+def launch_world(args):
+    """The rank layout of this run: (world, rank, local rank). `--gpus N > 1` with no launcher environment spawns the
+    N ranks (this process then only waits for them); a launcher world that is not --gpus ranks is an error."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1 and args.mode != "rows":
+            sys.exit(spawn_ranks(args))
+        return 1, 0, 0
+    world = int(env_world)
+    if args.mode != "rows" and world != args.gpus:
+        raise SystemExit(f"bench.py: the launcher started {world} rank(s) but --gpus is {args.gpus}: one rank per GPU, "
+                         f"run with --gpus {world} (or without a launcher: --gpus N spawns the N ranks itself)")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def launch_check(args, world, rank, local):
+    """--launch-check: the ranks come up and agree (no rendering, no GPU call)."""
+    import torch
+    ctl = Control(world, rank)
+    ndev = torch.cuda.device_count()
+    ranks = rank_devices(ctl, local % max(1, ndev) if world > 1 else 0, launch_check=True)
+    t = ctl.max(0.0)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mrays/s", "n_gpus": world, "steps": 0,
+                          "warmup": 0, "launch_check": True, "devices_visible": ndev, "ranks": ranks,
+                          "spawned": os.environ.get("SF_BENCH_SPAWNED") == "1", "max_over_ranks": t}), flush=True)
+    ctl.close()
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = launch_world(args)
+    if args.launch_check:
+        launch_check(args, world, rank, local)
+        return 0
     import torch
     n = world
     ndev = torch.cuda.device_count()
@@ -621,6 +797,8 @@ def main():
     kernel = sf.SF_KERNEL_WAVE if args.kernel == "wave" else sf.SF_KERNEL_PER_RAY
     if kernel != sf.SF_KERNEL_WAVE and args.mode == "dist":
         raise SystemExit("the per-ray kernel runs in --mode frames only")
+    check = not args.no_check
+    long_steps = args.long_steps or max(4 * args.steps, 200)
 
     # a tiny render on a throw-away context first: loads the code object, so that `first_render_ms`
     # below is the first render of a fresh context, not the process's first kernel launch
@@ -634,22 +812,26 @@ def main():
     if args.mode == "rows":
         run_rows(args, torch, ctl, max(n, args.gpus), kernel)
         ctl.close()
-        return
+        return 0
 
+    ranks = rank_devices(ctl, gpu)
     slots = max(1, min(8, args.slots))
     if args.mode == "dist":
         # the frame split over the ranks, each rank's bands into its own HBM (the distributed G-buffer)
         r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
-                      lambda i: i, fixed=True, latency=True, first=True, settle_ms=args.settle_ms)
+                      lambda i: i, fixed=True, latency=True, first=True, settle_ms=args.settle_ms,
+                      long_steps=long_steps, check=check)
         rays_step = width * height
     else:   # frames: every rank its own frames (frame i * N + rank), one GPU each, slots in flight
         r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, 1,
-                      lambda i: i * n + rank, fixed=True, latency=True, first=True, settle_ms=args.settle_ms)
+                      lambda i: i * n + rank, fixed=True, latency=True, first=True, settle_ms=args.settle_ms,
+                      long_steps=long_steps, check=check)
         rays_step = width * height * n
     d = r["dist"]
     t_step = r["t_step"]
     value = rays_step / t_step / 1e6
     st = r["stats"]
+    d.close()
 
     # weak-scaling companion of a multi-GPU run: every rank renders its own frames (no gather)
     indep = None
@@ -667,28 +849,16 @@ def main():
                        n if args.mode == "dist" else 1, (lambda i: i) if args.mode == "dist" else (lambda i: i * n + rank),
                        settle_ms=args.settle_ms)
         rays0_4 = (sf.lib().sf_slab_rows(2160, args.band_rows, n, 0) if args.mode == "dist" else 2160) * 3840
-        a4 = BYTES_PER_RAY * rays0_4 / (r4["trace_ms"] * 1e-3) / 1e9 if r4["trace_ms"] else None
+        a4 = BYTES_PER_RAY * rays0_4 / r4["t_step"] / 1e9
         c4 = {"config": "BASELINE configs[3]: 3840x2160, K=0.22", "max_depth": r4["stats"].max_depth,
               "value": round((3840 * 2160 * (n if args.mode == "frames" else 1)) / r4["t_step"] / 1e6, 2),
               "frame_ms": round(r4["t_step"] * 1e3, 4), "steps": 60, "warmup": 15,
-              "roofline": {"achieved": round(a4, 2) if a4 else None, "frac": round(a4 / HBM_PEAK_GBS, 5) if a4 else None,
-                           "kernel_ms": round(r4["trace_ms"], 4) if r4["trace_ms"] else None,
+              "roofline": {"achieved": round(a4, 2), "frac": round(a4 / HBM_PEAK_GBS, 5),
+                           "basis": "32 B/ray x rank 0's rays per frame / frame period",
+                           "kernel_event_ms_overlapped": round(r4["trace_ms"], 4) if r4["trace_ms"] else None,
                            "kernel_samples": r4["kernel_samples"],
                            "clock_mhz_live": round(r4["clock_mhz"], 1) if r4["clock_mhz"] else None}}
         r4["dist"].close()
-
-    check = None
-    if args.check and rank == 0:
-        from oracle import pyoracle
-        pos, nrm = d.download()
-        o, tl, tr, bl = r["last_view"]
-        setup = {"W": width, "H": height, "origin": o, "tl": tl, "tr": tr, "bl": bl,
-                 "root": sf.root_transform(o), "children": sf.child_transforms()}
-        rows = np.linspace(0, height - 1, 12).astype(int)
-        ro = pyoracle.render(setup, rows=rows)
-        check = bool(np.array_equal(ro["pos4"].view(np.uint32), pos[rows].view(np.uint32)) and
-                     np.array_equal(ro["nrm4"].view(np.uint32), nrm[rows].view(np.uint32)))
-    d.close()
 
     post = d2h = prog = None
     if rank == 0 and n == 1 and not args.no_extras:
@@ -703,11 +873,16 @@ def main():
             d2h = transfer_rates(ctx, torch, dev, stream, width, height, kernel)
         prog = progressive_rates(width, height, args.K)
 
+    checks = r["checks"]
+    checks_ok = checks_pass(ctl, checks) if check else None
+    out = None
     if rank == 0:
         band = args.band_rows
         rays0 = (sf.lib().sf_slab_rows(height, band, n, 0) if args.mode == "dist" else height) * width
-        trace_ms = r["trace_ms"] or t_step * 1e3
-        achieved = BYTES_PER_RAY * rays0 / (trace_ms * 1e-3) / 1e9
+        clock = r["clock_mhz"]
+        # roofline of the frame: the G-buffer stores of rank 0's share of one frame per frame period (the timed
+        # steps' period, as ms_per_step); with frames in flight no single kernel duration is a frame's
+        achieved = BYTES_PER_RAY * rays0 / t_step / 1e9
         build = sf.build_info()
         pmc, _ = load_pmc(TRACE_KERNEL, pmc_config_key(width, height, args.K, "moving"), build)
         traffic = pmc_traffic(pmc) if n == 1 else None
@@ -718,6 +893,23 @@ def main():
                    if n > 1 else f"1 GPU, {slots} frames in flight (sf_dist slots)")
         else:
             par = f"frames x{n} (independent frames per rank, {slots} in flight each)"
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": round(traffic) if traffic else None,
+                "kernel": TRACE_KERNEL,
+                "basis": "32 B/ray x rank 0's rays of one frame / ms_per_step (one trace launch per frame)",
+                "units_per_launch": rays0, "bytes_per_unit": BYTES_PER_RAY,
+                "kernel_event_ms_overlapped": round(r["trace_ms"], 4) if r["trace_ms"] else None,
+                "kernel_samples": r["kernel_samples"],
+                "clock_mhz_live": round(clock, 1) if clock else None,
+                "note": "path is issue-bound (SURVEY.md §8(d), see `valu`); kernel_event_ms_overlapped = mean HIP-event "
+                        "duration of the trace kernel on its stream, which with frames in flight shares the GPU with the "
+                        "next frames' launches and so exceeds the frame period by construction (not used above); "
+                        "traffic = PMC WRITE_SIZE + 2 x FETCH_SIZE per launch (profiles/pmc_traffic.json, only for "
+                        "this config and this library build, else null)"}
+        if "pipeline" in r:
+            roof["steady_achieved"] = round(BYTES_PER_RAY * rays0 / (r["pipeline"]["steady_frame_ms"] * 1e-3) / 1e9, 2)
+            roof["steady_frac"] = round(roof["steady_achieved"] / HBM_PEAK_GBS, 5)
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -746,21 +938,22 @@ def main():
             "fixed_camera": {"value": round(rays_step / r["t_fixed"] / 1e6, 2), "frame_ms": round(r["t_fixed"] * 1e3, 4),
                              "note": "same timed loop on the unchanging config view"},
             "rays_counted": int(st.rays),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": round(traffic) if traffic else None,
-                         "kernel": TRACE_KERNEL, "kernel_ms": round(trace_ms, 4), "kernel_samples": r["kernel_samples"],
-                         "clock_mhz_live": round(r["clock_mhz"], 1) if r["clock_mhz"] else None,
-                         "frame_rate_GBps": round(BYTES_PER_RAY * width * height / t_step / 1e9, 2),
-                         "note": "path is VALU/latency-bound (SURVEY.md §8(d), see `valu`); achieved = 32 B/ray x rank 0's "
-                                 "rays per launch / mean duration of its trace kernel (HIP events around it on its "
-                                 "stream; with frames in flight a kernel shares the GPU with the next frame's); "
-                                 "frame_rate_GBps = 32 B/ray of the whole frame per frame period; traffic = PMC "
-                                 "WRITE_SIZE + 2 x FETCH_SIZE per launch (profiles/pmc_traffic.json, only for this "
-                                 "config and this library build, else null)"},
-            "valu": pmc_valu(pmc) if n == 1 else None,
+            "roofline": roof,
+            "valu": pmc_valu(pmc, t_step * 1e3, clock) if n == 1 else None,
             "build": build,
+            "ranks": ranks,
         }
+        if "pipeline" in r:
+            out["pipeline"] = dict(r["pipeline"], note=(
+                "a second loop of long_steps frames from an empty pipeline, timed like the first: steady_frame_ms = "
+                "(its time - the timed loop's) / the extra frames; fill_ms = the timed loop's time beyond steps x "
+                "steady_frame_ms (its first frames run with no frame in flight), so ms_per_step = steady_frame_ms + "
+                "fill_ms / steps"))
+        if check:
+            out["check"] = {"bit_exact": checks_ok, **checks,
+                            "note": "outside the timed region; this rank's rows (rank 0's bands on N > 1): the last "
+                                    "timed moving frame against the oracle restatement, the last fixed-view frame "
+                                    "against the reference-made golden row digests; all ranks combined in bit_exact"}
         if n > 1 and args.mode == "dist":
             out["independent_frames"] = indep
             if args.rehearse:
@@ -769,8 +962,6 @@ def main():
             out["configs"] = {"c4": c4}
         if post is not None:
             out["post"], out["d2h"], out["frameless"] = post, d2h, prog
-        if check is not None:
-            out["check_rows_bit_exact"] = check
         if not args.no_cpu_baseline and n == 1:
             avail, quota = cpu_share()
             thr = args.cpu_threads or (min(avail, quota) if quota else avail)
@@ -790,32 +981,68 @@ def main():
 
     # Last, the same frames assembled on rank 0 (RCCL gather of the packed slabs + unpack). It is the only leg
     # with a data-path collective, so it runs after every other number is in hand, under a watchdog: an RCCL
-    # error is recorded in the line, a hang past --gather-timeout prints the line without it.
+    # error, a hang past --gather-timeout or a gathered frame that differs from the golden frame prints the line
+    # with the leg marked failed and exits EXIT_GATHER_FAILED.
+    rc = 0 if checks_ok in (None, True) else EXIT_CHECK_FAILED
     if n > 1 and args.mode == "dist" and not args.rehearse:
         if rank == 0:
             out["gathered_on_rank0"] = {"error": f"not finished within {args.gather_timeout:g} s"}
         wd = Watchdog(args.gather_timeout, (lambda: print(json.dumps(out), flush=True)) if rank == 0 else (lambda: None))
-        try:
-            rg = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
-                           lambda i: i, latency=True, gather=True, settle_ms=args.settle_ms)
-            rg["dist"].close()
-            gathered = {"value": round(rays_step / rg["t_step"] / 1e6, 2), "frame_ms": round(rg["t_step"] * 1e3, 4),
-                        "frame_latency_ms": round(rg["latency_ms"], 4),
-                        "bytes_per_frame": sum(sf.lib().sf_slab_rows(height, args.band_rows, n, kk)
-                                               for kk in range(1, n)) * width * 16,
-                        "format": "packed float4 (nx, ny, nz, minT) per pixel; rank 0 rebuilds pos = dir * minT",
-                        "transport": "RCCL grouped ncclSend/ncclRecv to rank 0 over xGMI, one communicator per slot",
-                        "note": "every frame complete in rank 0's G-buffer (reference layout): the rate a consumer "
-                                "on rank 0 sees; bound by the peers' links into rank 0"}
-        except Exception as e:   # (an RCCL error on one rank: the others fail or the watchdog ends them)
-            gathered = {"error": f"{type(e).__name__}: {e}"}
+        gathered = gather_leg(args, ctl, torch, dev, slots, n, rays_step, check)
         wd.cancel()
         if rank == 0:
             out["gathered_on_rank0"] = gathered
+        failed = ctl.max(1.0 if "error" in gathered or gathered.get("check", {}).get("bit_exact") is False else 0.0)
+        if failed:
+            rc = EXIT_GATHER_FAILED
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctl.close()
+    return rc
+
+
+def gather_leg(args, ctl, torch, dev, slots, n, rays_step, check):
+    """The timed frames assembled on rank 0 (sf_dist_render: RCCL grouped send/recv of the packed slabs, unpacked on
+    rank 0 beside its own bands), then the config view once more, gathered, against the golden row digests."""
+    width, height = args.width, args.height
+    try:
+        rg = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
+                       lambda i: i, latency=True, gather=True, settle_ms=args.settle_ms)
+        d = rg["dist"]
+        comm = d.comm_info(0)
+        slab_bytes = d.slab_bytes()
+        peer_bytes = sum(sf.lib().sf_slab_rows(height, args.band_rows, n, kk) for kk in range(1, n)) * width * slab_bytes
+        t = rg["t_step"]
+        g = {"value": round(rays_step / t / 1e6, 2), "frame_ms": round(t * 1e3, 4),
+             "frame_latency_ms": round(rg["latency_ms"], 4),
+             "rccl": {"comm_count": comm[0], "rank0_user_rank": comm[1], "rank0_device": comm[2]},
+             "slab_bytes_per_pixel": slab_bytes, "bytes_per_frame": peer_bytes,
+             "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                          "achieved": round(BYTES_PER_RAY * rays_step / t / 1e9, 2),
+                          "frac": round(BYTES_PER_RAY * rays_step / t / 1e9 / HBM_PEAK_GBS, 5),
+                          "basis": "rank 0 writes the whole frame's G-buffer (32 B/pixel) per frame period",
+                          "link_GBps_per_peer": round(peer_bytes / max(1, n - 1) / t / 1e9, 2)},
+             "format": ("one uint32 hit index per pixel (rank 0 rebuilds centre, minT, position and normal from it)"
+                        if slab_bytes == 4 else "float4 (nx, ny, nz, minT) per pixel; rank 0 rebuilds pos = dir * minT"),
+             "transport": "RCCL grouped ncclSend/ncclRecv to rank 0 over xGMI, one communicator per slot; rank 0's "
+                          "receive and unpack on a stream of their own beside its trace",
+             "note": "every frame complete in rank 0's G-buffer (reference layout): the rate a consumer on rank 0 sees"}
+        if check:
+            golden = golden_frame(width, height, args.K)
+            if golden is not None:
+                d.SetView(*sf.config_camera(width, height, args.K).corners())
+                d.Render()
+                d.Synchronize()
+                if ctl.rank == 0:
+                    pos, nrm = d.download()
+                    n_rows, bad = check_golden_rows(pos, nrm, golden, np.arange(height))
+                    g["check"] = {"fixture": f"tests/golden/frame_{golden['name']}.json", "rows": n_rows,
+                                  "rows_differing": bad[:16], "bit_exact": not bad}
+        d.close()
+        return g
+    except Exception as e:   # (an RCCL error on one rank: the others fail or the watchdog ends them)
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -75,9 +75,13 @@ typedef struct sf_render_params {
     uint32_t emit_aux;        /* 1: also write minT (float) and hit index (uint32) channels */
     uint32_t max_depth;       /* traversal stack levels to provision (0 = auto: 12, retried at
                                  SF_MAX_DEPTH_LIMIT if a tile needs more) */
-    uint32_t packed;          /* 1: write ONE float4 (nx, ny, nz, minT) per pixel into pos4 (nrm4 unused): a
-                                 band slab for the multi-GPU gather at 16 B/pixel instead of 32; the position is
-                                 dir * minT, recomputed bit for bit by sf_unpack_bands (wave kernel only) */
+    uint32_t packed;          /* band slab formats of the multi-GPU gather (wave kernel only; nrm4 unused):
+                                 1: ONE float4 (nx, ny, nz, minT) per pixel into pos4, 16 B/pixel instead of 32;
+                                    the receiver forms the position dir * minT bit for bit (sf_unpack_slabs);
+                                 2: ONE uint32 per pixel into pos4: the hit sphere's heap index (9n+1+i,
+                                    0xffffffff = miss), 4 B/pixel; the receiver rebuilds the sphere's frame, the
+                                    self test's minT, position and normal bit for bit. Only where sf_slab_bytes()
+                                    is 4 for the view (else SF_EINVAL) */
     void* stream;             /* hipStream_t to launch on; NULL = the context stream */
 } sf_render_params;
 
@@ -129,6 +133,20 @@ int sf_render_to(sf_ctx* ctx, const sf_render_params* params, float* pos4, float
 
 /* Rows of the slab a (band_rows, band_count, band_index) shard owns (compact layout). */
 uint32_t sf_slab_rows(uint32_t height, uint32_t band_rows, uint32_t band_count, uint32_t band_index);
+
+/* Bytes per pixel of the smallest lossless band slab for the context's current view: 4 (params.packed = 2, the
+   hit index) when the view proves every hit at depth <= 10 -- heap indices below 2^32 --, else 16 (packed = 1);
+   0 before sf_set_view. A pure function of the view: every rank of a split computes the same value. */
+uint32_t sf_slab_bytes(const sf_ctx* ctx);
+
+/* The receiving end of a banded frame, either slab format: `stage` (device) holds the packed compact slabs of
+   members first_member .. first_member + members - 1 of a (band_rows, band_count) split, each stage_rows x W
+   pixels of bytes_per_pixel (16: packed = 1, 4: packed = 2) bytes; every pixel is written to the context's G-buffer
+   at its frame position, bit for bit what an unbanded render writes (recomputed from the context's current view:
+   call it with the view the slabs were traced with). stage_rows must hold every member's slab (SF_EINVAL
+   otherwise). Asynchronous on `stream`. */
+int sf_unpack_slabs(sf_ctx* ctx, const void* stage, uint32_t bytes_per_pixel, uint32_t stage_rows, uint32_t band_rows,
+                    uint32_t band_count, uint32_t first_member, uint32_t members, void* stream);
 
 /* The receiving end of a banded frame: `stage4` (device) holds the packed slabs (params.packed = 1,
    compact = 1) of members first_member .. first_member + members - 1 of a (band_rows, band_count) split, each
@@ -307,9 +325,10 @@ int sf_kernel_clocks(sf_ctx* ctx, float* mhz, uint32_t n);
 /* One process, n member devices (the reference's host thread pool, Sphereflake.cpp:67-74, becomes n
    GPUs). The frame is cut into interleaved bands of band_rows rows, band b traced by member b % n;
    member 0 holds the final G-buffer (its context's buffers): it writes its bands in place; member k > 0
-   traces its bands as a packed slab (16 B/pixel, sf_render_params.packed) and copies it over xGMI into
-   member 0's stage on a copy stream of its own (overlapping its next frame's trace); member 0's stream
-   waits for the copies and unpacks the stage into its G-buffer (sf_unpack_bands). Slabs and stages are
+   traces its bands as a packed slab (4 B/pixel hit indices where sf_slab_bytes allows, else 16 B/pixel;
+   sf_render_params.packed) and copies it over xGMI into member 0's stage on a copy stream of its own
+   (overlapping its next frame's trace); member 0 unpacks the stage into its G-buffer (sf_unpack_slabs) on an
+   unpack stream of its own, beside its own trace, and its context stream waits for that. Slabs and stages are
    double-buffered by frame parity, so members run a frame ahead of member 0. A device may appear more than
    once (n contexts on one GPU: the single-GPU test of the path). Stats combine: max depth max, closest min,
    rays and overflow tiles summed. */
@@ -329,13 +348,17 @@ int sf_group_download(sf_group* group, float* pos4, float* nrm4);   /* synchrono
 int sf_group_get_stats(sf_group* group, sf_stats* out);             /* synchronises */
 int sf_group_reset_stats(sf_group* group);                          /* all three counters, every member */
 int sf_group_last_hip_error(const sf_group* group);
+/* Bytes per pixel a member ships for the current view (sf_slab_bytes of member 0). */
+int sf_group_slab_bytes(const sf_group* group);
 
 /* --- multi-GPU, one process per GPU ------------------------------------------------------
    The reference's worker pool (Sphereflake.cpp:67-74) as nranks processes, one GPU each (the torch.distributed /
    MPI model): every rank traces the interleaved bands b = rank (mod nranks) of each frame; ranks k > 0 trace
-   theirs as packed slabs (16 B/pixel, sf_render_params.packed) and send them to rank 0 with RCCL over xGMI
-   (grouped ncclSend / ncclRecv on the frame's stream); rank 0 traces its own bands in place and unpacks the
-   others' (sf_unpack_bands) into its G-buffer, bit for bit the single-GPU frame.
+   theirs as packed slabs (4 B/pixel hit indices where sf_slab_bytes allows, else 16 B/pixel;
+   sf_render_params.packed) and send them to rank 0 with RCCL over xGMI (ncclSend behind the trace on the frame's
+   stream); rank 0 traces its own bands in place while it receives the others' (one grouped ncclRecv) and unpacks
+   them (sf_unpack_slabs) on a receive stream of its own; the slot's context stream then waits for the unpack: the
+   frame in rank 0's G-buffer bit for bit the single-GPU frame.
    `slots` frames may be in flight: frame i runs on slot i % slots (its own context, stream, communicator and
    buffers), so a frame's trace fills the GPU while the previous frame's heaviest tiles and gather finish.
    Without ids there is no communicator, whatever nranks: frames in flight on one GPU (nranks = 1), or this rank's
@@ -369,6 +392,11 @@ int sf_dist_get_stats(sf_dist* dist, sf_stats* out);  /* over slots, and over ra
                                                          (then collective); synchronises */
 int sf_dist_reset_stats(sf_dist* dist);
 int sf_dist_last_error(const sf_dist* dist, int* hip_error, int* rccl_error);
+/* The RCCL communicator of `slot` as RCCL reports it: ncclCommCount, ncclCommUserRank, ncclCommCuDevice
+   (SF_ESTATE when the dist was made without ids). */
+int sf_dist_comm_info(const sf_dist* dist, int slot, int* count, int* rank, int* device);
+/* Bytes per pixel the gather ships for the current view (sf_slab_bytes of the slots' contexts). */
+int sf_dist_slab_bytes(const sf_dist* dist);
 
 /* The context's own stream (hipStream_t) -- where calls with a NULL stream are queued. */
 void* sf_context_stream(sf_ctx* ctx);

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <new>
 #include <utility>
+#include <vector>
 
 #include "sf_build_id.h"   // SF_SOURCE_HASH (generated: build/, scripts/source_hash.py)
 #include "sf_internal.h"
@@ -38,6 +39,10 @@ extern "C" __global__ void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_l
 extern "C" __global__ void sf_trace_ray(FrameArgs a);
 extern "C" __global__ void sf_band_unpack(FrameArgs a, const float4* stage, uint32_t stage_rows, uint32_t band_rows,
                                            uint32_t n, uint32_t first, uint32_t members, uint32_t row0);
+extern "C" __global__ void sf_node_table(FrameArgs a, float4* table, uint32_t nodes);
+extern "C" __global__ void sf_slab_unpack4(FrameArgs a, const uint32_t* stage, const float4* table, uint32_t table_depth,
+                                           uint32_t stage_rows, uint32_t band_rows, uint32_t n, uint32_t first,
+                                           uint32_t members, uint32_t row0);
 extern "C" __global__ void sf_post_ssao(PostArgs a);
 extern "C" __global__ void sf_post_blur(PostArgs a, uint32_t dir);
 extern "C" __global__ void sf_post_final(PostArgs a);
@@ -113,6 +118,15 @@ struct sf_ctx {
     int32_t* stats = nullptr;          // [0] max depth, [1] closest key, [2] unrecoverable overflow
     uint32_t* ovf_counters = nullptr;  // [0,1] overflow counts, then the tile queues (SF_QUEUE_WORD); alternating per render
     uint32_t* ovf_list = nullptr;      // 4 x tiles_x * tiles_y entries (one per work unit)
+    float4* node_table = nullptr;      // index slab unpack: frames of the nodes of depth <= SF_NODE_TABLE_DEPTH
+    float table_root[12];              // the root transform the table was built for
+    uint32_t table_gen = 0;            // ... and consts_gen (0: no table yet)
+    uint32_t consts_gen = 1;           // bumped by every constant-block upload (children, depth tables)
+    struct SlabCacheEntry {            // sf_slab_bytes of recent views (gen 0: empty)
+        float root[16];
+        uint32_t gen = 0, bytes = 0;
+    } slab_cache[64];
+    uint32_t slab_cache_next = 0;
     DeviceConsts* consts = nullptr;
     DeviceConsts host_consts;
     float child[9][16];
@@ -297,6 +311,7 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->stats);
     (void)hipFree(c->ovf_counters);
     (void)hipFree(c->ovf_list);
+    (void)hipFree(c->node_table);
     (void)hipFree(c->consts);
     (void)hipFree(c->mt_state);
     (void)hipFree(c->draws);
@@ -370,6 +385,7 @@ static int upload_consts(sf_ctx* c)
     c->host_consts.fast_div = c->fast_div ? 1u : 0u;
     c->host_consts.tx_magic = 0xffffffffu / ((c->W + 7) / 8);
     if (int rc_ = ctx_drain(c)) return rc_;   // no kernel of the context may still read the block
+    ++c->consts_gen;
     SF_HIP(c, hipMemcpyAsync(c->consts, &c->host_consts, sizeof(DeviceConsts), hipMemcpyHostToDevice, c->stream));
     SF_HIP(c, hipStreamSynchronize(c->stream));
     return SF_OK;
@@ -641,7 +657,9 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
     a.band_count = band_count;
     a.band_index = p.band_index;
     a.compact = p.compact ? 1u : 0u;
-    a.packed = p.packed ? 1u : 0u;
+    if (p.packed > SF_PACKED_INDEX) return SF_EINVAL;
+    if (p.packed == SF_PACKED_INDEX && sf_slab_bytes(c) != 4u) return SF_EINVAL;   // (a hit could be too deep)
+    a.packed = p.packed;
     if (a.packed && p.kernel == SF_KERNEL_PER_RAY) return SF_EINVAL;   // (the per-ray kernel writes the plain layout)
     a.emit_aux = p.emit_aux ? 1u : 0u;
     a.pos = pos;
@@ -832,29 +850,154 @@ int sf_render_to(sf_ctx* c, const sf_render_params* p, float* pos4, float* nrm4,
     return launch(c, p, pos4, nrm4, min_t, hidx);
 }
 
-int sf_unpack_bands(sf_ctx* c, const float* stage4, uint32_t stage_rows, uint32_t band_rows, uint32_t band_count,
-                    uint32_t first_member, uint32_t members, void* stream)
+// Depth bound of every hit under the context's view (-1: none provable). Every sphere lies inside the root's
+// bounding sphere (radius 2 around the root centre), so a depth-d node can pass the LOD test (t < T_d,
+// Sphereflake.h:146) only if |root centre| - 2 < T_d; a node is self-tested only when its parent passed, so hits
+// lie at most one level below the deepest such d. (The same bound launch() provisions its LDS levels from.)
+static int hit_depth_bound(const sf_ctx* c)
 {
-    if (!c || !stage4 || band_rows == 0 || band_rows % 8 != 0 || band_count == 0 ||
-        first_member + members > band_count)
+    const float rc = std::sqrt(c->root[12] * c->root[12] + c->root[13] * c->root[13] + c->root[14] * c->root[14]);
+    const float gap = (rc - 2.0f) * (1.0f - 1e-3f);
+    if (!(gap > 0.0f)) return -1;
+    uint32_t dmax = 0;
+    while (dmax + 1u < SF_DEPTH_TABLE && c->host_consts.dt.lod[dmax + 1u] > gap) ++dmax;
+    return (int)dmax + 1;
+}
+
+// True when no depth-SF_INDEX_SLAB_DEPTH node can pass the LOD test for any ray of the view, so every hit lies at depth
+// <= SF_INDEX_SLAB_DEPTH (heap index below 2^32). Branch and bound over the node tree in double precision: a node's
+// whole subtree lies in its bounding ball (centre c, radius 2 r_d: each level's ball is internally tangent to its
+// parent's), and a node at depth D can expand only if t < T_D, where its bounding root t >= |c - O| - 2 r_D (O = the
+// ray origin, the frame's origin: the root transform maps it to 0). A subtree whose ball stays farther than T_D
+// from O is pruned. Slack: the float chain's centres are within ~1e-6 |c| of these, the float t within ~1e-6 of
+// the distance; 1e-3 relative and 1e-5 absolute cover both. The search gives up (false) past kMaxNodes nodes.
+static bool index_depth_proven(const sf_ctx* c)
+{
+    const int D = SF_INDEX_SLAB_DEPTH;
+    const double TD = (double)c->host_consts.dt.lod[D] * (1.0 + 1e-3) + 1e-5;
+    struct Node {
+        double m[12];   // columns 0..3, xyz (the child_frame layout)
+        int d;
+    };
+    constexpr int kMaxNodes = 1 << 16;
+    std::vector<Node> stack;
+    stack.reserve(256);
+    Node root;
+    for (int col = 0; col < 4; ++col)
+        for (int r = 0; r < 3; ++r) root.m[3 * col + r] = (double)c->root[4 * col + r];
+    root.d = 0;
+    stack.push_back(root);
+    int visited = 0;
+    while (!stack.empty()) {
+        const Node nd = stack.back();
+        stack.pop_back();
+        if (++visited > kMaxNodes) return false;
+        const double* cc = nd.m + 9;
+        const double dist = std::sqrt(cc[0] * cc[0] + cc[1] * cc[1] + cc[2] * cc[2]);
+        const double R = 2.0 * (double)sfhost::radius((uint32_t)nd.d) * (1.0 + 1e-6) + 1e-5 * (dist + 1.0);
+        if (dist - R >= TD) continue;      // no depth-D node of this subtree comes within T_D of the origin
+        if (nd.d == D) return false;       // a depth-D node that may expand: a hit could lie at depth D + 1
+        const double s = (double)c->host_consts.dt.scale[nd.d];
+        for (int i = 0; i < 9; ++i) {
+            Node ch;
+            ch.d = nd.d + 1;
+            for (int col = 0; col < 4; ++col) {
+                double b[4];
+                for (int k = 0; k < 4; ++k) b[k] = (double)c->child[i][4 * col + k];
+                if (col == 3)
+                    for (int k = 0; k < 3; ++k) b[k] *= s;
+                for (int r = 0; r < 3; ++r)
+                    ch.m[3 * col + r] = nd.m[r] * b[0] + nd.m[3 + r] * b[1] + nd.m[6 + r] * b[2] + nd.m[9 + r] * b[3];
+            }
+            stack.push_back(ch);
+        }
+    }
+    return true;
+}
+
+uint32_t sf_slab_bytes(const sf_ctx* cc)
+{
+    if (!cc || !cc->has_view) return 0;
+    const int d = hit_depth_bound(cc);
+    if (d >= 0 && d <= SF_INDEX_SLAB_DEPTH) return 4u;   // (the cheap bound: the whole flake is far enough)
+    // the search, cached per view (the root transform) and constant block: a camera path revisits its views
+    sf_ctx* c = const_cast<sf_ctx*>(cc);   // (the cache only)
+    for (const auto& e : c->slab_cache)
+        if (e.gen == c->consts_gen && std::memcmp(e.root, c->root, sizeof e.root) == 0) return e.bytes;
+    const uint32_t bytes = index_depth_proven(c) ? 4u : 16u;
+    auto& e = c->slab_cache[c->slab_cache_next];
+    c->slab_cache_next = (c->slab_cache_next + 1u) % (uint32_t)(sizeof c->slab_cache / sizeof c->slab_cache[0]);
+    std::memcpy(e.root, c->root, sizeof e.root);
+    e.gen = c->consts_gen;
+    e.bytes = bytes;
+    return bytes;
+}
+
+// The unpack of packed band slabs into the G-buffer on stream s. join: order after the context's previous call
+// like every public call (sf_unpack_slabs); without it the caller orders the stream itself (sf_dist / sf_group
+// run the unpack beside the context's own trace, on a stream of their own, and join it back with an event).
+int sfi_unpack_slabs(sf_ctx* c, const void* stage, uint32_t bytes_per_pixel, uint32_t stage_rows, uint32_t band_rows,
+                     uint32_t band_count, uint32_t first_member, uint32_t members, hipStream_t s, bool join)
+{
+    if (!c || !stage || band_rows == 0 || band_rows % 8 != 0 || band_count == 0 || first_member >= band_count ||
+        members > band_count - first_member || (bytes_per_pixel != 4u && bytes_per_pixel != 16u))
         return SF_EINVAL;
     if (!c->has_view) return SF_ENOVIEW;
-    if (members == 0 || stage_rows == 0) return SF_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (members == 0) return SF_OK;
+    // every member's slab must fit its stage_rows rows: a shorter stage would leave its last rows stale
+    for (uint32_t k = first_member; k < first_member + members; ++k)
+        if (sf_slab_rows(c->H, band_rows, band_count, k) > stage_rows) return SF_EINVAL;
+    if (stage_rows == 0) return SF_OK;
+    if (bytes_per_pixel == 4u && sf_slab_bytes(c) != 4u) return SF_EINVAL;   // (the view allows no index slab)
     DevGuard g(c->device);
-    if (int rc = ctx_join(c, s)) return rc;
-    StreamMark mark_(c, s);
+    if (join) {
+        if (int rc = ctx_join(c, s)) return rc;
+    }
     FrameArgs a = frame_args(c);
     a.pos = c->pos;
     a.nrm = c->nrm;
+    if (bytes_per_pixel == 4u) {
+        if (!c->node_table)
+            SF_HIP(c, hipMalloc(&c->node_table, (size_t)SF_NODE_TABLE_NODES * 3 * sizeof(float4)));
+        float root12[12];
+        for (int col = 0; col < 4; ++col)
+            for (int r = 0; r < 3; ++r) root12[3 * col + r] = c->root[4 * col + r];
+        if (c->table_gen != c->consts_gen || std::memcmp(root12, c->table_root, sizeof root12) != 0) {
+            hipLaunchKernelGGL(sf_node_table, dim3((SF_NODE_TABLE_NODES + 255u) / 256u), dim3(256), 0, s, a,
+                               c->node_table, SF_NODE_TABLE_NODES);
+            SF_HIP(c, hipGetLastError());
+            std::memcpy(c->table_root, root12, sizeof root12);
+            c->table_gen = c->consts_gen;
+        }
+    }
     for (uint32_t r0 = 0; r0 < stage_rows; r0 += 65535u) {
         const uint32_t rows = stage_rows - r0 < 65535u ? stage_rows - r0 : 65535u;
-        hipLaunchKernelGGL(sf_band_unpack, dim3((c->W + 255u) / 256u, rows, members), dim3(256), 0, s, a,
-                           reinterpret_cast<const float4*>(stage4), stage_rows, band_rows, band_count, first_member,
-                           members, r0);
+        const dim3 grid((c->W + 255u) / 256u, rows, members);
+        if (bytes_per_pixel == 4u)
+            hipLaunchKernelGGL(sf_slab_unpack4, grid, dim3(256), 0, s, a, reinterpret_cast<const uint32_t*>(stage),
+                               (const float4*)c->node_table, SF_NODE_TABLE_DEPTH, stage_rows, band_rows, band_count,
+                               first_member, members, r0);
+        else
+            hipLaunchKernelGGL(sf_band_unpack, grid, dim3(256), 0, s, a, reinterpret_cast<const float4*>(stage),
+                               stage_rows, band_rows, band_count, first_member, members, r0);
         SF_HIP(c, hipGetLastError());
     }
+    if (join && s != c->stream) SF_HIP(c, hipEventRecord(c->join_ev, s));   // (StreamMark)
     return SF_OK;
+}
+
+int sf_unpack_slabs(sf_ctx* c, const void* stage, uint32_t bytes_per_pixel, uint32_t stage_rows, uint32_t band_rows,
+                    uint32_t band_count, uint32_t first_member, uint32_t members, void* stream)
+{
+    if (!c) return SF_EINVAL;
+    return sfi_unpack_slabs(c, stage, bytes_per_pixel, stage_rows, band_rows, band_count, first_member, members,
+                            stream ? (hipStream_t)stream : c->stream, true);
+}
+
+int sf_unpack_bands(sf_ctx* c, const float* stage4, uint32_t stage_rows, uint32_t band_rows, uint32_t band_count,
+                    uint32_t first_member, uint32_t members, void* stream)
+{
+    return sf_unpack_slabs(c, stage4, 16u, stage_rows, band_rows, band_count, first_member, members, stream);
 }
 
 // n draws of the context's mt19937 stream into `out`, on stream s (advances c->mt_state): the single-workgroup
@@ -870,11 +1013,24 @@ static int gen_draws(sf_ctx* c, hipStream_t s, uint32_t* out, uint32_t n)
     K = K < 2u ? 2u : K > c->mt_seg_max ? c->mt_seg_max : K;
     const uint32_t L = (n + K - 1u) / K;
     const uint32_t pw = (uint32_t)sfhost::mt_poly_words();
-    if (!c->mt_raw) {
-        SF_HIP(c, hipMalloc(&c->mt_raw, (size_t)kMtRawBlocks * 624 * 4));
-        SF_HIP(c, hipMalloc(&c->mt_partial, (size_t)(kMtSegMax - 1) * kMtParts * 624 * 4));
-        SF_HIP(c, hipMalloc(&c->mt_state2, 625 * 4));
-        SF_HIP(c, hipMalloc(&c->mt_polys, (size_t)kMtSegMax * pw * 8));
+    if (!c->mt_raw || !c->mt_partial || !c->mt_state2 || !c->mt_polys) {
+        // all four scratch buffers or none: a partial set would let a later call launch on null buffers
+        hipError_t e = hipSuccess;
+        if (!c->mt_raw) e = hipMalloc(&c->mt_raw, (size_t)kMtRawBlocks * 624 * 4);
+        if (e == hipSuccess && !c->mt_partial) e = hipMalloc(&c->mt_partial, (size_t)(kMtSegMax - 1) * kMtParts * 624 * 4);
+        if (e == hipSuccess && !c->mt_state2) e = hipMalloc(&c->mt_state2, 625 * 4);
+        if (e == hipSuccess && !c->mt_polys) e = hipMalloc(&c->mt_polys, (size_t)kMtSegMax * pw * 8);
+        if (e != hipSuccess) {
+            (void)hipFree(c->mt_raw);
+            (void)hipFree(c->mt_partial);
+            (void)hipFree(c->mt_state2);
+            (void)hipFree(c->mt_polys);
+            c->mt_raw = c->mt_partial = c->mt_state2 = nullptr;
+            c->mt_polys = nullptr;
+            c->mt_poly_key = 0;
+            c->last_hip = (int)e;
+            return e == hipErrorOutOfMemory ? SF_ENOMEM : SF_EHIP;
+        }
     }
     const uint64_t key = ((uint64_t)L << 8) | K;
     if (c->mt_poly_key != key) {   // (host polynomials cached per (L, K); ~20 ms for a new batch size)

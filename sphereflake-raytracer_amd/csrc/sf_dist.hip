@@ -6,10 +6,13 @@
 // cost ~150 nodes per ray and sky rows ~1, so interleaving balances the ranks without any cost exchange.
 //   rank 0   traces its bands straight into its context's G-buffer at frame positions, then receives every
 //            other rank's slab and unpacks it into the same G-buffer (sf_unpack_bands);
-//   rank k   traces its bands as a PACKED compact slab -- one float4 (nx, ny, nz, minT) per pixel, half the
-//            G-buffer's 32 B: the position is dir * minT, which rank 0 recomputes bit for bit -- and sends it.
-// The gather is grouped ncclSend / ncclRecv on the slot's stream, right behind the trace (it is a gather to one
-// rank, each peer's slab over its own xGMI link: no ring collective).
+//   rank k   traces its bands as a PACKED compact slab and sends it: one uint32 hit index per pixel (4 B, an
+//            eighth of the G-buffer's 32 B) where the view proves every hit's heap index below 2^32
+//            (sf_slab_bytes), else one float4 (nx, ny, nz, minT) -- rank 0 rebuilds the rest bit for bit.
+// The gather is a gather to one rank, each peer's slab over its own xGMI link (no ring collective): ncclSend on
+// the peer's slot stream right behind its trace; on rank 0 one grouped ncclRecv and the unpack on a receive stream
+// of the slot, started at the frame's start, so the peers' slabs land and unpack while rank 0 traces its own bands;
+// the slot's context stream then waits for the unpack (the frame complete in rank 0's G-buffer).
 //
 // Frames in flight: `slots` independent pipelines (context + stream + communicator + slab), frame i on slot
 // i % slots. A frame's persistent trace grid then fills the wave slots the previous frame's heaviest tiles
@@ -29,14 +32,21 @@
 #include "sf_internal.h"
 #include "sphereflake/sf.h"
 
+// (sf_capi.hip) the unpack without the context's stream join: the caller orders `s` itself
+extern "C" int sfi_unpack_slabs(sf_ctx* c, const void* stage, uint32_t bytes_per_pixel, uint32_t stage_rows, uint32_t band_rows,
+                     uint32_t band_count, uint32_t first_member, uint32_t members, hipStream_t s, bool join);
+
 struct sf_dist {
     int device = 0, rank = 0, nranks = 1;
     uint32_t W = 0, H = 0, band_rows = 8;
     struct Slot {
         sf_ctx* ctx = nullptr;
         ncclComm_t comm = nullptr;
-        float* slab = nullptr;       // rank > 0: this rank's packed slab (slab_rows x W float4)
-        float* stage = nullptr;      // rank 0: the other ranks' packed slabs (nranks - 1) x stage_rows x W float4
+        float* slab = nullptr;       // rank > 0: this rank's packed slab (slab_rows x W x 16 B at most)
+        float* stage = nullptr;      // rank 0: the other ranks' packed slabs (nranks - 1) x stage_rows x W x 16 B at most
+        hipStream_t recv = nullptr;  // rank 0 with peers: receive + unpack stream
+        hipEvent_t start = nullptr;  // rank 0: the frame's start on the context stream (G-buffer free to rewrite)
+        hipEvent_t done = nullptr;   // rank 0: the frame's unpack done (on `recv`)
     };
     std::vector<Slot> slot;
     uint32_t slab_rows = 0, stage_rows = 0;
@@ -84,9 +94,13 @@ void free_dist(sf_dist* d)
     for (auto& s : d->slot)
         if (s.ctx) (void)sf_synchronize(s.ctx);
     for (auto& s : d->slot) {
+        if (s.recv) (void)hipStreamSynchronize(s.recv);
         if (s.comm) (void)ncclCommDestroy(s.comm);
         (void)hipFree(s.slab);
         (void)hipFree(s.stage);
+        if (s.recv) (void)hipStreamDestroy(s.recv);
+        if (s.start) (void)hipEventDestroy(s.start);
+        if (s.done) (void)hipEventDestroy(s.done);
         if (s.ctx) sf_destroy(s.ctx);
     }
     (void)hipFree(d->red);
@@ -145,8 +159,12 @@ extern "C" int sf_dist_create(int device, uint32_t width, uint32_t height, uint3
         }
         hipError_t e = hipSuccess;
         if (rank > 0 && d->slab_rows) e = hipMalloc(&s.slab, (size_t)d->slab_rows * width * 16);
-        if (e == hipSuccess && rank == 0 && nranks > 1 && d->stage_rows)
+        if (e == hipSuccess && rank == 0 && nranks > 1 && d->stage_rows) {
             e = hipMalloc(&s.stage, (size_t)(nranks - 1) * d->stage_rows * width * 16);
+            if (e == hipSuccess && ids) e = hipStreamCreateWithFlags(&s.recv, hipStreamNonBlocking);
+            if (e == hipSuccess && ids) e = hipEventCreateWithFlags(&s.start, hipEventDisableTiming);
+            if (e == hipSuccess && ids) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
+        }
         if (e != hipSuccess) {
             d->last_hip = (int)e;
             return fail(e == hipErrorOutOfMemory ? SF_ENOMEM : SF_EHIP);
@@ -192,37 +210,78 @@ extern "C" int sf_dist_render(sf_dist* d)
     auto& s = d->slot[d->frames % d->slot.size()];
     if (n > 1 && !s.comm) return SF_ESTATE;   // made without ids: bands only (sf_dist_render_bands)
     hipStream_t st = (hipStream_t)sf_context_stream(s.ctx);
+    // the slab format follows from the view, the same on every rank (every rank sets the same views)
+    const uint32_t bytes = sf_slab_bytes(s.ctx);
+    if (bytes == 0) return SF_ENOVIEW;
+    const size_t words = bytes / 4u;   // 32-bit words per pixel on the wire
     sf_render_params p;
     std::memset(&p, 0, sizeof p);
     p.band_rows = d->band_rows;
     p.band_count = n;
     p.band_index = (uint32_t)d->rank;
     if (d->rank == 0) {
-        // rank 0: its bands in place; then the other ranks' slabs in, unpacked beside them
+        Dev g(d->device);
+        const bool peers = n > 1 && d->stage_rows;
+        // the frame starts here on the context stream: earlier work there (the consumers of this slot's previous
+        // frame) is done before the receive stream rewrites the G-buffer
+        if (peers) SFD_HIP(d, hipEventRecord(s.start, st));
+        // rank 0: its bands in place on the context stream ...
         if (int rc = sf_render(s.ctx, &p)) return rc;
-        if (n > 1 && d->stage_rows) {
-            Dev g(d->device);
-            const size_t cnt = (size_t)d->stage_rows * W * 4;   // floats per peer slot of the stage
+        if (peers) {
+            // ... while the peers' slabs land and unpack on the receive stream
+            SFD_HIP(d, hipStreamWaitEvent(s.recv, s.start, 0));
+            const size_t cnt = (size_t)d->stage_rows * W * words;   // 32-bit words per peer of the stage
             SFD_NCCL(d, ncclGroupStart());
             for (uint32_t k = 1; k < n; ++k) {
                 const size_t rows = sf_slab_rows(d->H, d->band_rows, n, k);
                 if (!rows) continue;
-                SFD_NCCL(d, ncclRecv(s.stage + (k - 1) * cnt, rows * W * 4, ncclFloat32, (int)k, s.comm, st));
+                SFD_NCCL(d, ncclRecv(reinterpret_cast<uint32_t*>(s.stage) + (k - 1) * cnt, rows * W * words, ncclUint32,
+                                     (int)k, s.comm, s.recv));
             }
             SFD_NCCL(d, ncclGroupEnd());
-            if (int rc = sf_unpack_bands(s.ctx, s.stage, d->stage_rows, d->band_rows, n, 1, n - 1, nullptr)) return rc;
+            if (int rc = sfi_unpack_slabs(s.ctx, s.stage, bytes, d->stage_rows, d->band_rows, n, 1, n - 1, s.recv, false))
+                return rc;
+            SFD_HIP(d, hipEventRecord(s.done, s.recv));
+            SFD_HIP(d, hipStreamWaitEvent(st, s.done, 0));   // the frame is complete on the context stream
         }
     } else {
         p.compact = 1;
-        p.packed = 1;
+        p.packed = bytes == 4u ? SF_PACKED_INDEX : SF_PACKED_NORMAL;
         if (d->slab_rows) {
             if (int rc = sf_render_to(s.ctx, &p, s.slab, nullptr, nullptr, nullptr)) return rc;
             Dev g(d->device);
-            SFD_NCCL(d, ncclSend(s.slab, (size_t)d->slab_rows * W * 4, ncclFloat32, 0, s.comm, st));
+            SFD_NCCL(d, ncclSend(s.slab, (size_t)d->slab_rows * W * words, ncclUint32, 0, s.comm, st));
         }
     }
     ++d->frames;
     return SF_OK;
+}
+
+extern "C" int sf_dist_comm_info(const sf_dist* d, int slot, int* count, int* rank, int* device)
+{
+    if (!d || slot < 0 || slot >= (int)d->slot.size()) return SF_EINVAL;
+    const ncclComm_t c = d->slot[slot].comm;
+    if (!c) return SF_ESTATE;
+    int v = 0;
+    if (count) {
+        if (ncclCommCount(c, &v) != ncclSuccess) return SF_ECOMM;
+        *count = v;
+    }
+    if (rank) {
+        if (ncclCommUserRank(c, &v) != ncclSuccess) return SF_ECOMM;
+        *rank = v;
+    }
+    if (device) {
+        if (ncclCommCuDevice(c, &v) != ncclSuccess) return SF_ECOMM;
+        *device = v;
+    }
+    return SF_OK;
+}
+
+extern "C" int sf_dist_slab_bytes(const sf_dist* d)
+{
+    if (!d) return SF_EINVAL;
+    return (int)sf_slab_bytes(d->slot[0].ctx);
 }
 
 // This rank's bands of the next frame into its slot's G-buffer at frame positions (reference layout): the frame

@@ -5,12 +5,13 @@
 // rows (band b -> member b mod n: flake rows cost ~150 nodes per ray, sky rows ~1, so contiguous
 // halves would be badly unbalanced) and every member device traces its own bands. Member 0 writes its
 // bands straight into its own (final) G-buffer at frame positions; member k > 0 traces its bands into a
-// PACKED compact slab in its own HBM (one float4 (nx, ny, nz, minT) per pixel: half the G-buffer's 32 B;
-// the position is dir * minT, rebuilt bit for bit on member 0) and ships it with one contiguous peer copy
-// over xGMI into member 0's stage, on a copy stream of its own, so the next frame's trace on the member
-// overlaps the copy. Member 0's stream waits for the frame's copies and unpacks the stage into the G-buffer
-// (sf_unpack_bands): only member 0's own stream ever writes its G-buffer, so work queued on member 0's
-// context after sf_group_render (download, post-process) sees the whole frame, and consumers of the
+// PACKED compact slab in its own HBM (one uint32 hit index per pixel where the view allows it, sf_slab_bytes:
+// an eighth of the G-buffer's 32 B; else one float4 (nx, ny, nz, minT); member 0 rebuilds the rest bit for bit)
+// and ships it with one contiguous peer copy over xGMI into member 0's stage, on a copy stream of its own, so
+// the next frame's trace on the member overlaps the copy. Member 0 unpacks the stage into the G-buffer
+// (sf_unpack_slabs) on an unpack stream of its own, beside its own trace, after the frame's copies and after
+// the frame's start on its context stream; the context stream then waits for the unpack, so work queued on
+// member 0's context after sf_group_render (download, post-process) sees the whole frame, and consumers of the
 // previous frame queued before it are never overwritten. Slabs and stages are double-buffered by frame
 // parity: member k traces frame f + 1 while frame f's copy drains, and frame f + 2's copy into a stage waits
 // only for member 0's unpack of frame f from it.
@@ -25,6 +26,10 @@
 #include "sf_internal.h"
 #include "sphereflake/sf.h"
 
+// (sf_capi.hip) the unpack without the context's stream join: the caller orders `s` itself
+extern "C" int sfi_unpack_slabs(sf_ctx* c, const void* stage, uint32_t bytes_per_pixel, uint32_t stage_rows, uint32_t band_rows,
+                     uint32_t band_count, uint32_t first_member, uint32_t members, hipStream_t s, bool join);
+
 struct sf_group {
     int n = 0;
     uint32_t W = 0, H = 0;
@@ -35,7 +40,9 @@ struct sf_group {
     float* stage[2] = { nullptr, nullptr };   // member 0: members 1..n-1's slabs, stage_rows x W float4 each
     std::vector<hipEvent_t> traced[2];   // member k's trace of the frame done (its context stream)
     std::vector<hipEvent_t> copied[2];   // member k's copy into member 0's stage done (its copy stream)
-    hipEvent_t unpacked[2] = { nullptr, nullptr };   // member 0 done reading stage[b] (its stream)
+    hipEvent_t unpacked[2] = { nullptr, nullptr };   // member 0 done reading stage[b] (its unpack stream)
+    hipEvent_t start0 = nullptr;         // member 0: the frame's start on its context stream
+    hipStream_t unpack0 = nullptr;       // member 0: unpack stream
     std::vector<hipStream_t> copy;       // members k > 0: copy stream
     uint32_t band_rows = 0, stage_rows = 0;   // the split the buffers are sized for (0: none yet)
     uint64_t frames = 0;
@@ -106,8 +113,11 @@ void free_group(sf_group* g)
     }
     {
         Dev d(g->device[0]);
+        if (g->unpack0) (void)hipStreamSynchronize(g->unpack0);
         for (int b = 0; b < 2; ++b)
             if (g->unpacked[b]) (void)hipEventDestroy(g->unpacked[b]);
+        if (g->start0) (void)hipEventDestroy(g->start0);
+        if (g->unpack0) (void)hipStreamDestroy(g->unpack0);
     }
     for (sf_ctx* c : g->ctx) sf_destroy(c);
     delete g;
@@ -169,6 +179,8 @@ extern "C" int sf_group_create(const int* devices, int n, uint32_t width, uint32
             }
         }
         if (k > 0) ok = ok && hipStreamCreateWithFlags(&g->copy[k], hipStreamNonBlocking) == hipSuccess;
+        if (k == 0) ok = ok && hipEventCreateWithFlags(&g->start0, hipEventDisableTiming) == hipSuccess;
+        if (k == 0) ok = ok && hipStreamCreateWithFlags(&g->unpack0, hipStreamNonBlocking) == hipSuccess;
         if (!ok) {
             free_group(g);
             return SF_EHIP;
@@ -239,7 +251,9 @@ extern "C" int sf_group_render(sf_group* g, uint32_t band_rows)
         g->stage_rows = sr;
     }
     const int b = (int)(g->frames & 1u);
-    const size_t stage_slab = (size_t)g->stage_rows * W * 16;   // bytes per member in the stage
+    const uint32_t bytes = sf_slab_bytes(g->ctx[0]);   // the slab format of this view (the same for every member)
+    if (bytes == 0) return SF_ENOVIEW;
+    const size_t stage_slab = (size_t)g->stage_rows * W * bytes;   // bytes per member in the stage
     // members k > 0: trace the packed slab, then copy it into member 0's stage on the copy stream
     for (uint32_t k = 1; k < n; ++k) {
         const uint32_t rows = sf_slab_rows(H, band_rows, n, k);
@@ -254,31 +268,41 @@ extern "C" int sf_group_render(sf_group* g, uint32_t band_rows)
         p.band_count = n;
         p.band_index = k;
         p.compact = 1;
-        p.packed = 1;
+        p.packed = bytes == 4u ? SF_PACKED_INDEX : SF_PACKED_NORMAL;
         if (int rc = sf_render_to(g->ctx[k], &p, g->slab[b][k], nullptr, nullptr, nullptr)) return rc;
         SFG_HIP(g, hipEventRecord(g->traced[b][k], sk));
         SFG_HIP(g, hipStreamWaitEvent(g->copy[k], g->traced[b][k], 0));
         // stage[b] was last read by member 0's unpack of frame f - 2
         if (g->stage_used[b]) SFG_HIP(g, hipStreamWaitEvent(g->copy[k], g->unpacked[b], 0));
         SFG_HIP(g, hipMemcpyAsync(reinterpret_cast<char*>(g->stage[b]) + (size_t)(k - 1) * stage_slab, g->slab[b][k],
-                                  (size_t)rows * W * 16, hipMemcpyDeviceToDevice, g->copy[k]));
+                                  (size_t)rows * W * bytes, hipMemcpyDeviceToDevice, g->copy[k]));
         SFG_HIP(g, hipEventRecord(g->copied[b][k], g->copy[k]));
     }
-    // member 0: its bands in place, then (after the copies) the others' unpacked beside them, all on its
-    // own stream
+    // member 0: its bands in place on its context stream, and beside them (after the copies, and after the
+    // frame's start on the context stream) the others' unpacked on the unpack stream, which the context stream
+    // then waits for
     sf_render_params p;
     std::memset(&p, 0, sizeof p);
     p.band_rows = band_rows;
     p.band_count = n;
     p.band_index = 0;
-    if (int rc = sf_render(g->ctx[0], &p)) return rc;
-    if (n > 1 && g->stage_rows) {
+    const bool peers = n > 1 && g->stage_rows;
+    hipStream_t s0 = (hipStream_t)sf_context_stream(g->ctx[0]);
+    if (peers) {
         Dev d(g->device[0]);
-        hipStream_t s0 = (hipStream_t)sf_context_stream(g->ctx[0]);
+        SFG_HIP(g, hipEventRecord(g->start0, s0));
+    }
+    if (int rc = sf_render(g->ctx[0], &p)) return rc;
+    if (peers) {
+        Dev d(g->device[0]);
+        SFG_HIP(g, hipStreamWaitEvent(g->unpack0, g->start0, 0));
         for (uint32_t k = 1; k < n; ++k)
-            if (sf_slab_rows(H, band_rows, n, k)) SFG_HIP(g, hipStreamWaitEvent(s0, g->copied[b][k], 0));
-        if (int rc = sf_unpack_bands(g->ctx[0], g->stage[b], g->stage_rows, band_rows, n, 1, n - 1, nullptr)) return rc;
-        SFG_HIP(g, hipEventRecord(g->unpacked[b], s0));
+            if (sf_slab_rows(H, band_rows, n, k)) SFG_HIP(g, hipStreamWaitEvent(g->unpack0, g->copied[b][k], 0));
+        if (int rc = sfi_unpack_slabs(g->ctx[0], g->stage[b], bytes, g->stage_rows, band_rows, n, 1, n - 1, g->unpack0,
+                                      false))
+            return rc;
+        SFG_HIP(g, hipEventRecord(g->unpacked[b], g->unpack0));
+        SFG_HIP(g, hipStreamWaitEvent(s0, g->unpacked[b], 0));
         g->stage_used[b] = true;
     }
     ++g->frames;
@@ -333,3 +357,5 @@ extern "C" int sf_group_reset_stats(sf_group* g)
 }
 
 extern "C" int sf_group_last_hip_error(const sf_group* g) { return g ? g->last_hip : 0; }
+
+extern "C" int sf_group_slab_bytes(const sf_group* g) { return g ? (int)sf_slab_bytes(g->ctx[0]) : SF_EINVAL; }

@@ -158,6 +158,21 @@ struct FrameArgs {
 };
 #define SF_CLOCK_WAVES 8u             // live shader clock samples per timed render (one per XCD group)
 
+// Band slab formats of the multi-GPU gather (FrameArgs.packed / sf_render_params.packed):
+//   SF_PACKED_NORMAL  16 B per pixel: float4 (nx, ny, nz, minT); the receiver forms pos = dir * minT
+//   SF_PACKED_INDEX    4 B per pixel: the hit's heap index (SF_SLAB_MISS: none); the receiver rebuilds the
+//                      sphere's frame (node table + child_frame), its self test's minT, pos and nrm
+// The index format needs every hit's heap index below 2^32 -- depth <= SF_INDEX_SLAB_DEPTH -- which the host
+// proves from the view (sf_slab_bytes) before choosing it.
+#define SF_PACKED_NORMAL 1u
+#define SF_PACKED_INDEX 2u
+#define SF_INDEX_SLAB_DEPTH 10
+#define SF_SLAB_MISS 0xffffffffu
+#define SF_SLAB_BAD 0xfffffffeu
+// node table of the index unpack: the frames of every node of depth <= SF_NODE_TABLE_DEPTH (3 float4 each)
+#define SF_NODE_TABLE_DEPTH 5u
+#define SF_NODE_TABLE_NODES 66430u    // (9^6 - 1) / 8
+
 // Headless SSAO post-process (Shaders/post_ssao.glsl, post_ssao_blur.glsl,
 // post_final.glsl, SSAO.cpp:106-142). Textures are modelled, not emulated: NEAREST/LINEAR filtering
 // with the texel coordinate snapped to 8 fractional bits (sf_post.hip).

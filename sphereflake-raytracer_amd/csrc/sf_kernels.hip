@@ -114,6 +114,27 @@ __device__ __forceinline__ float near_root(float tca, float d2, float R2)
     return (t0 <= t1) ? t0 : t1;
 }
 
+// One level down the transform chain (Sphereflake.h:162-164, SIMD_AVX.h:59-81 product without FMA): `out` = the
+// frame of child i of a depth-p node whose frame is P, both as 3 x 4 {column-major xyz} (xf[3 c + r]). The child's
+// unit frame has its translation column scaled by (4/3) r_p. The per-ray kernel and the slab unpack both chain
+// with it, so a node's frame is the same float values whichever computes it.
+__device__ __forceinline__ void child_frame(const DeviceConsts* __restrict__ K, uint32_t p, uint32_t i,
+                                            const float* P, float* out)
+{
+    const float s = K->dt.scale[p];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float* B = K->child[i] + 4 * c;
+        const float b0 = c == 3 ? B[0] * s : B[0];
+        const float b1 = c == 3 ? B[1] * s : B[1];
+        const float b2 = c == 3 ? B[2] * s : B[2];
+        const float b3 = B[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            out[3 * c + r] = ((P[r] * b0 + P[3 + r] * b1) + P[6 + r] * b2) + P[9 + r] * b3;
+    }
+}
+
 struct HitState {
     float minT;
     float cx, cy, cz;     // centre of the nearest accepted sphere
@@ -1354,6 +1375,14 @@ __device__ __forceinline__ void write_pixel(const FrameArgs& a, const Tile& t, f
     shade(dx, dy, dz, h, lut, px, py, pz, nx, ny, nz);
     const size_t o = (size_t)t.orow * a.W + t.x;
     if (a.packed) {   // (uniform)
+        if (a.packed == SF_PACKED_INDEX) {
+            // 4 B: the hit's heap index; the receiver rebuilds the rest. (The host selects this format only where
+            // no hit can lie deeper than SF_INDEX_SLAB_DEPTH, whose heap indices are below 2^32; a deeper one would
+            // be ambiguous and is written as SF_SLAB_BAD instead.)
+            reinterpret_cast<uint32_t*>(a.pos)[o] = !h.hit ? SF_SLAB_MISS
+                                                  : h.depth > SF_INDEX_SLAB_DEPTH ? SF_SLAB_BAD : h.index;
+            return;
+        }
         reinterpret_cast<float4*>(a.pos)[o] = make_float4(nx, ny, nz, h.minT);
         return;
     }
@@ -1991,6 +2020,107 @@ extern "C" __global__ __launch_bounds__(256) void sf_band_unpack(FrameArgs a, co
     reinterpret_cast<float4*>(a.nrm)[o] = make_float4(v.x, v.y, v.z, 1.0f);
 }
 
+// Heap index -> its path digits (child numbers), deepest first, 4 bits each, and its depth (the reference's heap
+// numbering: child i of node n is 9 n + 1 + i, Sphereflake.h:162-172). Indices of depth <= SF_INDEX_SLAB_DEPTH.
+__device__ __forceinline__ uint32_t heap_path(uint32_t n, uint64_t& path)
+{
+    uint32_t d = 0;
+    path = 0;
+    while (n) {
+        const uint32_t q = (n - 1u) / 9u;
+        path |= (uint64_t)(n - 1u - 9u * q) << (4u * d);
+        n = q;
+        ++d;
+    }
+    return d;
+}
+
+// The frames of every node of depth <= SF_NODE_TABLE_DEPTH under the view's root transform, for the index slab
+// unpack: node n's 12 floats (xf layout of child_frame) as 3 float4. One thread per node, chained from the root
+// with child_frame -- the same float values the traversal builds (its per-ray form is sf_trace_ray's chain).
+extern "C" __global__ __launch_bounds__(256) void sf_node_table(FrameArgs a, float4* __restrict__ table, uint32_t nodes)
+{
+    const uint32_t n = blockIdx.x * 256u + threadIdx.x;
+    if (n >= nodes) return;
+    uint64_t path;
+    const uint32_t d = heap_path(n, path);
+    float xf[12], nx[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) xf[k] = a.root[k];
+    for (uint32_t j = 0; j < d; ++j) {
+        child_frame(a.consts, j, (uint32_t)(path >> (4u * (d - 1u - j))) & 15u, xf, nx);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) xf[k] = nx[k];
+    }
+    table[3u * n + 0u] = make_float4(xf[0], xf[1], xf[2], xf[3]);
+    table[3u * n + 1u] = make_float4(xf[4], xf[5], xf[6], xf[7]);
+    table[3u * n + 2u] = make_float4(xf[8], xf[9], xf[10], xf[11]);
+}
+
+// Index slabs -> the frame G-buffer (multi-GPU gather at 4 B per pixel). `stage` holds `members`
+// slabs of uint32 heap indices (SF_SLAB_MISS: no hit) laid out as sf_band_unpack's. A hit's pixel is rebuilt with
+// the tracer's own operations: the sphere's frame from the node table (its ancestor at depth <= table_depth) and
+// child_frame for the levels below, then the node's self test (Sphereflake.h:174-224: tca, d2, the near root with
+// r_d^2) gives minT, and shade's position dir * minT and normal Normalize(position - centre). One thread per
+// staged pixel along a slab row: coalesced 4-B reads, 2 x 16-B writes.
+extern "C" __global__ __launch_bounds__(256) void sf_slab_unpack4(FrameArgs a, const uint32_t* __restrict__ stage,
+                                                                   const float4* __restrict__ table,
+                                                                   uint32_t table_depth, uint32_t stage_rows,
+                                                                   uint32_t band_rows, uint32_t n, uint32_t first,
+                                                                   uint32_t members, uint32_t row0)
+{
+    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t sr = row0 + blockIdx.y;
+    const uint32_t m = blockIdx.z;
+    if (x >= a.W || m >= members) return;
+    const uint32_t k = first + m, i = sr / band_rows, r = sr % band_rows;
+    const uint32_t y = (i * n + k) * band_rows + r;
+    if (y >= a.H) return;
+    const uint32_t idx = stage[((size_t)m * stage_rows + sr) * a.W + x];
+    const size_t o = (size_t)y * a.W + x;
+    if (idx >= SF_SLAB_BAD) {   // a miss: (0, 0, 0, 1) twice; SF_SLAB_BAD (never made by a correct split): NaN
+        const float v = idx == SF_SLAB_MISS ? 0.0f : __builtin_nanf("");
+        reinterpret_cast<float4*>(a.pos)[o] = make_float4(v, v, v, 1.0f);
+        reinterpret_cast<float4*>(a.nrm)[o] = make_float4(v, v, v, 1.0f);
+        return;
+    }
+    const DeviceConsts* __restrict__ K = a.consts;
+    uint64_t path;
+    const uint32_t d = heap_path(idx, path);
+    const uint32_t td = d < table_depth ? d : table_depth;
+    uint32_t anc = idx;
+    for (uint32_t j = td; j < d; ++j) anc = (anc - 1u) / 9u;
+    float xf[12], nx[12];
+    {
+        const float4 c0 = table[3u * anc], c1 = table[3u * anc + 1u], c2 = table[3u * anc + 2u];
+        xf[0] = c0.x; xf[1] = c0.y; xf[2] = c0.z; xf[3] = c0.w;
+        xf[4] = c1.x; xf[5] = c1.y; xf[6] = c1.z; xf[7] = c1.w;
+        xf[8] = c2.x; xf[9] = c2.y; xf[10] = c2.z; xf[11] = c2.w;
+    }
+    for (uint32_t j = td; j < d; ++j) {
+        child_frame(K, j, (uint32_t)(path >> (4u * (d - 1u - j))) & 15u, xf, nx);
+#pragma unroll
+        for (int q = 0; q < 12; ++q) xf[q] = nx[q];
+    }
+    float dx, dy, dz;
+    ray_dir(a, (float)x, (float)y, dx, dy, dz, K->lut);
+    const float cx = xf[9], cy = xf[10], cz = xf[11];
+    const float tca = (cx * dx + cy * dy) + cz * dz;
+    const float d2 = ((cx * cx + cy * cy) + cz * cz) - tca * tca;
+    HitState h;
+    h.minT = near_root(tca, d2, K->dt.r2_self[d]);
+    h.cx = cx;
+    h.cy = cy;
+    h.cz = cz;
+    h.index = idx;
+    h.depth = (int32_t)d;
+    h.hit = true;
+    float px, py, pz, qx, qy, qz;
+    shade(dx, dy, dz, h, K->lut, px, py, pz, qx, qy, qz);
+    reinterpret_cast<float4*>(a.pos)[o] = make_float4(px, py, pz, 1.0f);
+    reinterpret_cast<float4*>(a.nrm)[o] = make_float4(qx, qy, qz, 1.0f);
+}
+
 // Re-traces flagged tiles with SF_MAX_LEVELS levels. Grid-stride over the list; reads this
 // render's counter and zeroes the other one (the next render's), so no memset is needed.
 extern "C" __global__ __launch_bounds__(64) void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list,
@@ -2043,20 +2173,7 @@ extern "C" __global__ __launch_bounds__(256) void sf_trace_ray(FrameArgs a)
     int32_t maxd = -1;
     bool overflowed = false;
 
-    auto make_child = [&](uint32_t p, uint32_t i) {
-        const float s = K->dt.scale[p];
-        const float* P = xf[p];
-        float* out = xf[p + 1];
-        for (int c = 0; c < 4; ++c) {
-            const float* B = K->child[i] + 4 * c;
-            const float b0 = c == 3 ? B[0] * s : B[0];
-            const float b1 = c == 3 ? B[1] * s : B[1];
-            const float b2 = c == 3 ? B[2] * s : B[2];
-            const float b3 = B[3];
-            for (int r = 0; r < 3; ++r)
-                out[3 * c + r] = ((P[r] * b0 + P[3 + r] * b1) + P[6 + r] * b2) + P[9 + r] * b3;
-        }
-    };
+    auto make_child = [&](uint32_t p, uint32_t i) { child_frame(K, p, i, xf[p], xf[p + 1]); };
 
     if (t.valid) {
         uint32_t d = 0;

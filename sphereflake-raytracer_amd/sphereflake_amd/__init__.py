@@ -88,6 +88,8 @@ SIGNATURES = {
                                     ctypes.c_void_p, ctypes.c_void_p]),
     "sf_slab_rows": (ctypes.c_uint32, [ctypes.c_uint32] * 4),
     "sf_unpack_bands": (ctypes.c_int, [_CTX, ctypes.c_void_p] + [ctypes.c_uint32] * 5 + [ctypes.c_void_p]),
+    "sf_unpack_slabs": (ctypes.c_int, [_CTX, ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [ctypes.c_void_p]),
+    "sf_slab_bytes": (ctypes.c_uint32, [_CTX]),
     "sf_download": (ctypes.c_int, [_CTX, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "sf_download_async": (ctypes.c_int, [_CTX, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
@@ -146,6 +148,7 @@ SIGNATURES = {
     "sf_group_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(sf_stats)]),
     "sf_group_last_hip_error": (ctypes.c_int, [ctypes.c_void_p]),
     "sf_group_reset_stats": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_group_slab_bytes": (ctypes.c_int, [ctypes.c_void_p]),
     "sf_dist_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "sf_dist_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
@@ -161,6 +164,8 @@ SIGNATURES = {
     "sf_dist_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(sf_stats)]),
     "sf_dist_reset_stats": (ctypes.c_int, [ctypes.c_void_p]),
     "sf_dist_last_error": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "sf_dist_comm_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int] + [ctypes.POINTER(ctypes.c_int)] * 3),
+    "sf_dist_slab_bytes": (ctypes.c_int, [ctypes.c_void_p]),
 }
 SF_ECOMM = -8
 SF_DIST_ID_BYTES = 128
@@ -352,10 +357,15 @@ class GBuffer:
     normals: np.ndarray
 
 
+SF_PACKED_NORMAL = 1   # band slab: float4 (nx, ny, nz, minT) per pixel, 16 B
+SF_PACKED_INDEX = 2    # band slab: uint32 hit index per pixel, 4 B (where slab_bytes() == 4)
+
+
 def render_params(band_rows=0, band_count=1, band_index=0, compact=False, kernel=SF_KERNEL_WAVE,
-                  emit_aux=False, max_depth=0, stream=None, packed=False) -> sf_render_params:
+                  emit_aux=False, max_depth=0, stream=None, packed=0) -> sf_render_params:
+    """packed: 0 / False (G-buffer layout), 1 / True (16 B slab), 2 (4 B hit-index slab)."""
     return sf_render_params(band_rows, band_count, band_index, int(bool(compact)), kernel, int(bool(emit_aux)),
-                            max_depth, int(bool(packed)), stream)
+                            max_depth, int(packed), stream)
 
 
 class _FifoLock:
@@ -475,6 +485,17 @@ class Sphereflake:
         -> this context's G-buffer at frame positions (sf_unpack_bands), with the current view."""
         _check(lib().sf_unpack_bands(self._ctx, ctypes.c_void_p(stage_ptr), stage_rows, band_rows, band_count,
                                      first_member, members, stream), "sf_unpack_bands", self._ctx)
+
+    def unpack_slabs(self, stage_ptr: int, bytes_per_pixel: int, stage_rows: int, band_rows: int, band_count: int,
+                     first_member: int, members: int, stream=None):
+        """Band slabs of either format (bytes_per_pixel 16: packed=1, 4: packed=2) -> this context's G-buffer
+        (sf_unpack_slabs), with the current view."""
+        _check(lib().sf_unpack_slabs(self._ctx, ctypes.c_void_p(stage_ptr), bytes_per_pixel, stage_rows, band_rows,
+                                     band_count, first_member, members, stream), "sf_unpack_slabs", self._ctx)
+
+    def slab_bytes(self) -> int:
+        """Bytes per pixel of the smallest lossless band slab for the current view (sf_slab_bytes: 4 or 16)."""
+        return int(lib().sf_slab_bytes(self._ctx))
 
     def device_buffers(self):
         ptrs = [ctypes.c_void_p() for _ in range(4)]
@@ -808,6 +829,10 @@ class SphereflakeGroup:
         self._check(lib().sf_group_get_stats(self._g, ctypes.byref(s)), "sf_group_get_stats")
         return s
 
+    def slab_bytes(self) -> int:
+        """Bytes per pixel a member ships for the current view (4: hit index, 16: normal + minT)."""
+        return int(lib().sf_group_slab_bytes(self._g))
+
 
 def dist_unique_id() -> bytes:
     """A fresh RCCL unique id (sf_dist_unique_id): rank 0 makes one per slot and hands them to every rank."""
@@ -922,6 +947,16 @@ class SphereflakeDist:
         if got < 0:
             _check(got, "sf_kernel_times", ctx)
         return out[:got]
+
+    def comm_info(self, slot: int = 0):
+        """(ncclCommCount, ncclCommUserRank, ncclCommCuDevice) of a slot's RCCL communicator (sf_dist_comm_info)."""
+        v = [ctypes.c_int() for _ in range(3)]
+        self._check(lib().sf_dist_comm_info(self._d, int(slot), *[ctypes.byref(x) for x in v]), "sf_dist_comm_info")
+        return tuple(x.value for x in v)
+
+    def slab_bytes(self) -> int:
+        """Bytes per pixel the gather ships for the current view (4: hit index, 16: normal + minT)."""
+        return int(lib().sf_dist_slab_bytes(self._d))
 
     def kernel_clocks(self, slot: int, n: int = 64):
         ctx = self.context(slot)

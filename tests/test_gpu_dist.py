@@ -22,28 +22,73 @@ def device():
     assert sf.device_count() >= 1, "no HIP device visible: GPU tests must run on an MI355X"
 
 
-@pytest.mark.parametrize("name,n,band", [("c2", 2, 8), ("c2", 3, 16), ("c3", 8, 8), ("c3", 3, 8), ("t3", 4, 8)])
-def test_packed_slabs_unpack_to_golden(name, n, band):
-    """Member 0's bands in place, members 1..n-1 as packed compact slabs unpacked beside them: the frame
-    equals the golden frame bit for bit (positions recomputed as dir * minT, misses (0,0,0,1))."""
+@pytest.mark.parametrize("packed", [sf.SF_PACKED_NORMAL, sf.SF_PACKED_INDEX])
+@pytest.mark.parametrize("name,n,band", [("c2", 2, 8), ("c2", 3, 16), ("c3", 8, 8), ("c3", 3, 8), ("t3", 4, 8),
+                                         ("c3", 5, 8), ("c4", 6, 8), ("c1", 7, 16), ("c2", 4, 24)])
+def test_packed_slabs_unpack_to_golden(name, n, band, packed):
+    """Member 0's bands in place, members 1..n-1 as packed compact slabs unpacked beside them: the frame equals the
+    golden frame bit for bit -- 16-B slabs (pos recomputed as dir * minT) and 4-B index slabs (the sphere's frame,
+    minT, pos and nrm rebuilt from the heap index), N = 2..8."""
     import torch
     fx = load_frame(name)
     W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
     rows = [sf.lib().sf_slab_rows(H, band, n, k) for k in range(n)]
     stage_rows = max(rows[1:])
-    stage = torch.full((n - 1, stage_rows, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+    bpp = 16 if packed == sf.SF_PACKED_NORMAL else 4
+    stage = torch.full((n - 1, stage_rows, W, bpp // 4), float("nan"), dtype=torch.float32, device="cuda")
     with sf.Sphereflake(W, H) as s:
         s.SetCamera(sf.config_camera(W, H, K))
+        assert s.slab_bytes() == 4   # (every BASELINE view but c5's proves its hits at depth <= 10)
         for rep in range(2):   # row-major, then the heavy-first unit order
             s.Render(band_rows=band, band_count=n, band_index=0)
             for k in range(1, n):
                 s.render_to(stage[k - 1].data_ptr(), 0, band_rows=band, band_count=n, band_index=k, compact=True,
-                            packed=True)
-            s.unpack_bands(stage.data_ptr(), stage_rows, band, n, 1, n - 1)
+                            packed=packed)
+            s.unpack_slabs(stage.data_ptr(), bpp, stage_rows, band, n, 1, n - 1)
             pos, nrm, _, _ = s.download()
             assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == [], (name, n, band, rep)
         st = s.stats()
     assert st.max_depth == fx["stats"]["max_depth"]
+
+
+def test_unpack_rejects_short_stage_and_wrapping_members():
+    """sf_unpack_slabs refuses a stage shorter than a member's slab (its last rows would stay stale) and a member
+    range that wraps around uint32 or leaves the split."""
+    import torch
+    W, H, n, band = 128, 100, 3, 8
+    rows = [sf.lib().sf_slab_rows(H, band, n, k) for k in range(n)]
+    stage = torch.zeros((n - 1, max(rows), W, 4), dtype=torch.float32, device="cuda")
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, 0.25))
+        for args in ((16, max(rows) - 1, band, n, 1, n - 1), (16, max(rows), band, n, 1, 0xffffffff),
+                     (16, max(rows), band, n, 2, 2), (8, max(rows), band, n, 1, n - 1)):
+            with pytest.raises(sf.SphereflakeError) as e:
+                s.unpack_slabs(stage.data_ptr(), *args)
+            assert e.value.code == sf.SF_EINVAL, args
+        s.unpack_slabs(stage.data_ptr(), 16, max(rows), band, n, 1, n - 1)   # (the valid call)
+        s.Synchronize()
+
+
+def test_slab_bytes_follow_the_view():
+    """4-B index slabs only where the view proves every hit at depth <= 10 (heap indices below 2^32): the BASELINE
+    views c1-c4; c5 (depth 10, hits one level deeper) and a camera inside the flake's bounding sphere ship 16 B, and
+    an index render there is refused."""
+    import torch
+    for name, want in (("c1", 4), ("c2", 4), ("c3", 4), ("c4", 4), ("c5", 16)):
+        fx = load_frame(name)
+        W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+        with sf.Sphereflake(64, 64) as s:   # (the format depends on the view, not the frame size)
+            s.SetCamera(sf.config_camera(64, 64, K))
+            assert s.slab_bytes() == want, name
+    with sf.Sphereflake(64, 64) as s:
+        cam = sf.config_camera(64, 64, 0.25)
+        cam.SetPosition([0.1, 0.2, 0.3])
+        s.SetCamera(cam)
+        assert s.slab_bytes() == 16
+        buf = torch.empty((64, 64), dtype=torch.int32, device="cuda")
+        with pytest.raises(sf.SphereflakeError) as e:
+            s.render_to(buf.data_ptr(), 0, packed=sf.SF_PACKED_INDEX)
+        assert e.value.code == sf.SF_EINVAL
 
 
 def test_packed_rejects_per_ray_kernel():

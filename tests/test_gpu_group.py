@@ -57,6 +57,24 @@ def test_group_on_one_device_equals_golden(name, members, band):
                 assert st.rays == (frame + 1) * e["rays"]   # accumulates like the reference's counter
 
 
+def test_group_both_slab_formats():
+    """The slab format follows the view (sf_group_slab_bytes): 4-B hit indices where every hit is provably at depth
+    <= 10, 16-B normal + minT slabs where not (a camera inside the flake's bounding sphere) -- either way the group's
+    frame equals a one-context render of the view bit for bit."""
+    W, H = 200, 120
+    far = sf.config_camera(W, H, 0.25)
+    near = sf.config_camera(W, H, 0.25)
+    near.SetPosition(np.asarray(sf.DEFAULT_CAMERA_POSITION, np.float32) * np.float32(0.2))   # (inside: c5's K)
+    for cam, want in ((far, 4), (near, 16), (far, 4)):
+        with sf.SphereflakeGroup([0] * 3, W, H) as g:
+            g.SetCamera(cam)
+            assert g.slab_bytes() == want
+            g.Render(8)
+            pos, nrm = g.download()
+        rp, rn, _ = single(W, H, cam)
+        assert same_bits(pos, rp) and same_bits(nrm, rn), want
+
+
 def test_group_moving_views_and_ragged_last_band():
     """H = 100 with 8-row bands over 3 members: 13 bands, the last one 4 rows (partial copy). A sequence
     of views, each frame equal to the one-context render of the same view."""

@@ -140,6 +140,72 @@ def test_packed_slab_format_is_lossless(name):
     assert np.all(ref["nrm4"][~hit][:, :3] == 0.0)
 
 
+def _index_unpack(setup, index, lut_fn):
+    """numpy float32 restatement of sf_slab_unpack4 for one frame: from each pixel's heap index (9n+1+i) rebuild the
+    sphere's frame down the chain from the root (Sphereflake.h:162-164, SIMD_AVX.h:59-81: column c = ((P0 b0 + P1 b1)
+    + P2 b2) + P3 b3, translation column scaled by (4/3) r_p), its self test's minT (tca, d2, the near root with
+    r_d^2, SIMD_AVX.h:236-270), then the position dir * minT and the normal Normalize(pos - centre)."""
+    f = np.float32
+    W, H = setup["W"], setup["H"]
+    child = setup["children"].reshape(9, 4, 4)          # [i][column][row], glm column-major
+    root = setup["root"].reshape(4, 4)
+    rad = setup["radius"]
+    dx, dy, dz = _ray_dirs(setup)
+    pos = np.zeros((H, W, 4), np.float32)
+    nrm = np.zeros((H, W, 4), np.float32)
+    pos[..., 3] = nrm[..., 3] = 1.0
+    for y in range(H):
+        for x in range(W):
+            n = int(index[y, x])
+            if n == 0xffffffff:
+                continue
+            digits = []
+            while n:
+                q = (n - 1) // 9
+                digits.append(n - 1 - 9 * q)
+                n = q
+            P = [root[c][:3].copy() for c in range(4)]
+            for p, i in enumerate(reversed(digits)):
+                s = f(f(4.0) / f(3.0)) * rad[p]
+                out = []
+                for c in range(4):
+                    b = child[i][c].copy()
+                    if c == 3:
+                        b[:3] = b[:3] * s
+                    out.append(((P[0] * b[0] + P[1] * b[1]) + P[2] * b[2]) + P[3] * b[3])
+                P = out
+            d = len(digits)
+            cx, cy, cz = P[3]
+            tca = (cx * dx[y, x] + cy * dy[y, x]) + cz * dz[y, x]
+            d2 = ((cx * cx + cy * cy) + cz * cz) - tca * tca
+            thc = np.sqrt(f(rad[d] * rad[d]) - d2, dtype=np.float32)
+            t0, t1 = tca + thc, tca - thc
+            t = t0 if t0 <= t1 else t1
+            px, py, pz = dx[y, x] * t, dy[y, x] * t, dz[y, x] * t
+            qx, qy, qz = px - cx, py - cy, pz - cz
+            ln = (qx * qx + qy * qy) + qz * qz
+            nr = f(lut_fn(float(ln)))
+            sc = (f(0.5) * nr) * (f(3.0) - (ln * nr) * nr)
+            pos[y, x, :3] = (px, py, pz)
+            nrm[y, x, :3] = (qx * sc, qy * sc, qz * sc)
+    return pos, nrm
+
+
+@pytest.mark.parametrize("name", ["t1", "t2", "t3", "t4", "t5"])
+def test_index_slab_format_is_lossless(name):
+    """An index slab pixel is the hit's heap index alone (4 B): rank 0 rebuilds the sphere's frame, minT, position and
+    normal from it (sf_slab_unpack4). On every golden pixel -- frames rendered by the reference itself -- that equals
+    the reference's position and normal bit for bit."""
+    from oracle import pyoracle
+    from sphereflake_amd import lib
+    setup = pyoracle.load_setup(name)
+    ref = load_npz(name)
+    assert int(ref["depth"].max()) <= 10   # (the index format's domain: heap indices below 2^32)
+    pos, nrm = _index_unpack(setup, ref["index"], lambda v: lib().sf_rsqrtps(v))
+    assert np.array_equal(pos.view(np.uint32), ref["pos4"].view(np.uint32))
+    assert np.array_equal(nrm.view(np.uint32), ref["nrm4"].view(np.uint32))
+
+
 def _ids_worker(rank, world, port, slots, errq, outq):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -209,17 +275,61 @@ def test_bench_control_combines_rank_stats(world):
 
 def test_bench_watchdog_prints_line_and_exits():
     """A leg past its deadline (the RCCL gather hanging on an unseen node): the watchdog runs its callback (rank 0
-    prints the line without that leg) and ends the process with status 0."""
+    prints the line with the leg marked failed) and ends the process with EXIT_GATHER_FAILED -- a hang is never a
+    success."""
     import subprocess
     import sys
     code = ("import sys, time; sys.path.insert(0, %r); import bench\n"
             "bench.Watchdog(0.5, lambda: print('LINE', flush=True))\n"
             "time.sleep(30)\nprint('NOT REACHED')\n") % REPO
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 0, r.stderr
+    import bench
+    assert r.returncode == bench.EXIT_GATHER_FAILED != 0, r.stderr
     assert r.stdout.strip() == "LINE"
     code2 = ("import sys, time; sys.path.insert(0, %r); import bench\n"
              "w = bench.Watchdog(1.0, lambda: print('LINE', flush=True))\nw.cancel()\ntime.sleep(1.5)\n"
              "print('DONE')\n") % REPO
     r = subprocess.run([sys.executable, "-c", code2], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and r.stdout.strip() == "DONE", r.stderr
+
+
+def _bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=REPO)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_gpus_n_spawns_the_ranks(n):
+    """`python3 bench.py --gpus N` with no launcher starts the N rank processes itself (torch.distributed.run on
+    127.0.0.1) before any GPU call: the line reports n_gpus N and every rank, each with its own local rank.
+    (--launch-check stops before rendering, so this runs on the CPU.)"""
+    r, line = _bench(["--gpus", str(n), "--launch-check"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert line is not None and line["n_gpus"] == n and line["spawned"] is True
+    assert sorted(x["rank"] for x in line["ranks"]) == list(range(n))
+    assert sorted(x["local_rank"] for x in line["ranks"]) == list(range(n))
+
+
+def test_bench_world_mismatch_exits_nonzero():
+    """A launcher world that is not --gpus ranks is refused (non-zero exit, no line): no silent 1-GPU measurement
+    labelled as N, no N ranks measured as 1."""
+    for world, gpus in ((3, 2), (2, 1)):
+        r, line = _bench(["--gpus", str(gpus), "--launch-check"],
+                         {"WORLD_SIZE": str(world), "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                          "MASTER_PORT": str(_free_port())}, timeout=120)
+        assert r.returncode != 0 and line is None, (world, gpus, r.stdout)
+        assert "--gpus" in r.stderr
+
+
+def test_bench_one_gpu_launch_check():
+    r, line = _bench(["--launch-check"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert line["n_gpus"] == 1 and line["spawned"] is False and len(line["ranks"]) == 1
