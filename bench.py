@@ -97,6 +97,7 @@ DEFAULT_SLOTS = 3                    # frames in flight: 1080p 0.149 / 0.140 / 0
 
 GATHER_TIMEOUT_S = 180.0             # the RCCL-gathered leg (multi-GPU) runs last, under a watchdog
 
+LONG_SETTLE_MS = 30.0               # before the steady-period loop (the GPU was idle only for the timed loop's readouts)
 SETTLE_MS = 150.0                    # the shader clock ramps from ~2075 to ~2370 MHz over the first ~60 ms of load
                                      # (profiles/r3/ramp.txt): warm-up lasts at least this long
 
@@ -280,21 +281,26 @@ def post_rates(ctx, torch, stream, width, height, reps=20):
     return out
 
 
-def progressive_rates(width, height, k, batch=1 << 18, reps=10):
+def progressive_rates(width, height, k, batch=1 << 18, reps=40, settle_ms=SETTLE_MS):
     """the frame-less mode (the reference's Initialize() worker stream: mt19937 draws,
     Sobol pixel picks, 8-ray AVX / 4-ray SSE packets with packet early-outs, last-writer scatter) on a
-    fresh context with the same camera, in batches of `batch` packets continuing one stream. Two untimed
-    batches first and a wait: the steady state of a running loop (the adaptive LDS levels follow the depth the
-    finished batches reached, the next batch's draws and bins are prefetched)."""
-    out = {"batch_packets": batch, "batches_timed": reps}
+    fresh context with the same camera, in batches of `batch` packets continuing one stream. Untimed batches
+    first, for at least `settle_ms` of load: the steady state of a running loop (the adaptive LDS levels follow
+    the depth the finished batches reached, the next batch's draws and bins are prefetched) at the steady shader
+    clock -- this leg follows the PCIe-bound transfer legs, after which the clock has dropped and ramps back over
+    ~60 ms of load (profiles/r3/ramp.txt), longer than a few timed batches."""
+    out = {"batch_packets": batch, "batches_timed": reps, "settle_ms": settle_ms}
     with sf.Sphereflake(width, height) as s:
         s.SetCamera(sf.config_camera(width, height, k))
         for variant, lanes in (("avx", 8), ("sse", 4)):
             s.SetVariant(variant)
             s.Progressive(12345, batch, 0)
             s.Synchronize()
-            s.Progressive(12345, batch)
-            s.Synchronize()
+            t_w = time.perf_counter()
+            while (time.perf_counter() - t_w) * 1e3 < settle_ms:
+                for _ in range(8):
+                    s.Progressive(12345, batch)
+                s.Synchronize()
             t = time.perf_counter()
             for _ in range(reps):
                 s.Progressive(12345, batch)
@@ -661,18 +667,27 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
     if st.overflow_tiles:
         raise RuntimeError("traversal overflowed SF_MAX_DEPTH_LIMIT")
     out["stats"] = st
-    if check and (rank == 0 or not gather):   # the last timed frame, outside the timed region
-        pos, nrm = d.download_slot(d.last_slot())
+    if check and (rank == 0 or not gather):   # the last timed frame, outside the timed region (downloaded now,
+        pos, nrm = d.download_slot(d.last_slot())   # checked after the long loop: no idle GPU before that loop)
         rows = mine[np.linspace(0, len(mine) - 1, min(12, len(mine))).astype(int)] if len(mine) else mine
-        out["checks"]["moving_oracle_rows"] = {"rows": len(rows), "bit_exact":
-                                               check_oracle_rows(pos, nrm, views[-1], width, height, rows)}
+        moving = (pos[rows].copy(), nrm[rows].copy(), rows)
         del pos, nrm
     if long_steps > steps:
+        # (a short settle first: the readouts above left the GPU idle for a few ms)
+        settle(d, render, views, max(1, warmup), time.perf_counter(), LONG_SETTLE_MS)
         t_long = timed(long_steps, lambda i: view_at(warmup + steps + i))
         period = (t_long - out["t_step"] * steps) / (long_steps - steps)
         out["pipeline"] = {"steady_frame_ms": round(period * 1e3, 5),
                            "fill_ms": round((out["t_step"] - period) * steps * 1e3, 5),
                            "long_steps": long_steps, "long_frame_ms": round(t_long / long_steps * 1e3, 5)}
+    if check and (rank == 0 or not gather):
+        p_rows, n_rows, rows = moving
+        pos = np.zeros((height, width, 4), np.float32)
+        nrm = np.zeros((height, width, 4), np.float32)
+        pos[rows], nrm[rows] = p_rows, n_rows
+        out["checks"]["moving_oracle_rows"] = {"rows": len(rows), "bit_exact":
+                                               check_oracle_rows(pos, nrm, views[-1], width, height, rows)}
+        del pos, nrm, moving
     if fixed:   # the same loop on one unchanging view (the config camera)
         cfg_view = frame_camera(width, height, k, 0).corners()
         d.SetView(*cfg_view)

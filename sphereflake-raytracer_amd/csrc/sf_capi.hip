@@ -237,6 +237,8 @@ struct sf_ctx {
     int order_mode = -1;
     uint32_t order_every = 0;          // env SF_ORDER_EVERY = k: rebuild the order after every k-th render only
                                        // (0 = auto: 3 for small frames, 1 otherwise)
+    bool order_record = true;
+    bool tie_inline = true;            // env SF_TIE_INLINE=0: ties under the front-first order go to sf_fixup_wave          // env SF_ORDER_RECORD=0: only the render before a rebuild records tile costs
     uint32_t order_phase = 0;          // renders since the last rebuild
     // Measurement: HIP events around the main trace kernel of each render (sf_set_kernel_timing)
     static constexpr int kTimed = 64;
@@ -475,6 +477,8 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     }
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_ORDER")) c->order_mode = std::atoi(ev) != 0 ? 1 : 0;
+    if (const char* ev = std::getenv("SF_TIE_INLINE")) c->tie_inline = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_ORDER_RECORD")) c->order_record = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_ORDER_EVERY")) c->order_every = std::atoi(ev) > 1 ? (uint32_t)std::atoi(ev) : 1u;   // (explicit)
     if (const char* ev = std::getenv("SF_PROG_BIN")) c->prog_bin = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_PREFETCH")) c->prog_prefetch = std::atoi(ev) != 0;
@@ -714,6 +718,11 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
         uint32_t* cnt = c->ovf_counters + c->parity;
         const uint32_t wpb = c->waves_per_block;
         const dim3 block(64 * wpb);
+        // levels proven sufficient on the persistent kernel: only a tie under the front-first child order can flag
+        // a tile, and its own wave re-traces it in index order -- no fixup launch after the trace
+        const bool front_first = (c->flags & (SF_FLAG_NO_OCCL_CULL | SF_FLAG_NO_FRONT_FIRST)) == 0u;
+        const bool tie_inline = bounded && c->persistent && front_first && c->tie_inline;
+        if (tie_inline) a.flags |= SF_FLAG_TIE_INLINE;
         if (c->persistent) {
             const void* kern = wpb == 1 ? (const void*)sf_trace_queue1
                              : wpb == 2 ? (const void*)sf_trace_queue2 : (const void*)sf_trace_queue4;
@@ -760,7 +769,9 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             const bool rebuild = use_order && (c->order_n != ntiles || c->order_phase + 1u >= every);
             if (use_order) c->order_phase = rebuild ? 0u : c->order_phase + 1u;
             if (use_order) {
-                a.tile_cost = c->tile_cost;
+                // tile costs: recorded by every render (order_record), or only by the render whose costs the
+                // rebuild reads
+                a.tile_cost = (rebuild || c->order_record) ? c->tile_cost : nullptr;
                 a.chunk_cnt = rebuild ? c->chunk_cnt : nullptr;
                 a.part_cost = c->part_cost;
                 a.part_done = c->part_done;
@@ -816,9 +827,9 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
         SF_HIP(c, hipGetLastError());
         // Re-trace of overflowed tiles (it also zeroes the next render's overflow counter itself). With the
         // levels proven sufficient (persistent kernel) only an exact tie under the front-first child order can
-        // flag a tile -- never seen on the BASELINE views --: then a small grid suffices.
-        const bool front_first = (c->flags & (SF_FLAG_NO_OCCL_CULL | SF_FLAG_NO_FRONT_FIRST)) == 0u;
-        if (!(bounded && c->persistent) || front_first) {
+        // flag a tile -- never seen on the BASELINE views --: its own wave re-traces it (tie_inline), or with
+        // SF_TIE_INLINE=0 the fixup's small grid.
+        if (!(bounded && c->persistent) || (front_first && !tie_inline)) {
             const size_t lds_fix = (size_t)SF_LDS_WAVE_FLOATS(SF_MAX_DEPTH_LIMIT) * 4;
             const uint32_t fb = (bounded && c->persistent) ? 8u : 4u * (uint32_t)c->fixup_blocks;
             hipLaunchKernelGGL(sf_fixup_wave, dim3(fb), dim3(64), lds_fix, s, a,

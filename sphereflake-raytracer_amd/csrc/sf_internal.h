@@ -80,8 +80,16 @@
 // children in index order only (A/B; results identical): by default the per-ray traversal enters the children
 // nearer than their parent's centre along the tile's cone axis first
 #define SF_FLAG_NO_FRONT_FIRST 0x200u
-// tests only: every tile of the main kernels takes the tie fallback (re-traced by sf_fixup_wave in index order)
+// tests only: every tile of the main kernels takes the tie fallback (re-traced in index order: by the same wave
+// under SF_FLAG_TIE_INLINE, else by sf_fixup_wave)
 #define SF_FLAG_DIAG_FORCE_RETRACE 0x400u
+// set by the host, never by a caller: the persistent trace's LDS levels are proven sufficient, so a tile can only be
+// flagged for an exact tie under the front-first child order, and the wave that traced it re-traces it in index order
+// at once (same levels, no overflow list, no fixup launch after the trace)
+#define SF_FLAG_TIE_INLINE 0x800u
+// (kernel-internal) the index-order re-trace pass of such a tile: its writes replace the first pass's, its cost is
+// not recorded
+#define SF_FLAG_REDO_PASS 0x1000u
 
 struct DepthTables {
     float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)

@@ -1403,13 +1403,18 @@ struct TileStats {
 // One lane's global atomic add on behalf of the wave, result broadcast to every lane. EXEC is set to
 // lane 0 inside the asm block, so the compiler's CFG has no lane-0-only region: such regions inside a
 // loop let the structurizer run lanes in different iterations, which breaks wave-uniform code.
+// A wave-uniform address, said to be so: it can go to an asm "s" operand (an SGPR pair) whatever the compiler's
+// divergence analysis concludes about how it was formed (the -fgpu-rdc link's can differ from the compile's).
+__device__ __forceinline__ uint32_t* uniform_ptr(uint32_t* p)
+{
+    const uint64_t pi = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pi), hi = __builtin_amdgcn_readfirstlane((uint32_t)(pi >> 32));
+    return reinterpret_cast<uint32_t*>((uint64_t)lo | ((uint64_t)hi << 32));
+}
+
 __device__ __forceinline__ uint32_t wave_fetch_add(uint32_t* p, uint32_t v)
 {
-    {   // the address is uniform: say so, so that it can go to the asm in an SGPR pair
-        const uint64_t pi = reinterpret_cast<uint64_t>(p);
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pi), hi = __builtin_amdgcn_readfirstlane((uint32_t)(pi >> 32));
-        p = reinterpret_cast<uint32_t*>((uint64_t)lo | ((uint64_t)hi << 32));
-    }
+    p = uniform_ptr(p);   // the address is uniform: say so, so that it can go to the asm in an SGPR pair
     uint32_t r, out;
     uint64_t saved;
     const uint32_t zero = 0u;
@@ -1432,6 +1437,7 @@ __device__ __forceinline__ uint32_t wave_fetch_add(uint32_t* p, uint32_t v)
 // compiler's own later waits stricter.
 __device__ __forceinline__ void wave_atomic_inc_nowait(uint32_t* p)
 {
+    p = uniform_ptr(p);
     uint64_t saved;
     const uint32_t zero = 0u, one = 1u;
     __asm__ volatile(
@@ -1447,6 +1453,7 @@ __device__ __forceinline__ void wave_atomic_inc_nowait(uint32_t* p)
 // One lane's global atomic max on behalf of the wave, completed before it returns (EXEC forced to lane 0).
 __device__ __forceinline__ void wave_atomic_max(uint32_t* p, uint32_t v)
 {
+    p = uniform_ptr(p);
     uint64_t saved;
     const uint32_t zero = 0u;
     __asm__ volatile(
@@ -1478,7 +1485,7 @@ __device__ __forceinline__ uint32_t part_axis_lane(uint32_t part)
 }
 
 struct NoPrefetch {
-    __device__ void operator()() const {}
+    __device__ void operator()(bool) const {}
 };
 
 // `pre` runs right after the traversal, before the tile's shading and stores: the persistent kernel takes
@@ -1487,11 +1494,13 @@ struct NoPrefetch {
 template <bool FIXUP, bool PIPE = false, class Prefetch = NoPrefetch>
 __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __restrict__ L, const float4 bcol, uint32_t tile,
                                                 uint32_t levels, uint32_t* overflow_list, uint32_t* overflow_count,
-                                                uint32_t part = 0u, const Prefetch& pre = Prefetch())
+                                                uint32_t part = 0u, const Prefetch& pre = Prefetch(), uint32_t fl = ~0u)
 {
+    // (fl: the launch's flags, with SF_FLAG_REDO_PASS | SF_FLAG_NO_FRONT_FIRST on a re-trace pass; ~0u: flags)
+    const uint32_t flags = fl == ~0u ? a.flags : fl;
     const DeviceConsts* __restrict__ K = a.consts;
     const uint32_t lane = threadIdx.x & 63u;
-    if (a.flags & SF_FLAG_DIAG_HALF) part = (a.flags & SF_FLAG_DIAG_HALF_SEL) ? 2u : 1u;
+    if (flags & SF_FLAG_DIAG_HALF) part = (flags & SF_FLAG_DIAG_HALF_SEL) ? 2u : 1u;
     const Tile t = tile_of(a, tile, lane, part);
     const uint64_t t_start = a.tile_trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint64_t c_start = (!FIXUP && a.tile_cost) ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -1507,16 +1516,21 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     // tie rule (see traverse). The fixup kernel always traces in index order.
 #ifndef SF_OLD_TRAVERSE
     traverse_ray<PIPE>(K, a.root, L, bcol, levels, dx, dy, dz, t.valid, h, maxd, status,
-                       FIXUP ? (a.flags | SF_FLAG_NO_FRONT_FIRST) : a.flags,
+                       FIXUP ? (flags | SF_FLAG_NO_FRONT_FIRST) : flags,
                        FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
 #else
     traverse<0, PIPE>(K, a.root, L, bcol, levels, dx, dy, dz, t.valid, h, maxd, status,
-                      FIXUP ? (a.flags | SF_FLAG_NO_FRONT_FIRST) : a.flags,
+                      FIXUP ? (flags | SF_FLAG_NO_FRONT_FIRST) : flags,
                       FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
 #endif
-    if (!FIXUP && (a.flags & SF_FLAG_DIAG_FORCE_RETRACE)) status |= SF_STATUS_TIE;
+    if (!FIXUP && (flags & (SF_FLAG_DIAG_FORCE_RETRACE | SF_FLAG_REDO_PASS)) == SF_FLAG_DIAG_FORCE_RETRACE)
+        status |= SF_STATUS_TIE;
     const bool overflowed = status != 0u;
-    pre();
+    // a tie under the front-first order with the levels proven (SF_FLAG_TIE_INLINE): this wave re-traces the unit
+    // in index order right after (trace_queue_body, told by `pre`); anything else flagged goes to the overflow list
+    const bool retrace = !FIXUP && __builtin_amdgcn_readfirstlane(
+                                       (int)(status == SF_STATUS_TIE && (flags & SF_FLAG_TIE_INLINE))) != 0;
+    pre(retrace);
     if (!FIXUP && a.tile_trace) {
         // diagnostics only: never read by the kernel, never feeds an output value. Every lane stores
         // the same (uniform) words: no lane-0-only region.
@@ -1534,7 +1548,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
 #endif
     }
 
-    if (!FIXUP && a.tile_cost && !(a.flags & SF_FLAG_DIAG_HALF)) {
+    if (!FIXUP && a.tile_cost && !(flags & (SF_FLAG_DIAG_HALF | SF_FLAG_REDO_PASS))) {
         // scheduling hint for the next render (sf_order_scan / sf_order_scatter); uniform values.
         const uint64_t cyc = __builtin_amdgcn_s_memtime() - c_start;
         uint32_t cost = cyc > 0xffffffffull ? 0xffffffffu : (uint32_t)cyc;
@@ -1561,7 +1575,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
             }
         }
     }
-    if (!FIXUP && overflowed) {
+    if (!FIXUP && overflowed && !retrace) {
         // a deeper (or index-order) re-trace (sf_fixup_wave) rewrites this whole tile
         const uint32_t slot = wave_fetch_add(overflow_count, 1u);
         overflow_list[slot] = tile;   // uniform value and address
@@ -1703,10 +1717,16 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 #endif
         // position in the render's unit order: the static first unit, then the ticket the previous tile
         // took after its traversal (past the end: the XCD's queue is empty)
+        // (or, bit 31 set, a unit to re-trace in index order: part << SF_UNIT_PRIO_SHIFT | tile -- a tie under the
+        // front-first order with SF_FLAG_TIE_INLINE; the ticket is taken after that pass)
         const uint32_t g = first;
-        if (g >= nunits) break;
+        const bool again = (g >> 31) != 0u;
+        if (!again && g >= nunits) break;
         uint32_t t = g, part = 0u;
-        if (at.tile_order) {      // heaviest tiles of the previous render first (scalar load)
+        if (again) {
+            t = g & SF_UNIT_TILE_MASK;
+            part = (g >> SF_UNIT_PRIO_SHIFT) & 7u;
+        } else if (at.tile_order) {      // heaviest tiles of the previous render first (scalar load)
 #if defined(__HIP_DEVICE_COMPILE__)
             typedef const __attribute__((address_space(4))) uint32_t* ConstU32;
             const uint32_t u = ((ConstU32)(const void*)at.tile_order)[g];
@@ -1729,11 +1749,13 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
         // the next unit's ticket, taken when this tile's traversal ends (see trace_tile)
         // (an agent-coherent load of the queue word before the atomic, to skip dry queues, made the frame
         // 1.7x slower: it contends with the atomics on the line)
-        auto ticket = [&]() {
-            first = nwaves + wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u) * nq + k;   // uniform
+        auto ticket = [&](bool retrace) {
+            first = retrace ? (0x80000000u | (part << SF_UNIT_PRIO_SHIFT) | t)
+                            : nwaves + wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u) * nq + k;   // uniform
         };
         const TileStats st = trace_tile<false, PIPE>(at, L, bcol, t, at.max_depth, at.overflow_list, at.counters + at.parity, part,
-                                               ticket);
+                                               ticket, again ? (at.flags | SF_FLAG_NO_FRONT_FIRST | SF_FLAG_REDO_PASS)
+                                                             : at.flags);
         if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace) {   // diagnostics only (uniform words)
             uint64_t* ut = at.tile_trace + 3u * (at.tiles_x * at.tile_rows) + SF_DIAG_SLOTS + 3u * g;
             ut[0] = u_start;

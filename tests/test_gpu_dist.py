@@ -57,26 +57,27 @@ def test_unpack_rejects_short_stage_and_wrapping_members():
     import torch
     W, H, n, band = 128, 100, 3, 8
     rows = [sf.lib().sf_slab_rows(H, band, n, k) for k in range(n)]
-    stage = torch.zeros((n - 1, max(rows), W, 4), dtype=torch.float32, device="cuda")
+    sr = max(rows[1:])   # (members 1..n-1 are unpacked; member 0's slab may be longer)
+    stage = torch.zeros((n - 1, sr, W, 4), dtype=torch.float32, device="cuda")
     with sf.Sphereflake(W, H) as s:
         s.SetCamera(sf.config_camera(W, H, 0.25))
-        for args in ((16, max(rows) - 1, band, n, 1, n - 1), (16, max(rows), band, n, 1, 0xffffffff),
-                     (16, max(rows), band, n, 2, 2), (8, max(rows), band, n, 1, n - 1)):
+        for args in ((16, sr - 1, band, n, 1, n - 1), (16, sr, band, n, 1, 0xffffffff),
+                     (16, sr, band, n, 2, 2), (8, sr, band, n, 1, n - 1), (16, sr, band, n, 3, 1)):
             with pytest.raises(sf.SphereflakeError) as e:
                 s.unpack_slabs(stage.data_ptr(), *args)
             assert e.value.code == sf.SF_EINVAL, args
-        s.unpack_slabs(stage.data_ptr(), 16, max(rows), band, n, 1, n - 1)   # (the valid call)
+        s.unpack_slabs(stage.data_ptr(), 16, sr, band, n, 1, n - 1)   # (the valid call)
         s.Synchronize()
 
 
 def test_slab_bytes_follow_the_view():
     """4-B index slabs only where the view proves every hit at depth <= 10 (heap indices below 2^32): the BASELINE
-    views c1-c4; c5 (depth 10, hits one level deeper) and a camera inside the flake's bounding sphere ship 16 B, and
-    an index render there is refused."""
+    views c1-c4, and a camera inside the root sphere (no depth-10 node comes near it); c5's camera (depth-10 nodes
+    expand, so hits lie one level deeper) ships 16 B, and an index render there is refused."""
     import torch
     for name, want in (("c1", 4), ("c2", 4), ("c3", 4), ("c4", 4), ("c5", 16)):
         fx = load_frame(name)
-        W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+        K = float.fromhex(fx["K"])
         with sf.Sphereflake(64, 64) as s:   # (the format depends on the view, not the frame size)
             s.SetCamera(sf.config_camera(64, 64, K))
             assert s.slab_bytes() == want, name
@@ -84,6 +85,8 @@ def test_slab_bytes_follow_the_view():
         cam = sf.config_camera(64, 64, 0.25)
         cam.SetPosition([0.1, 0.2, 0.3])
         s.SetCamera(cam)
+        assert s.slab_bytes() == 4
+        s.SetCamera(sf.config_camera(64, 64, 0.2))
         assert s.slab_bytes() == 16
         buf = torch.empty((64, 64), dtype=torch.int32, device="cuda")
         with pytest.raises(sf.SphereflakeError) as e:

@@ -757,22 +757,31 @@ def test_parallel_mt_draws_equal_sequential(sizes, monkeypatch):
     assert (st.max_depth, st.closest, st.rays) == (est.max_depth, est.closest, est.rays)
 
 
+@pytest.mark.parametrize("inline,order", [("1", ""), ("0", ""), ("1", "split")])
 @pytest.mark.parametrize("flags", ["0x200", "0x400"])
 @pytest.mark.parametrize("name", ["t3", "c2"])
-def test_front_first_order_and_tie_fallback(name, flags, monkeypatch):
+def test_front_first_order_and_tie_fallback(name, flags, inline, order, monkeypatch):
     """Children entered in index order only (SF_FLAG_NO_FRONT_FIRST), and every tile forced through the tie
-    fallback of the front-first order (SF_FLAG_DIAG_FORCE_RETRACE: the tile is queued like an overflow and
-    sf_fixup_wave re-traces it in index order, its small grid when the levels are proven): golden frames and
-    stats either way."""
+    fallback of the front-first order (SF_FLAG_DIAG_FORCE_RETRACE): with the levels proven, the tile's own wave
+    re-traces it in index order at once (SF_TIE_INLINE, default; also with the heavy-first order splitting tiles into
+    part units), or (SF_TIE_INLINE=0) it is queued like an overflow and sf_fixup_wave re-traces it: golden frames,
+    aux channels and stats every way."""
     monkeypatch.setenv("SF_FLAGS", flags)
+    monkeypatch.setenv("SF_TIE_INLINE", inline)
+    if order == "split":
+        monkeypatch.setenv("SF_ORDER", "1")
+        monkeypatch.setenv("SF_SPLIT_BUCKETS", "model")
+        monkeypatch.setenv("SF_SPLIT_PARTS", "4")
     fx = load_frame(name)
     W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
     with sf.Sphereflake(W, H) as s:
         s.SetCamera(sf.config_camera(W, H, K))
-        for _ in range(2):
+        for _ in range(3):
             s.Render(emit_aux=True)
             pos, nrm, mint, idx = s.download(aux=True)
             assert frame_digest(pos, nrm) == fx["frame_digest"], flags
+            if "row_digest_aux" in fx and fx.get("row_step", 1) == 1:
+                assert bad_rows(fx["row_digest_aux"], aux_digests(mint, idx)) == []
         st = s.stats()
     assert st.max_depth == fx["stats"]["max_depth"]
     assert np.float32(st.closest) == np.float32(float.fromhex(fx["stats"]["closest"]))
