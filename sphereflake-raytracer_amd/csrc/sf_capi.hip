@@ -229,15 +229,23 @@ struct sf_ctx {
     // and downloads issued on different streams of one context run in call order, as on one stream.
     hipStream_t last_stream = nullptr; // stream of the latest enqueued work (nullptr: the context stream)
     hipEvent_t join_ev = nullptr;      // the point later calls order after (see ctx_join / StreamMark)
-    // Heavy-first tile order: -1 (default) for frames whose tiles fill the persistent grid at most twice (small
-    // frames and multi-GPU shares, latency-bound: the heaviest tiles start first and may be split into parts),
-    // row-major on larger frames, where with frames in flight the order's kernels and per-tile cost recording
-    // cost more than the tail they shorten (round 3: 1080p 0.0816 -> 0.079 ms, 4K 0.382 -> 0.376 ms per frame);
-    // env SF_ORDER=0 never, SF_ORDER=1 always
+    // Heavy-first tile order: -1 (default) on whole frames whose tiles fill at most half the persistent grid's
+    // waves (640x360: rebuilt after every 3rd render, costs recorded by every render) and on whole frames of more
+    // than twice its waves (1080p and up: rebuilt after every 16th render from that render's costs only, model
+    // splits: no steady-state cost, shorter frame ends); row-major between (1280x720) and on multi-GPU shares, where
+    // with frames in flight the order measured slower (round 3); env SF_ORDER=0 never, SF_ORDER=1 always
     int order_mode = -1;
     uint32_t order_every = 0;          // env SF_ORDER_EVERY = k: rebuild the order after every k-th render only
-                                       // (0 = auto: 3 for small frames, 1 otherwise)
-    bool order_record = true;
+                                       // (0 = auto: 3 for small frames, 16 for frames over twice the grid, else 1)
+    int order_record_env = -1;         // env SF_ORDER_RECORD=0|1: tile costs recorded only by the render a rebuild
+                                       // reads / by every render (default: only on frames over twice the grid)
+    bool split_env = false;            // SF_SPLIT_BUCKETS given
+    // The frame-less prefetch stream at the device's greatest priority (env SF_PF_PRIO=0: normal): HIP deals streams
+    // over GPU_MAX_HW_QUEUES (4) hardware queues, and in a process that made other streams first (the bench) the
+    // prefetch stream shared the context stream's queue, serialising the next batch's draws behind this batch's
+    // trace: SSE 0.440 -> 0.306, AVX 0.607 -> 0.480 ms per 2^18-packet batch in the bench process; a fresh process
+    // measured 0.322 / 0.509 with normal priority (profiles/r4/frameless.txt)
+    bool pf_prio = true;
     bool tie_inline = true;            // env SF_TIE_INLINE=0: ties under the front-first order go to sf_fixup_wave          // env SF_ORDER_RECORD=0: only the render before a rebuild records tile costs
     uint32_t order_phase = 0;          // renders since the last rebuild
     // Measurement: HIP events around the main trace kernel of each render (sf_set_kernel_timing)
@@ -477,8 +485,9 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     }
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_ORDER")) c->order_mode = std::atoi(ev) != 0 ? 1 : 0;
+    if (const char* ev = std::getenv("SF_PF_PRIO")) c->pf_prio = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_TIE_INLINE")) c->tie_inline = std::atoi(ev) != 0;
-    if (const char* ev = std::getenv("SF_ORDER_RECORD")) c->order_record = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("SF_ORDER_RECORD")) c->order_record_env = std::atoi(ev) != 0 ? 1 : 0;
     if (const char* ev = std::getenv("SF_ORDER_EVERY")) c->order_every = std::atoi(ev) > 1 ? (uint32_t)std::atoi(ev) : 1u;   // (explicit)
     if (const char* ev = std::getenv("SF_PROG_BIN")) c->prog_bin = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PROG_PREFETCH")) c->prog_prefetch = std::atoi(ev) != 0;
@@ -491,6 +500,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     }
     if (const char* ev = std::getenv("SF_SPLIT_BUCKETS"))
         c->split_buckets = std::strcmp(ev, "model") == 0 ? SF_SPLIT_MODEL : (uint32_t)std::atoi(ev);
+    if (std::getenv("SF_SPLIT_BUCKETS")) c->split_env = true;
     if (const char* ev = std::getenv("SF_SPLIT_PARTS")) c->split_parts = std::atoi(ev) == 4 ? 4u : 2u;
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_PRIO_BUCKETS")) c->prio_buckets = (uint32_t)std::atoi(ev);
@@ -744,9 +754,20 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             // band row of the frame, and with frames in flight the order measured slower there at every N (1080p
             // over 8 GPUs: 0.0212 vs 0.0204 ms per frame, `profiles/r3/share2/r3aw.txt`).
             const bool tiny = 2u * ntiles <= nblk * wpb && band_count == 1u;
-            const bool use_order = c->order_mode > 0 || (c->order_mode < 0 && tiny);
+            // Round 4: whole frames of more than twice the grid's waves (1080p and up) take the order too, in a form
+            // that costs the steady state nothing: rebuilt after every 16th render from that render's tile costs
+            // alone (the renders between record nothing), heavy tiles split by the makespan model. With 3 frames in
+            // flight the steady frame period is unchanged (1080p 0.0787 vs 0.0792 ms, 4K 0.373 vs 0.373), but a
+            // frame whose successors are not yet queued -- the last of a timed loop, a lone frame -- no longer ends
+            // on its heaviest tiles' serial traversal: one frame alone 0.175 -> 0.151-0.164 ms at 1080p, and the
+            // driver's 20-step loop 0.0871 -> 0.0846 ms per frame (mean of 4 interleaved runs a side,
+            // profiles/r4/order_ab.txt). Frames between half and twice the grid (1280x720) measured slower with it
+            // (0.0358 -> 0.0388 ms) and keep the row-major order.
+            const bool large = !small && band_count == 1u;
+            const bool use_order = c->order_mode > 0 || (c->order_mode < 0 && (tiny || large));
+            const uint32_t split_buckets = (large && !c->split_env) ? SF_SPLIT_MODEL : c->split_buckets;
             // work units: tiles, or up to `split_parts` per tile when the schedule may split tiles
-            const uint32_t units_max = (use_order && c->split_buckets != 0u) ? c->split_parts * ntiles : ntiles;
+            const uint32_t units_max = (use_order && split_buckets != 0u) ? c->split_parts * ntiles : ntiles;
             const uint32_t need = (units_max + wpb - 1) / wpb;
             if (nblk > need) nblk = need;
             if (c->max_blocks && nblk > c->max_blocks) nblk = c->max_blocks;
@@ -765,13 +786,13 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             // order costs the trace nothing measurable while the two order kernels are ~5 us of a ~80 us
             // frame, so by default they are rebuilt after every 3rd render (640x360 -6 %, 1280x720 -4 %);
             // full grids are throughput-bound and a stale order costs more than the kernels (1080p).
-            const uint32_t every = c->order_every ? c->order_every : (small ? 3u : 1u);
+            const uint32_t every = c->order_every ? c->order_every : (small ? 3u : large ? 16u : 1u);
             const bool rebuild = use_order && (c->order_n != ntiles || c->order_phase + 1u >= every);
             if (use_order) c->order_phase = rebuild ? 0u : c->order_phase + 1u;
             if (use_order) {
-                // tile costs: recorded by every render (order_record), or only by the render whose costs the
-                // rebuild reads
-                a.tile_cost = (rebuild || c->order_record) ? c->tile_cost : nullptr;
+                // tile costs: recorded by every render, or only by the render whose costs the rebuild reads
+                const bool record = c->order_record_env >= 0 ? c->order_record_env != 0 : !large;
+                a.tile_cost = (rebuild || record) ? c->tile_cost : nullptr;
                 a.chunk_cnt = rebuild ? c->chunk_cnt : nullptr;
                 a.part_cost = c->part_cost;
                 a.part_done = c->part_done;
@@ -806,7 +827,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 // dispatch less on the frame's stream); more: one wave per chunk in a launch of its own
                 const bool fuse = nc <= SF_ORDER_FUSE_CHUNKS;
                 hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, c->chunk_cnt, nc, ntiles,
-                                   c->split_buckets, c->split_parts, spare, waves, c->prio_buckets, c->chunk_off,
+                                   split_buckets, c->split_parts, spare, waves, c->prio_buckets, c->chunk_off,
                                    c->order_meta, fuse ? (const uint32_t*)c->tile_cost : nullptr,
                                    fuse ? c->tile_order : nullptr);
                 SF_HIP(c, hipGetLastError());
@@ -1167,7 +1188,13 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     // the buffer the previous batch traced from, overlapped with this batch's trace.
     if (c->prog_prefetch && packets >= SF_PROG_PREFETCH_MIN) {
         if (!c->pf_stream) {
-            SF_HIP(c, hipStreamCreateWithFlags(&c->pf_stream, hipStreamNonBlocking));
+            if (c->pf_prio) {   // (a stream of the device's greatest priority: a hardware queue of its own)
+                int least = 0, greatest = 0;
+                SF_HIP(c, hipDeviceGetStreamPriorityRange(&least, &greatest));
+                SF_HIP(c, hipStreamCreateWithPriority(&c->pf_stream, hipStreamNonBlocking, greatest));
+            } else {
+                SF_HIP(c, hipStreamCreateWithFlags(&c->pf_stream, hipStreamNonBlocking));
+            }
             SF_HIP(c, hipEventCreateWithFlags(&c->pf_done, hipEventDisableTiming));
             SF_HIP(c, hipEventCreateWithFlags(&c->mt_ready, hipEventDisableTiming));
             SF_HIP(c, hipEventCreateWithFlags(&c->traced, hipEventDisableTiming));
@@ -1421,6 +1448,11 @@ int sf_post_process(sf_ctx* c, const sf_post_params* prm, const float* pos4, con
     a.fh = (float)c->H;
     a.faw = (float)aw;
     a.fah = (float)ah;
+    // uniform reciprocals, correctly rounded here once instead of per fragment (the same IEEE division)
+    a.rfw = 1.0f / a.fw;
+    a.rfh = 1.0f / a.fh;
+    a.rfaw = 1.0f / a.faw;
+    a.rfah = 1.0f / a.fah;
     a.pos = pos4 ? pos4 : c->pos;
     a.nrm = nrm4 ? nrm4 : c->nrm;
     a.noise = c->noise;

@@ -189,6 +189,7 @@ struct PostArgs {
     uint32_t W, H;                    // G-buffer (= blur / final target) size
     uint32_t aw, ah;                  // SSAO target size (W / downscale, H / downscale)
     float fw, fh, faw, fah;
+    float rfw, rfh, rfaw, rfah;       // RN(1 / fw) ... RN(1 / fah): the shaders' uniform reciprocals
     const float* pos;                 // float4 per pixel
     const float* nrm;
     const float* noise;               // SF_NOISE_SIZE^2 float4 (.xy read)

@@ -2119,14 +2119,25 @@ extern "C" __global__ __launch_bounds__(256) void sf_slab_unpack4(FrameArgs a, c
         xf[4] = c1.x; xf[5] = c1.y; xf[6] = c1.z; xf[7] = c1.w;
         xf[8] = c2.x; xf[9] = c2.y; xf[10] = c2.z; xf[11] = c2.w;
     }
-    for (uint32_t j = td; j < d; ++j) {
+    // the frames down to the parent, then only the sphere's centre: child_frame's translation column (the same
+    // operations on the same operands)
+    for (uint32_t j = td; j + 1u < d; ++j) {
         child_frame(K, j, (uint32_t)(path >> (4u * (d - 1u - j))) & 15u, xf, nx);
 #pragma unroll
         for (int q = 0; q < 12; ++q) xf[q] = nx[q];
     }
+    float cx = xf[9], cy = xf[10], cz = xf[11];
+    if (d > td) {
+        const uint32_t i = (uint32_t)path & 15u;
+        const float s = K->dt.scale[d - 1u];
+        const float* B = K->child[i] + 12;
+        const float b0 = B[0] * s, b1 = B[1] * s, b2 = B[2] * s, b3 = B[3];
+        cx = ((xf[0] * b0 + xf[3] * b1) + xf[6] * b2) + xf[9] * b3;
+        cy = ((xf[1] * b0 + xf[4] * b1) + xf[7] * b2) + xf[10] * b3;
+        cz = ((xf[2] * b0 + xf[5] * b1) + xf[8] * b2) + xf[11] * b3;
+    }
     float dx, dy, dz;
     ray_dir(a, (float)x, (float)y, dx, dy, dz, K->lut);
-    const float cx = xf[9], cy = xf[10], cz = xf[11];
     const float tca = (cx * dx + cy * dy) + cz * dz;
     const float d2 = ((cx * cx + cy * cy) + cz * cz) - tca * tca;
     HitState h;
