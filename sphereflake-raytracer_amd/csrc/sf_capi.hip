@@ -499,7 +499,8 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
         c->mt_seg_max = k < 2 ? 2u : k > (int)kMtSegMax ? kMtSegMax : (uint32_t)k;
     }
     if (const char* ev = std::getenv("SF_SPLIT_BUCKETS"))
-        c->split_buckets = std::strcmp(ev, "model") == 0 ? SF_SPLIT_MODEL : (uint32_t)std::atoi(ev);
+        c->split_buckets = std::strcmp(ev, "model") == 0 ? SF_SPLIT_MODEL
+                         : std::strcmp(ev, "auto") == 0 ? SF_SPLIT_AUTO : (uint32_t)std::atoi(ev);
     if (std::getenv("SF_SPLIT_BUCKETS")) c->split_env = true;
     if (const char* ev = std::getenv("SF_SPLIT_PARTS")) c->split_parts = std::atoi(ev) == 4 ? 4u : 2u;
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);

@@ -1756,7 +1756,7 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
         const TileStats st = trace_tile<false, PIPE>(at, L, bcol, t, at.max_depth, at.overflow_list, at.counters + at.parity, part,
                                                ticket, again ? (at.flags | SF_FLAG_NO_FRONT_FIRST | SF_FLAG_REDO_PASS)
                                                              : at.flags);
-        if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace) {   // diagnostics only (uniform words)
+        if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace && !again) {   // diagnostics only (uniform words)
             uint64_t* ut = at.tile_trace + 3u * (at.tiles_x * at.tile_rows) + SF_DIAG_SLOTS + 3u * g;
             ut[0] = u_start;
             ut[1] = __builtin_amdgcn_s_memrealtime();
