@@ -210,6 +210,9 @@ struct sf_ctx {
     // stats word, refreshed asynchronously after every render). Only sizes the traversal stack;
     // a tile that needs more is re-traced by sf_fixup_wave, so a stale hint costs time, never results.
     int32_t* h_depth = nullptr;
+    int32_t* h_stats = nullptr;        // pinned: the stats words, copied on the stream by sf_synchronize
+    bool stats_dirty = true;           // work was enqueued since the last sf_synchronize checked the stats
+    int32_t unresolved = 0;            // the stats' unresolved-tile count at the last check
     uint64_t* tile_trace = nullptr;    // diagnostics: per tile {start, end, hw id}
     // Heavy-first tile scheduling: every persistent render records per-tile cycles; sf_tile_order
     // turns them into the next render's tile permutation (heaviest first), so the tail of the
@@ -280,6 +283,7 @@ struct sf_ctx {
 // touches that stream again afterwards: the caller may destroy it once the work is done.
 static int ctx_join(sf_ctx* c, hipStream_t s)
 {
+    c->stats_dirty = true;   // (every call that enqueues work joins first)
     hipStream_t last = c->last_stream ? c->last_stream : c->stream;
     if (s == last) return SF_OK;
     if (last == c->stream) SF_HIP(c, hipEventRecord(c->join_ev, c->stream));   // (the context's own stream)
@@ -352,6 +356,7 @@ static void free_ctx(sf_ctx* c)
     if (c->pf_stream) (void)hipStreamDestroy(c->pf_stream);
     (void)hipFree(c->owner);
     if (c->h_depth) (void)hipHostFree(c->h_depth);
+    if (c->h_stats) (void)hipHostFree(c->h_stats);
     (void)hipFree(c->tile_trace);
     (void)hipFree(c->tile_cost);
     (void)hipFree(c->tile_order);
@@ -550,6 +555,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if ((e = hipMemsetAsync(c->chunk_cnt, 0, nchunks * SF_ORDER_BUCKETS * 4, c->stream)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->consts, sizeof(DeviceConsts))) != hipSuccess) return fail(e);
     if ((e = hipHostMalloc(&c->h_depth, 4, hipHostMallocDefault)) != hipSuccess) return fail(e);
+    if ((e = hipHostMalloc(&c->h_stats, 16, hipHostMallocDefault)) != hipSuccess) return fail(e);
     *c->h_depth = -1;
     // G-buffer starts as glm vec4() = (0,0,0,0) (Sphereflake.cpp:48-49, type_vec4.inl:59-64)
     if ((e = hipMemsetAsync(c->pos, 0, npx * 16, c->stream)) != hipSuccess) return fail(e);
@@ -1328,14 +1334,25 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
     return SF_OK;
 }
 
+// The stats words ride the stream in a small copy to pinned memory, queued behind the context's work, so the host
+// waits once (a synchronous hipMemcpy after the drain was a second round trip, ~10-20 us per call: per slot of a
+// dist, at the end of every timed loop and every lone frame); a context with nothing enqueued since the last call
+// only drains.
 int sf_synchronize(sf_ctx* c)
 {
     if (!c) return SF_EINVAL;
     DevGuard g(c->device);
+    const bool check = c->stats_dirty;
+    if (check) {
+        if (int rc_ = ctx_join(c, c->stream)) return rc_;
+        SF_HIP(c, hipMemcpyAsync(c->h_stats, c->stats, 12, hipMemcpyDeviceToHost, c->stream));
+    }
     if (int rc_ = ctx_drain(c)) return rc_;
-    int32_t st[3];
-    SF_HIP(c, hipMemcpy(st, c->stats, 12, hipMemcpyDeviceToHost));
-    if (st[2] != 0) return SF_EDEPTH;
+    if (check) {
+        c->stats_dirty = false;
+        c->unresolved = ((volatile int32_t*)c->h_stats)[2];
+    }
+    if (c->unresolved != 0) return SF_EDEPTH;
     return SF_OK;
 }
 

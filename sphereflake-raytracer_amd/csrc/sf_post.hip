@@ -103,13 +103,18 @@ __device__ inline float2 sample_noise(const float* noise, float u, float v)
 
 __device__ inline bool is_background(float4 p) { return p.x * p.x + p.y * p.y + p.z * p.z == 0.0f; }   // length == 0
 
-// post_ssao.glsl:19-25 occlude(); rx, ry = 1 / framebufferSize
-__device__ inline float occlude(const PostArgs& a, float fx, float fy, float ox, float oy, float rx, float ry, float4 p,
-                                float4 n)
+// post_ssao.glsl:19-25 occlude(), split in two: the tap's texel (NEAREST) and its sample, then the occlusion term
+// from the fetched sample -- so that ssao_at can have all 16 samples in flight before it uses the first (the taps
+// reach tens of pixels: each fetch is an L2 round trip, and one tap at a time left the kernel latency-bound)
+__device__ inline uint32_t tap_texel(const PostArgs& a, float fx, float fy, float ox, float oy, float rx, float ry)
 {
     const int tx = nearest((fx + ox) * rx, a.fw, (int)a.W);
     const int ty = nearest((fy + oy) * ry, a.fh, (int)a.H);
-    const float4 s = ld4(a.pos, (uint32_t)ty * a.W + (uint32_t)tx);
+    return (uint32_t)ty * a.W + (uint32_t)tx;
+}
+
+__device__ inline float occlude(const PostArgs& a, float4 s, float4 p, float4 n)
+{
     const float dx = s.x - p.x, dy = s.y - p.y, dz = s.z - p.z;
     const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
     const float id = 1.0f / dist;
@@ -136,7 +141,9 @@ __device__ inline uint8_t ssao_at(const PostArgs& a, uint32_t i, uint32_t j)
     const float len = sqrtf(qx * qx + qy * qy);
     const float il = 1.0f / len;
     const float nx = qx * il, ny = qy * il;
-    float ao = 0.0f;
+    // the 16 taps' texels and samples first (post_ssao.glsl:49-55: per kernel direction k, 0.25 c1, 0.75 c1,
+    // 0.5 c2, c2), then the terms summed in the shader's order
+    float4 s[16];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const float kx = k == 0 ? 1.0f : k == 1 ? -1.0f : 0.0f;   // kernel[4] (post_ssao.glsl:15)
@@ -144,11 +151,14 @@ __device__ inline uint8_t ssao_at(const PostArgs& a, uint32_t i, uint32_t j)
         const float f = 2.0f * (nx * kx + ny * ky);                 // reflect(I, N) = I - 2 dot(N, I) N
         const float c1x = (kx - f * nx) * rad, c1y = (ky - f * ny) * rad;
         const float c2x = c1x * 0.707f - c1y * 0.707f, c2y = c1x * 0.707f + c1y * 0.707f;
-        ao += occlude(a, fx, fy, c1x * 0.25f, c1y * 0.25f, rx, ry, p, n);
-        ao += occlude(a, fx, fy, c1x * 0.75f, c1y * 0.75f, rx, ry, p, n);
-        ao += occlude(a, fx, fy, c2x * 0.5f, c2y * 0.5f, rx, ry, p, n);
-        ao += occlude(a, fx, fy, c2x, c2y, rx, ry, p, n);
+        s[4 * k + 0] = ld4(a.pos, tap_texel(a, fx, fy, c1x * 0.25f, c1y * 0.25f, rx, ry));
+        s[4 * k + 1] = ld4(a.pos, tap_texel(a, fx, fy, c1x * 0.75f, c1y * 0.75f, rx, ry));
+        s[4 * k + 2] = ld4(a.pos, tap_texel(a, fx, fy, c2x * 0.5f, c2y * 0.5f, rx, ry));
+        s[4 * k + 3] = ld4(a.pos, tap_texel(a, fx, fy, c2x, c2y, rx, ry));
     }
+    float ao = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) ao += occlude(a, s[q], p, n);
     ao = ao / 16.0f;
     return quant(1.0f - ao);
 }
