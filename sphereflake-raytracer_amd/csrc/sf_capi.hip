@@ -26,6 +26,7 @@ extern "C" __global__ void sf_trace_queue1(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2(FrameArgs a);
 extern "C" __global__ void sf_trace_queue4(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2p(FrameArgs a);
+extern "C" __global__ void sf_trace_queue2c(FrameArgs a);
 extern "C" __global__ void sf_order_scan(uint32_t* chunk_cnt, uint32_t nc, uint32_t n_tiles,
                                          uint32_t split_buckets, uint32_t parts, uint32_t spare, uint32_t waves,
                                          uint32_t prio_buckets,
@@ -249,6 +250,7 @@ struct sf_ctx {
     // trace: SSE 0.440 -> 0.306, AVX 0.607 -> 0.480 ms per 2^18-packet batch in the bench process; a fresh process
     // measured 0.322 / 0.509 with normal priority (profiles/r4/frameless.txt)
     bool pf_prio = true;
+    bool compact = false;              // env SF_COMPACT=1: the trace kernel with active-ray compaction of sparse nodes
     bool tie_inline = true;            // env SF_TIE_INLINE=0: ties under the front-first order go to sf_fixup_wave          // env SF_ORDER_RECORD=0: only the render before a rebuild records tile costs
     uint32_t order_phase = 0;          // renders since the last rebuild
     // Measurement: HIP events around the main trace kernel of each render (sf_set_kernel_timing)
@@ -490,6 +492,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     }
     if (const char* ev = std::getenv("SF_PERSISTENT")) c->persistent = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_ORDER")) c->order_mode = std::atoi(ev) != 0 ? 1 : 0;
+    if (const char* ev = std::getenv("SF_COMPACT")) c->compact = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_PF_PRIO")) c->pf_prio = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_TIE_INLINE")) c->tie_inline = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("SF_ORDER_RECORD")) c->order_record_env = std::atoi(ev) != 0 ? 1 : 0;
@@ -742,8 +745,9 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
         if (tie_inline) a.flags |= SF_FLAG_TIE_INLINE;
         if (c->persistent) {
             const void* kern = wpb == 1 ? (const void*)sf_trace_queue1
-                             : wpb == 2 ? (const void*)sf_trace_queue2 : (const void*)sf_trace_queue4;
-            const int key = (int)(wpb * 64 + a.max_depth);
+                             : wpb == 2 ? (c->compact ? (const void*)sf_trace_queue2c : (const void*)sf_trace_queue2)
+                                        : (const void*)sf_trace_queue4;
+            const int key = (int)(wpb * 64 + a.max_depth) | (c->compact ? 1 << 20 : 0);
             if (c->occ_key != key) {
                 int nb = 0;
                 SF_HIP(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, (int)block.x, wpb * lds));
@@ -818,6 +822,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             const bool pipe = c->pipe >= 0 ? c->pipe == 1 : small;
             if (wpb == 1) hipLaunchKernelGGL(sf_trace_queue1, grid, block, lds, s, a);
             else if (wpb == 2 && pipe) hipLaunchKernelGGL(sf_trace_queue2p, grid, block, 2 * lds, s, a);
+            else if (wpb == 2 && c->compact) hipLaunchKernelGGL(sf_trace_queue2c, grid, block, 2 * lds, s, a);
             else if (wpb == 2) hipLaunchKernelGGL(sf_trace_queue2, grid, block, 2 * lds, s, a);
             else hipLaunchKernelGGL(sf_trace_queue4, grid, block, 4 * lds, s, a);
             SF_HIP(c, hipGetLastError());

@@ -1002,7 +1002,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
 // push, no load at the pop). A node keeps on the VGPR stack its untested children (the cone-culled mask,
 // front children first, as before) instead of its pending ones, and its visiting lanes as one bit per level
 // (`actbits`).
-template <bool PIPE = false>
+template <bool PIPE = false, bool COMPACT = false>
 __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ Lbase,
                                              const float4 bcol, uint32_t levels, float dx, float dy, float dz, bool valid,
                                              HitState& h, int32_t& maxd, uint32_t& status, uint32_t K_flags,
@@ -1291,6 +1291,49 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             actv = avx;
             SF_STAMP(1);
             C = expand(pc, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, avx, leafN);
+            if (COMPACT && C != 0u) {
+                // ---- Active-ray compaction of sparse nodes (north star: "wavefront ballot / prefix-sum active-ray
+                // compaction down the recursion"; sf_trace_queue2c, opt-in). Deep in the tree a node is often visited
+                // by a handful of the tile's rays, and each of its children then costs a wave-wide test for those few
+                // lanes. Where at most 7 lanes visit the node and 3 or more children are left, the visiting rays are
+                // packed by their prefix-sum rank (mbcnt of the ballot) into 7 LDS slots, replicated into 9 groups of 7
+                // lanes, and group g tests child g: every child's bounding test in ONE wave pass, the same float
+                // operations on bit-identical directions. Children no visiting ray hits leave the mask; the loop then
+                // tests the others per lane as before. A filter: no decision changes (results bit for bit).
+                __builtin_amdgcn_sched_barrier(0);   // (not interleaved with the expansion: register pressure)
+                const uint64_t actm = wave_ballot(avx > 0.0f);
+                const uint32_t na = (uint32_t)__builtin_popcountll(actm);
+                const uint32_t M = (C | (C >> 9)) & 0x1ffu;   // the untested children by index
+                if (na <= 7u && __builtin_popcount(M) >= 3) {
+                    const float R2b = depth_consts(K, d + 1u).x;
+                    // pack through the level's E words (unused by this traversal): visiting lane of rank k writes its
+                    // direction to slot k (16 B), the others to a junk slot; every lane reads the slot of its group
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(actm >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)actm, 0u));
+                    float* const sc = reinterpret_cast<float*>(L.E(d)) + 1;   // (16-byte aligned; 32 floats)
+                    *reinterpret_cast<float4*>(sc + (avx > 0.0f ? 4u * rank : 28u)) = make_float4(dx, dy, dz, 0.0f);
+                    lds_fence();
+                    uint32_t ln = lane;
+                    __asm__ volatile("" : "+v"(ln));   // (formed here, not hoisted and kept live across the DFS)
+                    const uint32_t g = (ln * 37u) >> 8;   // lane / 7 (exact for lanes 0..63)
+                    const uint32_t sl = ln - 7u * g;      // lane % 7
+                    const float4 q = *reinterpret_cast<const float4*>(sc + 4u * sl);
+                    const bool ok = sl < na && g < 9u && ((M >> g) & 1u) != 0u;
+                    const uint32_t gi = g < 9u ? g : 8u;
+                    const float4 cg = *reinterpret_cast<const float4*>(L.table(d) + gi * 4u);   // child g
+                    const float tca = (cg.x * q.x + cg.y * q.y) + cg.z * q.z;
+                    const float d2 = cg.w - tca * tca;
+                    const float xs = R2b - d2;
+                    const uint64_t bal =
+                        wave_ballot(__builtin_fminf(__builtin_fminf(tca, xs), ok ? __builtin_inff() : -1.0f) >= 0.0f);
+                    // child k is hit by some visiting ray iff bits 7k..7k+6 of the ballot are not all zero (lane k asks)
+                    const uint32_t kk = ln < 9u ? ln : 0u;
+                    const uint64_t grp = (bal >> (7u * kk)) & 0x7full;
+                    const uint32_t hitm = (uint32_t)wave_ballot(ln < 9u && grp != 0ull) & 0x1ffu;
+                    const uint32_t keep = __builtin_amdgcn_readfirstlane(hitm);
+                    C &= keep | (keep << 9);
+                }
+            }
             SF_STAMP(6);
             continue;
         }
@@ -1491,7 +1534,7 @@ struct NoPrefetch {
 // `pre` runs right after the traversal, before the tile's shading and stores: the persistent kernel takes
 // its next queue ticket there, so the atomic's round trip overlaps the shading instead of following the
 // G-buffer stores (whose completion a later wait would otherwise include: vmcnt counts in order).
-template <bool FIXUP, bool PIPE = false, class Prefetch = NoPrefetch>
+template <bool FIXUP, bool PIPE = false, class Prefetch = NoPrefetch, bool COMPACT = false>
 __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __restrict__ L, const float4 bcol, uint32_t tile,
                                                 uint32_t levels, uint32_t* overflow_list, uint32_t* overflow_count,
                                                 uint32_t part = 0u, const Prefetch& pre = Prefetch(), uint32_t fl = ~0u)
@@ -1515,7 +1558,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     // that order flags the tile like an overflow, and the fixup re-traces it in index order -- the reference's
     // tie rule (see traverse). The fixup kernel always traces in index order.
 #ifndef SF_OLD_TRAVERSE
-    traverse_ray<PIPE>(K, a.root, L, bcol, levels, dx, dy, dz, t.valid, h, maxd, status,
+    traverse_ray<PIPE, COMPACT>(K, a.root, L, bcol, levels, dx, dy, dz, t.valid, h, maxd, status,
                        FIXUP ? (flags | SF_FLAG_NO_FRONT_FIRST) : flags,
                        FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
 #else
@@ -1641,7 +1684,7 @@ extern "C" __global__ __launch_bounds__(256) void sf_trace_wave4(FrameArgs a, ui
 // atomic queue until it runs dry. Dynamic balancing: tile costs vary ~100x (sky vs. deep flake),
 // and the in-order workgroup dispatcher otherwise idles CUs behind long tiles. counters: [0,1]
 // overflow counts, [2,3] tile queues, alternating per render (this render zeroes the next one's).
-template <int WAVES, bool PIPE = false>
+template <int WAVES, bool PIPE = false, bool COMPACT = false>
 __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 {
     extern __shared__ float lds[];
@@ -1753,7 +1796,8 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
             first = retrace ? (0x80000000u | (part << SF_UNIT_PRIO_SHIFT) | t)
                             : nwaves + wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u) * nq + k;   // uniform
         };
-        const TileStats st = trace_tile<false, PIPE>(at, L, bcol, t, at.max_depth, at.overflow_list, at.counters + at.parity, part,
+        const TileStats st = trace_tile<false, PIPE, decltype(ticket), COMPACT>(at, L, bcol, t, at.max_depth, at.overflow_list,
+                                                                               at.counters + at.parity, part,
                                                ticket, again ? (at.flags | SF_FLAG_NO_FRONT_FIRST | SF_FLAG_REDO_PASS)
                                                              : at.flags);
         if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace && !again) {   // diagnostics only (uniform words)
@@ -1805,6 +1849,11 @@ extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue4(FrameArgs a)
 {
     trace_queue_body<4>(a);
+}
+// active-ray compaction of sparse nodes (opt-in, SF_COMPACT=1; see traverse_ray): measured against the default
+extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue2c(FrameArgs a)
+{
+    trace_queue_body<2, false, true>(a);
 }
 // latency variant (pipelined child loop) for frames whose tiles do not fill the persistent grid twice
 extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue2p(FrameArgs a)

@@ -812,3 +812,23 @@ def test_member_share_with_and_without_order_bit_exact(order, monkeypatch):
             assert np.array_equal(nrm[rows].view(np.uint32), ref_nrm[rows].view(np.uint32)), k
         # (sf_get_tile_order reports whole-frame orders only: a share's order is not readable through it)
         assert s.stats().overflow_tiles == 0
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3", "c4"])
+def test_active_ray_compaction_kernel_bit_exact(name, monkeypatch):
+    """The opt-in trace kernel with active-ray compaction of sparse nodes (SF_COMPACT=1, sf_trace_queue2c: the few
+    rays visiting a node packed by their prefix-sum rank so one wave pass tests all its children) is a filter: the
+    G-buffer, minT, hit index and stats equal the golden frame's on every render (row-major, then ordered)."""
+    monkeypatch.setenv("SF_COMPACT", "1")
+    fx = load_frame(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for k in range(2):
+            s.Render(emit_aux=True)
+            pos, nrm, mint, idx = s.download(aux=True)
+            assert bad_rows(fx["row_digest_gbuf"], row_digests(pos, nrm)) == [], (name, k)
+            if fx.get("row_step", 1) == 1:
+                assert bad_rows(fx["row_digest_aux"], aux_digests(mint, idx)) == [], (name, k)
+        st = s.stats()
+    assert st.max_depth == fx["stats"]["max_depth"] and st.overflow_tiles == 0

@@ -30,9 +30,15 @@ def random_view(rng, k):
     return W, H, K, cam
 
 
-@pytest.mark.parametrize("variant", ["avx", "sse"])
+@pytest.mark.parametrize("variant", ["avx", "sse", "compact"])
 @pytest.mark.parametrize("seed", range(16))
-def test_random_view_bit_exact(seed, variant):
+def test_random_view_bit_exact(seed, variant, monkeypatch):
+    """("compact": the AVX variant traced by the opt-in active-ray compaction kernel, SF_COMPACT=1 with the
+    throughput variant forced, SF_PIPE=0, since these small frames would take the latency variant.)"""
+    if variant == "compact":
+        monkeypatch.setenv("SF_COMPACT", "1")
+        monkeypatch.setenv("SF_PIPE", "0")
+        variant = "avx"
     rng = np.random.default_rng(1000 + seed)
     W, H, K, cam = random_view(rng, seed)
     o, tl, tr, bl = cam.corners()
@@ -53,3 +59,34 @@ def test_random_view_bit_exact(seed, variant):
         st = s.stats()
     assert st.max_depth == ref["stats"]["max_depth"]
     assert np.float32(st.closest) == np.float32(ref["stats"]["closest"])
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_view_band_slabs_bit_exact(seed):
+    """The multi-GPU slab formats on random views (camera scale 0.12-2.5: inside and outside the flake's bounding
+    ball, where the index format's depth proof succeeds or falls back): member 0's bands in place, members 1-2 as
+    slabs of the format sf_slab_bytes picks for the view, unpacked beside them -- the frame equals the oracle bit for
+    bit. When the view allows 4-B slabs the 16-B form is unpacked too."""
+    import torch
+    rng = np.random.default_rng(1000 + seed)
+    W, H, K, cam = random_view(rng, seed)
+    o, tl, tr, bl = cam.corners()
+    setup = {"W": W, "H": H, "origin": o, "tl": tl, "tr": tr, "bl": bl,
+             "root": sf.root_transform(o), "children": sf.child_transforms()}
+    ref = pyoracle.render(setup)
+    n, band = 3, 8
+    sr = max(sf.lib().sf_slab_rows(H, band, n, k) for k in range(1, n))
+    with sf.Sphereflake(W, H) as s:
+        s.SetView(o, tl, tr, bl)
+        fmts = [4, 16] if s.slab_bytes() == 4 else [16]
+        for bpp in fmts:
+            stage = torch.full((n - 1, sr, W, bpp // 4), float("nan"), dtype=torch.float32, device="cuda")
+            s.Render(band_rows=band, band_count=n, band_index=0)
+            for k in range(1, n):
+                s.render_to(stage[k - 1].data_ptr(), 0, band_rows=band, band_count=n, band_index=k, compact=True,
+                            packed=sf.SF_PACKED_INDEX if bpp == 4 else sf.SF_PACKED_NORMAL)
+            s.unpack_slabs(stage.data_ptr(), bpp, sr, band, n, 1, n - 1)
+            pos, nrm, _, _ = s.download()
+            what = f"seed {seed} {W}x{H} K={K:.3f} slab {bpp} B"
+            assert np.array_equal(pos.view(np.uint32), ref["pos4"].view(np.uint32)), what
+            assert np.array_equal(nrm.view(np.uint32), ref["nrm4"].view(np.uint32)), what
