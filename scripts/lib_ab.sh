@@ -12,7 +12,7 @@ for rep in $(seq 1 ${REPS:-3}); do
   for LF in "$@"; do
     L=${LF%@*}; F=0; [ "$L" != "$LF" ] && F=${LF#*@}
     SF_LIB_PARTIAL=1 SF_FLAGS=$F SF_LIB=$R/$L timeout -k 10 120 python3 -u bench.py --no-cpu-baseline --no-extras --steps 200 --warmup 30 $ARGS > $OUT/b.json
-    python3 -c "import json; j=json.loads(open('$OUT/b.json').read().strip().split(chr(10))[-1]); print('$LF', 'frame', j['frame_ms'], 'trace', j['roofline']['kernel_ms'], 'clk', j['roofline'].get('clock_mhz_live'), 'Mrays', j['value'], 'fixed', j['fixed_camera']['frame_ms'] if j.get('fixed_camera') else None)"
+    python3 -c "import json; j=json.loads(open('$OUT/b.json').read().strip().split(chr(10))[-1]); print('$LF', 'frame', j['frame_ms'], 'steady', j['pipeline']['steady_frame_ms'], 'clk', j['roofline'].get('clock_mhz_live'), 'Mrays', j['value'], 'fixed', j['fixed_camera']['frame_ms'] if j.get('fixed_camera') else None)"
   done
 done
 if [ "${PMC:-0}" = "1" ]; then

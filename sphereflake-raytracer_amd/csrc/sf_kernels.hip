@@ -1800,8 +1800,10 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
                                                                                at.counters + at.parity, part,
                                                ticket, again ? (at.flags | SF_FLAG_NO_FRONT_FIRST | SF_FLAG_REDO_PASS)
                                                              : at.flags);
-        if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace && !again) {   // diagnostics only (uniform words)
-            uint64_t* ut = at.tile_trace + 3u * (at.tiles_x * at.tile_rows) + SF_DIAG_SLOTS + 3u * g;
+        if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace) {   // diagnostics only (uniform words)
+            // (g & SF_UNIT_TILE_MASK: a re-trace pass's ticket word carries bit 31 and the part; masked, its record
+            // lands in range -- on its tile's slot -- without keeping a flag live across the traversal)
+            uint64_t* ut = at.tile_trace + 3u * (at.tiles_x * at.tile_rows) + SF_DIAG_SLOTS + 3u * (g & SF_UNIT_TILE_MASK);
             ut[0] = u_start;
             ut[1] = __builtin_amdgcn_s_memrealtime();
             ut[2] = t | (part << SF_UNIT_PART_SHIFT);
