@@ -1,0 +1,56 @@
+"""Host logic of bench.py on the CPU: the parity check of the timed frames (golden row digests, the rows a rank
+owns), the roofline/issue arithmetic on the frame period, and the rank launcher's world check."""
+import numpy as np
+import pytest
+
+from conftest import REPO, load_frame, load_npz
+
+import bench
+
+
+@pytest.mark.parametrize("name", ["t1", "t2", "t3"])
+def test_golden_row_check_accepts_reference_frame_and_flags_a_bit(name):
+    """check_golden_rows: the reference-rendered frame passes every row; one flipped mantissa bit in one pixel is
+    reported as that row (the bench exits 5 on it)."""
+    fx = load_frame(name)
+    ref = load_npz(name)
+    pos, nrm = ref["pos4"].copy(), ref["nrm4"].copy()
+    H = pos.shape[0]
+    n, bad = bench.check_golden_rows(pos, nrm, fx, np.arange(H))
+    assert n == H and bad == []
+    y = H // 2
+    nrm.view(np.uint32)[y, 3, 1] ^= 1
+    n, bad = bench.check_golden_rows(pos, nrm, fx, np.arange(H))
+    assert bad == [y]
+
+
+def test_golden_row_check_respects_row_step_and_ownership():
+    """Only the rows the fixture holds (every row_step-th) and the rows this rank owns are checked."""
+    fx = load_frame("t3")
+    ref = load_npz("t3")
+    H = ref["pos4"].shape[0]
+    fx2 = dict(fx, row_step=2, row_digest_gbuf=fx["row_digest_gbuf"][::2])
+    rows = bench.owned_rows(H, 8, 3, 1)
+    n, bad = bench.check_golden_rows(ref["pos4"], ref["nrm4"], fx2, rows)
+    assert bad == [] and n == len([y for y in rows if y % 2 == 0])
+
+
+@pytest.mark.parametrize("H,band,world", [(1080, 8, 8), (45, 8, 3), (7, 8, 2)])
+def test_owned_rows_partition_the_frame(H, band, world):
+    rows = np.concatenate([bench.owned_rows(H, band, world, r) for r in range(world)])
+    assert np.array_equal(np.sort(rows), np.arange(H))
+    assert np.array_equal(bench.owned_rows(H, band, 1, 0), np.arange(H))
+
+
+def test_issue_fractions_on_the_frame_period():
+    """pmc_valu prices the PMC instruction counts on one frame period at the live clock: VALU over 1024 SIMDs x
+    cycles / 2, SALU over 256 CUs x cycles; the lone-dispatch view stays separate."""
+    c = {"SQ_INSTS_VALU": 59.5e6, "SQ_INSTS_SALU": 33.0e6, "GRBM_GUI_ACTIVE": 8 * 300000.0, "SQ_WAVE_CYCLES": 3.5e8,
+         "profiled_dispatch_us": 130.0, "SQ_WAIT_INST_ANY": 1.35e8, "SQ_WAIT_ANY": 1.0e8}
+    v = bench.pmc_valu(c, 0.078, 2370.0)
+    fc = 0.078e-3 * 2370e6
+    assert v["frame_cycles"] == round(fc)
+    assert abs(v["valu_issue_frac"] - 59.5e6 / (1024 * fc / 2)) < 1e-4
+    assert abs(v["salu_issue_frac"] - 33.0e6 / (256 * fc)) < 1e-4
+    assert v["lone_dispatch"]["valu_issue_frac"] == round(59.5e6 / (1024 * 300000.0 / 2), 4)
+    assert bench.pmc_valu(None, 0.078, 2370.0) is None
