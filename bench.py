@@ -98,10 +98,10 @@ DEFAULT_SLOTS = 3                    # frames in flight: 1080p 0.149 / 0.140 / 0
 GATHER_TIMEOUT_S = 180.0             # the RCCL-gathered leg (multi-GPU) runs last, under a watchdog
 
 LONG_SETTLE_MS = 30.0               # before the steady-period loop (the GPU was idle only for the timed loop's readouts)
-SETTLE_MS = 400.0                    # the shader clock ramps from ~2075 to ~2370 MHz over the first ~60 ms of load on
-                                     # most boxes (profiles/r3/ramp.txt), but one round-4 box still ran the timed loop
-                                     # at 2241 MHz after 150 ms and its later loop faster (profiles/r4/r4f): warm-up
-                                     # lasts at least this long
+SETTLE_MS = 150.0                    # the shader clock ramps from ~2075 to ~2370 MHz over the first ~60 ms of load
+                                     # (profiles/r3/ramp.txt): warm-up lasts at least this long. (Under sustained load
+                                     # the chip may then give clock back -- 2134-2380 MHz across round-4 boxes and
+                                     # settle lengths, profiles/r4/final: the line reports the live clock.)
 
 
 def settle(d, render, views, n_views, t_start, ms):
@@ -936,8 +936,8 @@ def main():
             "warmup": args.warmup,
             "settle": {"min_ms": args.settle_ms, "frames": r["settle_frames"],
                        "note": "untimed frames after --warmup until the GPU has been under load min_ms: the shader "
-                               "clock ramps from ~2075 to ~2370 MHz over the first ~60 ms on most boxes, slower on "
-                               "some (profiles/r3/ramp.txt, profiles/r4/r4f)"},
+                               "clock ramps from ~2075 to ~2370 MHz over the first ~60 ms (profiles/r3/ramp.txt); "
+                               "the clock the timed loop ran at is roofline.clock_mhz_live"},
             "ms_per_step": round(t_step * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong" if args.mode == "dist" else "weak",
