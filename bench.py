@@ -91,8 +91,25 @@ def parse():
     return ap.parse_args()
 
 
-DEFAULT_SLOTS = 3                    # frames in flight: 1080p 0.149 / 0.140 / 0.136 / 0.133 ms per frame at 1-4
-                                     # (profiles/r3/overlap_1080.txt); 3 keeps the latency at ~3 frames
+DEFAULT_SLOTS = 0                    # frames in flight: 0 = by the share's tiles (frames_in_flight)
+SLOTS_FULL, SLOTS_SHARE = 3, 4       # 1080p: 3 in flight 0.0751 ms steady, 4 0.0792 (the frame fills the grid);
+                                     # a member's share over 8 GPUs: 3 0.0194 ms, 4 0.0156-0.0160, 5 0.0174-0.0232,
+                                     # 6 0.020 (the process's 4 hardware queues); over 4: 0.0247 / 0.0235; over 2:
+                                     # 0.0452 / 0.0459 (profiles/r4/slots/)
+SHARE_GRID_FRAC = 1.5                # a share of at most this many persistent-grid waves' worth of tiles takes 4
+GRID_WAVES_PER_CU = 32               # the trace kernel's grid: 4 SIMDs x 8 waves per CU (LDS-limited occupancy)
+
+
+def frames_in_flight(requested, cus, width, height, band_rows, n):
+    """Frames in flight for a loop whose rank renders rank 0's bands of an n-way split (n = 1: whole frames).
+    A share that leaves most of the persistent grid's wave slots idle is bounded by the per-frame chain
+    (trace, order, host enqueue: ~55-60 us for a 1080p share over 8) over the frames that overlap, so it takes
+    one frame more; frames that fill the grid are throughput-bound and a 4th frame only adds contention."""
+    if requested:
+        return max(1, min(8, requested))
+    rows = sf.lib().sf_slab_rows(height, band_rows, n, 0) if n > 1 else height
+    tiles = -(-width // 8) * -(-rows // 8)
+    return SLOTS_SHARE if tiles <= SHARE_GRID_FRAC * GRID_WAVES_PER_CU * cus else SLOTS_FULL
 
 
 GATHER_TIMEOUT_S = 180.0             # the RCCL-gathered leg (multi-GPU) runs last, under a watchdog
@@ -629,15 +646,20 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
         render()
         d.Synchronize()
         out["first_render_ms"] = (time.perf_counter() - t) * 1e3
+    # Kernel timing is switched on before the warm-up: the first switch-on creates each slot's events and clock
+    # buffer (~5.7 ms of host calls at 3 slots), and an idle GPU gives its clock back within that gap -- a timed loop
+    # started after it ran at 2200-2240 MHz instead of ~2375 (0.085 vs 0.0785 ms per frame, profiles/r4/clock/).
+    # Switched on again after the settle, it only restarts the sample ring (host state, no GPU call).
+    kp = slot_period(steps, slots)
+    for s in range(slots):
+        d.kernel_timing(s, True, period=kp)
     t_w = time.perf_counter()
     for i in range(warmup):
         d.SetView(*views[i])
         render()
     out["settle_frames"] = settle(d, render, views, max(1, warmup), t_w, settle_ms)
-    kp = slot_period(steps, slots)
     for s in range(slots):
         d.kernel_timing(s, True, period=kp)
-    d.Synchronize()
     d.reset_stats()
 
     def timed(n, view_of):
@@ -677,11 +699,19 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
     if long_steps > steps:
         # (a short settle first: the readouts above left the GPU idle for a few ms)
         settle(d, render, views, max(1, warmup), time.perf_counter(), LONG_SETTLE_MS)
+        kpl = slot_period(long_steps, slots)
+        for s in range(slots):   # the live clock of this loop too (the chip's clock moves between loops)
+            d.kernel_timing(s, True, period=kpl)
         t_long = timed(long_steps, lambda i: view_at(warmup + steps + i))
+        clk_l = []
+        for s in range(slots):
+            clk_l += list(d.kernel_clocks(s, n=64))
+            d.kernel_timing(s, False)
         period = (t_long - out["t_step"] * steps) / (long_steps - steps)
         out["pipeline"] = {"steady_frame_ms": round(period * 1e3, 5),
                            "fill_ms": round((out["t_step"] - period) * steps * 1e3, 5),
-                           "long_steps": long_steps, "long_frame_ms": round(t_long / long_steps * 1e3, 5)}
+                           "long_steps": long_steps, "long_frame_ms": round(t_long / long_steps * 1e3, 5),
+                           "long_clock_mhz_live": round(float(np.median(clk_l)), 1) if clk_l else None}
     if check and (rank == 0 or not gather):
         p_rows, n_rows, rows = moving
         pos = np.zeros((height, width, 4), np.float32)
@@ -832,7 +862,8 @@ def main():
         return 0
 
     ranks = rank_devices(ctl, gpu)
-    slots = max(1, min(8, args.slots))
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    slots = frames_in_flight(args.slots, cus, width, height, args.band_rows, n if args.mode == "dist" else 1)
     if args.mode == "dist":
         # the frame split over the ranks, each rank's bands into its own HBM (the distributed G-buffer)
         r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
@@ -853,7 +884,8 @@ def main():
     # weak-scaling companion of a multi-GPU run: every rank renders its own frames (no gather)
     indep = None
     if args.mode == "dist" and n > 1:
-        ri = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, 1,
+        ri = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup,
+                       frames_in_flight(args.slots, cus, width, height, args.band_rows, 1), args.band_rows, 1,
                        lambda i: i * n + rank, settle_ms=args.settle_ms)
         ri["dist"].close()
         indep = {"value": round(n * width * height / ri["t_step"] / 1e6, 2), "frame_ms": round(ri["t_step"] * 1e3, 4),
@@ -862,7 +894,9 @@ def main():
     # BASELINE configs[3] (3840x2160, K = 0.22, depth 9) on the same path, all ranks
     c4 = None
     if not args.no_extras and (width, height, round(args.K, 4)) == (W, H, K):
-        r4 = dist_loop(ctl, torch, dev, 3840, 2160, 0.22, 60, 15, slots, args.band_rows,
+        r4 = dist_loop(ctl, torch, dev, 3840, 2160, 0.22, 60, 15,
+                       frames_in_flight(args.slots, cus, 3840, 2160, args.band_rows, n if args.mode == "dist" else 1),
+                       args.band_rows,
                        n if args.mode == "dist" else 1, (lambda i: i) if args.mode == "dist" else (lambda i: i * n + rank),
                        settle_ms=args.settle_ms)
         rays0_4 = (sf.lib().sf_slab_rows(2160, args.band_rows, n, 0) if args.mode == "dist" else 2160) * 3840
@@ -1006,7 +1040,9 @@ def main():
         if rank == 0:
             out["gathered_on_rank0"] = {"error": f"not finished within {args.gather_timeout:g} s"}
         wd = Watchdog(args.gather_timeout, (lambda: print(json.dumps(out), flush=True)) if rank == 0 else (lambda: None))
-        gathered = gather_leg(args, ctl, torch, dev, slots, n, rays_step, check)
+        # (3 in flight whatever the share: rank 0 also runs a receive stream per slot, and more streams than the
+        # process's 4 hardware queues put a waiting receive in front of another slot's trace)
+        gathered = gather_leg(args, ctl, torch, dev, args.slots or SLOTS_FULL, n, rays_step, check)
         wd.cancel()
         if rank == 0:
             out["gathered_on_rank0"] = gathered
