@@ -54,3 +54,13 @@ def test_issue_fractions_on_the_frame_period():
     assert abs(v["salu_issue_frac"] - 33.0e6 / (256 * fc)) < 1e-4
     assert v["lone_dispatch"]["valu_issue_frac"] == round(59.5e6 / (1024 * 300000.0 / 2), 4)
     assert bench.pmc_valu(None, 0.078, 2370.0) is None
+
+
+@pytest.mark.parametrize("w,h,n,want", [(1920, 1080, 1, 3), (1920, 1080, 2, 3), (1920, 1080, 4, 4), (1920, 1080, 8, 4),
+                                        (640, 360, 1, 4), (1280, 720, 1, 3), (3840, 2160, 8, 3), (3840, 2160, 1, 3)])
+def test_frames_in_flight_by_share(w, h, n, want):
+    """4 frames in flight where rank 0's share of 8x8 tiles is at most 1.5 persistent grids (256 CUs x 32 waves),
+    else 3; an explicit --slots wins (clamped to 1..8)."""
+    assert bench.frames_in_flight(0, 256, w, h, 8, n) == want
+    assert bench.frames_in_flight(5, 256, w, h, 8, n) == 5
+    assert bench.frames_in_flight(99, 256, w, h, 8, n) == 8
