@@ -25,6 +25,7 @@
 
 #include <cstdint>
 
+#include "sf_fastmath.h"
 #include "sf_internal.h"
 
 namespace {
@@ -41,6 +42,16 @@ __device__ inline int nearest(float u, float size, int n)   // NEAREST, CLAMP_TO
 {
     const int t = (int)floorf(snap(u * size, size) * (1.0f / 256.0f));
     return min(max(t, 0), n - 1);
+}
+
+// nearest() in fewer operations, the same texel for every u (NaN and infinities included): s256 = 256 size, hi =
+// 256 n - 1. (u size) 256 rounds as u (256 size) (a power-of-two scale commutes with rounding; where u size is
+// subnormal both snap to texel 0, where they overflow both are +-inf); clamping the snapped coordinate to [0, 256 n -
+// 1] before the floor gives the texel clamped to [0, n - 1] after it (below 0 both give texel 0, at or above 256 n - 1
+// both give n - 1, NaN: 0 in both); and floor(k / 256) of the integer k = rint(...) is k >> 8.
+__device__ inline uint32_t nearest_fast(float u, float s256, float hi)
+{
+    return (uint32_t)rintf(fminf(fmaxf(u * s256, 0.0f), hi)) >> 8;
 }
 
 struct Lin {
@@ -106,14 +117,19 @@ __device__ inline bool is_background(float4 p) { return p.x * p.x + p.y * p.y + 
 // post_ssao.glsl:19-25 occlude(), split in two: the tap's texel (NEAREST) and its sample, then the occlusion term
 // from the fetched sample -- so that ssao_at can have all 16 samples in flight before it uses the first (the taps
 // reach tens of pixels: each fetch is an L2 round trip, and one tap at a time left the kernel latency-bound)
-__device__ inline uint32_t tap_texel(const PostArgs& a, float fx, float fy, float ox, float oy, float rx, float ry)
+struct TapAxes {
+    float sw, hw, sh, hh;   // 256 W, 256 W - 1, 256 H, 256 H - 1 (nearest_fast)
+};
+
+__device__ inline uint32_t tap_texel(const PostArgs& a, const TapAxes& ax, float fx, float fy, float ox, float oy,
+                                     float rx, float ry)
 {
-    const int tx = nearest((fx + ox) * rx, a.fw, (int)a.W);
-    const int ty = nearest((fy + oy) * ry, a.fh, (int)a.H);
-    return (uint32_t)ty * a.W + (uint32_t)tx;
+    const uint32_t tx = nearest_fast((fx + ox) * rx, ax.sw, ax.hw);
+    const uint32_t ty = nearest_fast((fy + oy) * ry, ax.sh, ax.hh);
+    return ty * a.W + tx;
 }
 
-__device__ inline float occlude(const PostArgs& a, float4 s, float4 p, float4 n)
+__device__ inline float occlude_ieee(const PostArgs& a, float4 s, float4 p, float4 n)
 {
     const float dx = s.x - p.x, dy = s.y - p.y, dz = s.z - p.z;
     const float dist = sqrtf(dx * dx + dy * dy + dz * dz);
@@ -122,6 +138,37 @@ __device__ inline float occlude(const PostArgs& a, float4 s, float4 p, float4 n)
     const float m = t - a.bias;
     const float c = m > 0.0f ? m : 0.0f;   // max(0.0, NaN) -> 0
     return c * (1.0f / (1.0f + dist * dist * a.scale)) * a.intensity;
+}
+
+// The range of a fragment's arguments to the short forms: min / max of d2 (a zero d2 counted as +inf in the min:
+// sqrt(0) is in range) and of |1 + dist^2 scale|. (NaN arguments need no flag: a NaN anywhere in a tap makes its
+// term NaN on both paths, and the fragment's 8-bit value 0.)
+struct TapRange {
+    float d2_min = __builtin_inff(), d2_max = 0.0f, arg_min = __builtin_inff(), arg_max = 0.0f;
+    __device__ bool in_range() const
+    {
+        return d2_min >= SF_SQRT_MID_LO && d2_max <= 3.402823466e38f && arg_min >= SF_RCP_MID_LO && arg_max <= SF_RCP_MID_HI;
+    }
+};
+
+// occlude_ieee with dist = sqrt(d2), 1 / dist and 1 / (1 + dist^2 scale) by the short correctly rounded forms
+// (sf_fastmath.h): the same bits where their arguments are in range (tracked in `rg`; where one is not -- a tiny,
+// huge or infinite argument, rare -- the caller recomputes the fragment with occlude_ieee)
+__device__ inline float occlude(const PostArgs& a, float4 s, float4 p, float4 n, TapRange& rg)
+{
+    const float dx = s.x - p.x, dy = s.y - p.y, dz = s.z - p.z;
+    const float d2 = dx * dx + dy * dy + dz * dz;
+    const float dist = sqrt_rn_mid(d2);
+    const float id = d2 == 0.0f ? __builtin_inff() : rcp_rn_mid(dist);   // (d2 in range: dist in [2^-48, 2^64])
+    const float arg = 1.0f + dist * dist * a.scale;
+    rg.d2_min = fminf(rg.d2_min, d2 == 0.0f ? __builtin_inff() : d2);
+    rg.d2_max = fmaxf(rg.d2_max, d2);
+    rg.arg_min = fminf(rg.arg_min, __builtin_fabsf(arg));
+    rg.arg_max = fmaxf(rg.arg_max, __builtin_fabsf(arg));
+    const float t = n.x * (dx * id) + n.y * (dy * id) + n.z * (dz * id);
+    const float m = t - a.bias;
+    const float c = m > 0.0f ? m : 0.0f;   // max(0.0, NaN) -> 0
+    return c * rcp_rn_mid(arg) * a.intensity;
 }
 
 // post_ssao.glsl:27-61 at SSAO-target fragment (i, j); returns the 8-bit target value
@@ -141,6 +188,7 @@ __device__ inline uint8_t ssao_at(const PostArgs& a, uint32_t i, uint32_t j)
     const float len = sqrtf(qx * qx + qy * qy);
     const float il = 1.0f / len;
     const float nx = qx * il, ny = qy * il;
+    const TapAxes ax{ a.fw * 256.0f, a.fw * 256.0f - 1.0f, a.fh * 256.0f, a.fh * 256.0f - 1.0f };
     // the 16 taps' texels and samples first (post_ssao.glsl:49-55: per kernel direction k, 0.25 c1, 0.75 c1,
     // 0.5 c2, c2), then the terms summed in the shader's order
     float4 s[16];
@@ -151,14 +199,30 @@ __device__ inline uint8_t ssao_at(const PostArgs& a, uint32_t i, uint32_t j)
         const float f = 2.0f * (nx * kx + ny * ky);                 // reflect(I, N) = I - 2 dot(N, I) N
         const float c1x = (kx - f * nx) * rad, c1y = (ky - f * ny) * rad;
         const float c2x = c1x * 0.707f - c1y * 0.707f, c2y = c1x * 0.707f + c1y * 0.707f;
-        s[4 * k + 0] = ld4(a.pos, tap_texel(a, fx, fy, c1x * 0.25f, c1y * 0.25f, rx, ry));
-        s[4 * k + 1] = ld4(a.pos, tap_texel(a, fx, fy, c1x * 0.75f, c1y * 0.75f, rx, ry));
-        s[4 * k + 2] = ld4(a.pos, tap_texel(a, fx, fy, c2x * 0.5f, c2y * 0.5f, rx, ry));
-        s[4 * k + 3] = ld4(a.pos, tap_texel(a, fx, fy, c2x, c2y, rx, ry));
+        s[4 * k + 0] = ld4(a.pos, tap_texel(a, ax, fx, fy, c1x * 0.25f, c1y * 0.25f, rx, ry));
+        s[4 * k + 1] = ld4(a.pos, tap_texel(a, ax, fx, fy, c1x * 0.75f, c1y * 0.75f, rx, ry));
+        s[4 * k + 2] = ld4(a.pos, tap_texel(a, ax, fx, fy, c2x * 0.5f, c2y * 0.5f, rx, ry));
+        s[4 * k + 3] = ld4(a.pos, tap_texel(a, ax, fx, fy, c2x, c2y, rx, ry));
     }
     float ao = 0.0f;
+    TapRange rg;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) ao += occlude(a, s[q], p, n);
+    for (int q = 0; q < 16; ++q) ao += occlude(a, s[q], p, n, rg);
+    if (!rg.in_range()) {   // (rare) some tap's argument outside the short forms' ranges: the fragment again, IEEE throughout
+        ao = 0.0f;
+#pragma unroll 1
+        for (int q = 0; q < 16; ++q) {
+            const int k = q >> 2, r = q & 3;
+            const float kx = k == 0 ? 1.0f : k == 1 ? -1.0f : 0.0f;
+            const float ky = k == 2 ? 1.0f : k == 3 ? -1.0f : 0.0f;
+            const float f = 2.0f * (nx * kx + ny * ky);
+            const float c1x = (kx - f * nx) * rad, c1y = (ky - f * ny) * rad;
+            const float c2x = c1x * 0.707f - c1y * 0.707f, c2y = c1x * 0.707f + c1y * 0.707f;
+            const float ox = r == 0 ? c1x * 0.25f : r == 1 ? c1x * 0.75f : r == 2 ? c2x * 0.5f : c2x;
+            const float oy = r == 0 ? c1y * 0.25f : r == 1 ? c1y * 0.75f : r == 2 ? c2y * 0.5f : c2y;
+            ao += occlude_ieee(a, ld4(a.pos, tap_texel(a, ax, fx, fy, ox, oy, rx, ry)), p, n);
+        }
+    }
     ao = ao / 16.0f;
     return quant(1.0f - ao);
 }
