@@ -15,3 +15,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/$OUT/frameless -o run --output-format csv -- python3 $R/scripts/prog_bench.py > $R/$OUT/frameless.log 2>&1
 cat $R/$OUT/frameless.log | grep -v amdgpu
 cat $(find $R/$OUT/frameless -name "*kernel_stats.csv")
+# the frame-less draws alone: without the prefetch (SF_PROG_PREFETCH=0) each batch's draw kernels run on the
+# context stream ahead of its trace, not beside the previous batch's trace -- their durations unshared
+SF_PROG_PREFETCH=0 PROG_BATCHES=262144 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $R/$OUT/frameless_alone -o run --output-format csv -- python3 $R/scripts/prog_bench.py > $R/$OUT/frameless_alone.log 2>&1
+cat $(find $R/$OUT/frameless_alone -name "*kernel_stats.csv") | grep -i "mt_\|Name"

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Frame-less (progressive) mode throughput: random 8-ray packets of one reference worker stream
 (mt19937 draws + Sobol pixel choice + packet traversal + last-writer scatter), 1920x1080 K=0.25.
-Prints rays/s for a few batch sizes. Diagnostics, not the bench line."""
+Prints rays/s for a few batch sizes (PROG_BATCHES, comma-separated packet counts). Diagnostics, not the bench line."""
 import os
 import sys
 import time
@@ -16,7 +16,7 @@ with sf.Sphereflake(W, H) as s:
     for variant in ("avx", "sse"):
         s.SetVariant(variant)
         lanes = 8 if variant == "avx" else 4
-        for batch in (1 << 14, 1 << 16, 1 << 18):
+        for batch in [int(b) for b in os.environ.get("PROG_BATCHES", "16384,65536,262144").split(",")]:
             s.Progressive(12345, batch, 0)
             s.Synchronize()
             reps = 5

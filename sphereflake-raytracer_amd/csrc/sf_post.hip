@@ -140,15 +140,14 @@ __device__ inline float occlude_ieee(const PostArgs& a, float4 s, float4 p, floa
     return c * (1.0f / (1.0f + dist * dist * a.scale)) * a.intensity;
 }
 
-// The range of a fragment's arguments to the short forms: min / max of d2 (a zero d2 counted as +inf in the min:
-// sqrt(0) is in range) and of |1 + dist^2 scale|. (NaN arguments need no flag: a NaN anywhere in a tap makes its
-// term NaN on both paths, and the fragment's 8-bit value 0.)
+// The range of a fragment's arguments to the short forms, both kinds against the tighter bounds [2^-96, 2^124]
+// (the fragment falls back more often than it must only for arguments no frame produces): the min of d2 (a zero d2
+// counted as +inf: sqrt(0) is in range) and |1 + dist^2 scale|, and the max of both -- two v_min3/v_max3 per tap.
+// (NaN arguments need no flag: a NaN anywhere in a tap makes its term NaN on both paths, and the fragment's 8-bit
+// value 0.)
 struct TapRange {
-    float d2_min = __builtin_inff(), d2_max = 0.0f, arg_min = __builtin_inff(), arg_max = 0.0f;
-    __device__ bool in_range() const
-    {
-        return d2_min >= SF_SQRT_MID_LO && d2_max <= 3.402823466e38f && arg_min >= SF_RCP_MID_LO && arg_max <= SF_RCP_MID_HI;
-    }
+    float lo = __builtin_inff(), hi = 0.0f;
+    __device__ bool in_range() const { return lo >= SF_SQRT_MID_LO && hi <= SF_RCP_MID_HI; }
 };
 
 // occlude_ieee with dist = sqrt(d2), 1 / dist and 1 / (1 + dist^2 scale) by the short correctly rounded forms
@@ -159,15 +158,12 @@ __device__ inline float occlude(const PostArgs& a, float4 s, float4 p, float4 n,
     const float dx = s.x - p.x, dy = s.y - p.y, dz = s.z - p.z;
     const float d2 = dx * dx + dy * dy + dz * dz;
     const float dist = sqrt_rn_mid(d2);
-    const float id = d2 == 0.0f ? __builtin_inff() : rcp_rn_mid(dist);   // (d2 in range: dist in [2^-48, 2^64])
+    const float id = d2 == 0.0f ? __builtin_inff() : rcp_rn_mid(dist);   // (d2 in range: dist in [2^-48, 2^62])
     const float arg = 1.0f + dist * dist * a.scale;
-    rg.d2_min = fminf(rg.d2_min, d2 == 0.0f ? __builtin_inff() : d2);
-    rg.d2_max = fmaxf(rg.d2_max, d2);
-    rg.arg_min = fminf(rg.arg_min, __builtin_fabsf(arg));
-    rg.arg_max = fmaxf(rg.arg_max, __builtin_fabsf(arg));
+    rg.lo = fminf(fminf(rg.lo, d2 == 0.0f ? __builtin_inff() : d2), __builtin_fabsf(arg));
+    rg.hi = fmaxf(fmaxf(rg.hi, d2), __builtin_fabsf(arg));
     const float t = n.x * (dx * id) + n.y * (dy * id) + n.z * (dz * id);
-    const float m = t - a.bias;
-    const float c = m > 0.0f ? m : 0.0f;   // max(0.0, NaN) -> 0
+    const float c = fmaxf(t - a.bias, 0.0f);   // max(0.0, NaN) -> 0 (a -0 here only adds a zero of either sign)
     return c * rcp_rn_mid(arg) * a.intensity;
 }
 
