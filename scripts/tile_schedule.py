@@ -45,11 +45,14 @@ def main():
               f"iterations with <= 32 active lanes: {ph[14] / it:.3f}; occlusion-checked entries {ph[13] / per:.0f}, "
               f"wholly culled {ph[12] / per:.0f}; waves {ph[15] / per:.0f}")
     elif ph.sum() > 0:
-        names = {1: "push", 6: "expand: node read + build", 2: "expand: child tests", 3: "head->self",
-                 4: "self test", 5: "pop"}
-        tot = ph[1:7].sum()
+        # traverse_ray's stamps: 0 = back at the loop head (a child whose bounding/LOD test no lane passed, an inline
+        # leaf, a culled entry), 2 = a child's bounding + LOD test that some lane passed, 4 = occlusion cull + self
+        # test, 1 = push, 6 = expand (node read + child build + cone cull), 5 = pop
+        names = {0: "loop head (misses, leaves, culls)", 2: "child test (some lane hit)", 4: "occlusion + self test",
+                 1: "push", 6: "expand", 5: "pop", 3: "-"}
+        tot = ph[0:7].sum()
         print("segment shares (stamp build, all reps):",
-              ", ".join(f"{names[k]} {100 * ph[k] / tot:.1f}%" for k in (1, 6, 2, 3, 4, 5)))
+              ", ".join(f"{names[k]} {100 * ph[k] / tot:.1f}%" for k in (0, 2, 4, 1, 6, 5)))
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     np.save(a.out, tr)
     if ut[:, 1].any():   # SF_FLAG_DIAG_UNITS: per work unit

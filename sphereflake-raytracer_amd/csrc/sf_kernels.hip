@@ -315,7 +315,8 @@ __device__ __forceinline__ void wave_atomic_add_u64(uint64_t* p, uint64_t v)
 
 // Diagnostic build only (make PHASES=1): s_memtime stamps at the DFS segment boundaries, summed per
 // segment into 64-bit scalars and added to phase_sums once per wave. Segments: 0->1 push bookkeeping,
-// 1->2 expand (node read, build, child tests), 3->4 self test, 4->5 pop; 0 is taken at the loop head.
+// 1->2 expand (node read, build, child tests), 3->4 self test, 4->5 pop; 0 is taken at the loop head (and sums
+// what ran since the previous stamp: the child tests no lane passed).
 // Never compiled into the product library; read its SHARES, not its run time.
 #ifdef SF_PHASE_STAMPS
 #define SF_STAMP_DECL uint64_t ph_last = __builtin_amdgcn_s_memtime(), ph_sum[7] = {0, 0, 0, 0, 0, 0, 0}
@@ -325,13 +326,13 @@ __device__ __forceinline__ void wave_atomic_add_u64(uint64_t* p, uint64_t v)
         __builtin_amdgcn_sched_barrier(0);                                                     \
         __asm__ volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
         __builtin_amdgcn_sched_barrier(0);                                                     \
-        if ((k) != 0) ph_sum[k] += t_ - ph_last;                                               \
+        ph_sum[k] += t_ - ph_last;                                                             \
         ph_last = t_;                                                                          \
     } while (0)
 #define SF_STAMP_FLUSH(p)                                                                      \
     do {                                                                                       \
         if (p) {                                                                               \
-            for (int k_ = 1; k_ < 7; ++k_) wave_atomic_add_u64((uint64_t*)(p) + k_, ph_sum[k_]);  \
+            for (int k_ = 0; k_ < 7; ++k_) wave_atomic_add_u64((uint64_t*)(p) + k_, ph_sum[k_]);  \
         }                                                                                      \
     } while (0)
 #elif defined(SF_COUNTS)
