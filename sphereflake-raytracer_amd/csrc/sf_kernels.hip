@@ -376,6 +376,27 @@ __device__ __forceinline__ float4 depth_consts(const DeviceConsts* K, uint32_t d
     return reinterpret_cast<const float4*>(K->depth8)[2u * d];   // host pass: never executed
 #endif
 }
+// depth_consts / depth_cull / depth_far of the depth whose byte offset `o` = d << 5 the caller carries
+__device__ __forceinline__ float4 depth_consts_at(const DeviceConsts* K, uint32_t o)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) float4* ConstF4;
+    typedef const __attribute__((address_space(4))) char* ConstC;
+    return *(ConstF4)((ConstC)(const void*)K->depth8 + o);
+#else
+    return reinterpret_cast<const float4*>(K->depth8)[o >> 4];
+#endif
+}
+__device__ __forceinline__ float depth_word_at(const DeviceConsts* K, uint32_t o, uint32_t w)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) float* ConstF;
+    typedef const __attribute__((address_space(4))) char* ConstC;
+    return *(ConstF)((ConstC)(const void*)K->depth8 + o + 4u * w);
+#else
+    return reinterpret_cast<const float*>(K->depth8)[(o >> 2) + w];
+#endif
+}
 // {leaf, 0, 0, 0} of depth d (see DeviceConsts::depth8)
 __device__ __forceinline__ float depth_leaf(const DeviceConsts* K, uint32_t d)
 {
@@ -1193,6 +1214,8 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
     };
 
     uint32_t stk_pc = 0u, stk_ix = 0u;   // VGPR stack, lane k = level k: {untested | leaf << 18}, idxB
+    const float* tcur = L.table(0u);     // uniform: L.table(d), moved at push / pop (not formed per child)
+    uint32_t kofs = 1u << 5;             // uniform: byte offset of depth d + 1's constants, moved likewise
     uint32_t C = 0u, leafN = 0u;         // uniform: the open node's untested children in entry order (child i at bit
                                          // i if it is a front child, else at bit 9 + i); its inline-leaf children
     float actv;                          // per lane: +inf if the lane visits the open node, -1 otherwise
@@ -1220,9 +1243,9 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             C &= C - 1u;
             const uint32_t c = min(p, p - 9u);   // (p < 9: front child p; else child p - 9)
             // the children's depth constants (scalar loads, in flight with the centre's LDS read)
-            const float4 dc = depth_consts(K, d + 1u);
+            const float4 dc = depth_consts_at(K, kofs);
             lds_fence();
-            const float4 pc = *reinterpret_cast<const float4*>(L.table(d) + c * 4u);
+            const float4 pc = *reinterpret_cast<const float4*>(tcur + c * 4u);
             const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
             const float d2 = pc.w - tca * tca;
             // bounding (SIMD_AVX.h:247-258) for the visiting lanes: one v_min3 compare, its VCC the branch
@@ -1244,8 +1267,8 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
                 SF_COUNT(2, 1);
                 continue;
             }
-            const float Tfar = depth_far(K, d + 1u);
-            const float cull_r = depth_cull(K, d + 1u);
+            const float Tfar = depth_word_at(K, kofs, 6u);     // depth_far(K, d + 1)
+            const float cull_r = depth_word_at(K, kofs, 5u);   // depth_cull(K, d + 1)
             const uint64_t exm = child_lod(tca, d2, xs, hb, hbm, dc.x, dc.w, Tfar);
             SF_STAMP(2);
             if (exm == 0ull) continue;
@@ -1291,7 +1314,9 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             d += 1u;
             actv = avx;
             SF_STAMP(1);
-            C = expand(pc, L.table(d - 1u) + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, avx, leafN);
+            C = expand(pc, tcur + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, avx, leafN);
+            tcur += SF_LDS_LEVEL;
+            kofs += 1u << 5;
             if (COMPACT && C != 0u) {
                 // ---- Active-ray compaction of sparse nodes (north star: "wavefront ballot / prefix-sum active-ray
                 // compaction down the recursion"; sf_trace_queue2c, opt-in). Deep in the tree a node is often visited
@@ -1342,6 +1367,8 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         ancm &= wave_ballot(h.depth != (int32_t)d);
         if (d == 0u) break;
         d -= 1u;
+        tcur -= SF_LDS_LEVEL;
+        kofs -= 1u << 5;
         {
             const uint32_t pw = __builtin_amdgcn_readlane(stk_pc, d);
             C = pw & 0x3ffffu;
