@@ -1059,6 +1059,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
     }
     if (!wave_ballot(ex0)) return;
     maxd = 0;
+    float cull_t = depth_consts(K, 1u).w;   // uniform: depth maxd + 1's LOD threshold, reloaded when maxd grows
 
     // ---- the wave's ray cone (as in traverse)
     {
@@ -1216,6 +1217,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
     uint32_t stk_pc = 0u, stk_ix = 0u;   // VGPR stack, lane k = level k: {untested | leaf << 18}, idxB
     const float* tcur = L.table(0u);     // uniform: L.table(d), moved at push / pop (not formed per child)
     uint32_t kofs = 1u << 5;             // uniform: byte offset of depth d + 1's constants, moved likewise
+    float R2c = depth_consts_at(K, kofs).x;   // uniform: depth d + 1's bounding radius^2, reloaded likewise
     uint32_t C = 0u, leafN = 0u;         // uniform: the open node's untested children in entry order (child i at bit
                                          // i if it is a front child, else at bit 9 + i); its inline-leaf children
     float actv;                          // per lane: +inf if the lane visits the open node, -1 otherwise
@@ -1249,7 +1251,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
             const float d2 = pc.w - tca * tca;
             // bounding (SIMD_AVX.h:247-258) for the visiting lanes: one v_min3 compare, its VCC the branch
-            const float xs = dc.x - d2;
+            const float xs = R2c - d2;
             const bool hb = __builtin_fminf(__builtin_fminf(tca, xs), actv) >= 0.0f;
             const uint64_t hbm = wave_ballot(hb);
             SF_COUNT(1, 1);
@@ -1274,7 +1276,10 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             if (exm == 0ull) continue;
             // ---- child c passed bounding + LOD for the lanes of exm: enter it
             SF_COUNT(3, 1);
-            maxd = (int32_t)d + 1 > maxd ? (int32_t)d + 1 : maxd;   // Sphereflake.h:157-160
+            if ((int32_t)d + 1 > maxd) {   // Sphereflake.h:157-160
+                maxd = (int32_t)d + 1;
+                cull_t = depth_consts_at(K, kofs + (1u << 5)).w;
+            }
             // occlusion cull (see traverse): lanes for which no sphere of the child's subtree can be accepted or
             // pass LOD deeper than the depth already reached do not enter
             // The fattened radius rho = R (1 + m) + m |c| (see traverse) without |c|: a lane of exm hit the bounding
@@ -1283,7 +1288,6 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             // m tca = cull_r + m tca per lane, no square root.
             uint64_t amx = exm;
             if (occl_cull) {
-                const float cull_t = depth_consts(K, (uint32_t)maxd + 1u).w;
                 const float v = __builtin_fminf(tca - h.minT, tca - cull_t);
                 const uint64_t cm = wave_ballot(v - SF_OCCL_MARGIN * tca > cull_r);
                 amx = exm & ~cm;
@@ -1317,6 +1321,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             C = expand(pc, tcur + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, avx, leafN);
             tcur += SF_LDS_LEVEL;
             kofs += 1u << 5;
+            R2c = depth_consts_at(K, kofs).x;
             if (COMPACT && C != 0u) {
                 // ---- Active-ray compaction of sparse nodes (north star: "wavefront ballot / prefix-sum active-ray
                 // compaction down the recursion"; sf_trace_queue2c, opt-in). Deep in the tree a node is often visited
@@ -1369,6 +1374,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         d -= 1u;
         tcur -= SF_LDS_LEVEL;
         kofs -= 1u << 5;
+        R2c = depth_consts_at(K, kofs).x;
         {
             const uint32_t pw = __builtin_amdgcn_readlane(stk_pc, d);
             C = pw & 0x3ffffu;
