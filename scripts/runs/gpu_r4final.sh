@@ -14,7 +14,7 @@ bash scripts/multi_rehearsal.sh > $OUT/multi.log 2>&1 || { tail -5 $OUT/multi.lo
 cp gpurun_out/multi/*.json $OUT/ 2>/dev/null
 timeout -k 10 300 python3 -u bench.py --gpus 2 --rehearse --steps 40 --warmup 5 > $OUT/spawn2.json 2> $OUT/spawn2.err || { tail -5 $OUT/spawn2.err; exit 9; }
 SF_FLAGS=0x20 timeout -k 10 120 python3 -u scripts/latency_probe.py > $OUT/latency.txt 2>&1 || { tail -5 $OUT/latency.txt; exit 10; }
-PROBE_STEPS=600 PROBE_N=1,2,4,8 PROBE_SLOTS=3 PROBE_SPLITS=auto timeout -k 10 300 python3 -u scripts/share_probe.py > $OUT/share_probe.txt 2>&1 || { tail -3 $OUT/share_probe.txt; exit 11; }
+PROBE_STEPS=600 PROBE_N=1,2,4,8 PROBE_SLOTS=3,4 PROBE_SPLITS=auto timeout -k 10 300 python3 -u scripts/share_probe.py > $OUT/share_probe.txt 2>&1 || { tail -3 $OUT/share_probe.txt; exit 11; }
 grep slots $OUT/share_probe.txt
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/rows8 -o run --output-format csv -- python3 $R/bench.py --mode rows --gpus 8 --steps 60 --warmup 5 --no-cpu-baseline > $OUT/rows8.log 2>&1 || { tail -5 $OUT/rows8.log; exit 12; }
