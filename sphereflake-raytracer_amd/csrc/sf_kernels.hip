@@ -1148,7 +1148,9 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
     // left to test; leafm = its inline-leaf children | its front children << 9. At the deepest provisioned level
     // (no table for the children's children) the children are tested here, from the centre lanes: any that some
     // lane expands flags the tile for the deeper re-trace, and none is entered.
-    auto expand = [&](const float4 pc, const float* col, uint32_t cs, uint32_t d, float actv, uint32_t& leafm) -> uint32_t {
+    // (tb: table(d), ko: d + 1's constants offset -- the caller's carried values, not formed here again)
+    auto expand = [&](const float4 pc, const float* col, uint32_t cs, uint32_t d, float actv, uint32_t& leafm,
+                      float* tb, uint32_t ko) -> uint32_t {
         d = __builtin_amdgcn_readfirstlane(d);
         SF_COUNT(0, 1);
         SF_COUNT(7, __builtin_popcountll(wave_ballot(actv >= 0.0f)));   // (COUNTS builds: lanes visiting the node)
@@ -1158,9 +1160,9 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float3 p2 = *reinterpret_cast<const float3*>(col + 2u * cs);
         const float4 cn = *reinterpret_cast<const float4*>(L.cone());
         const float sinT = L.cone()[4];
-        const float4 dtn = depth_consts(K, d);
-        const float4 dtc = depth_consts(K, d + 1u);
-        const float leaf1 = depth_leaf(K, d + 1u);
+        const float4 dtn = depth_consts_at(K, ko - (1u << 5));
+        const float4 dtc = depth_consts_at(K, ko);
+        const float leaf1 = depth_word_at(K, ko, 4u);   // depth_leaf(K, d + 1)
         const float leafc = lod_cull ? leaf1 : __builtin_inff();
         const float sm = bc == 3u ? dtn.z : 1.0f;
         const float b0 = b[0] * sm, b1 = b[1] * sm, b2 = b[2] * sm;
@@ -1169,7 +1171,6 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float z = ((p0.z * b0 + p1.z * b1) + p2.z * b2) + pc.z * b[3];
         const float w = (x * x + y * y) + z * z;
         if (d + 1u < levels) {
-            float* const tb = L.table(d);
             *reinterpret_cast<float3*>(tb + slot) = make_float3(x, y, z);
             *(bc == 3u ? tb + slot + 3u : L.cone() + 5u) = w;
         }
@@ -1193,7 +1194,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             front = (uint32_t)(wave_ballot(ca < kp) >> 31) & 0x1ffu;
         }
         if (d + 1u >= levels) {
-            const float T = dtc.w, Tfar = depth_far(K, d + 1u);
+            const float T = dtc.w, Tfar = depth_word_at(K, ko, 6u);   // depth_far(K, d + 1)
             while (M) {
                 const uint32_t i = __builtin_ctz(M);
                 M &= ~(1u << i);
@@ -1215,7 +1216,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
     };
 
     uint32_t stk_pc = 0u, stk_ix = 0u;   // VGPR stack, lane k = level k: {untested | leaf << 18}, idxB
-    const float* tcur = L.table(0u);     // uniform: L.table(d), moved at push / pop (not formed per child)
+    float* tcur = L.table(0u);           // uniform: L.table(d), moved at push / pop (not formed per child)
     uint32_t kofs = 1u << 5;             // uniform: byte offset of depth d + 1's constants, moved likewise
     float R2c = depth_consts_at(K, kofs).x;   // uniform: depth d + 1's bounding radius^2, reloaded likewise
     uint32_t C = 0u, leafN = 0u;         // uniform: the open node's untested children in entry order (child i at bit
@@ -1231,7 +1232,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float d2 = pc.w - tca * tca;
         self_test(pc, tca, d2, 0u, actv, 0u, depth_consts(K, 0u).y);
         if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u)))))
-            C = expand(pc, L.root() + 4u, 4u, 0u, actv, leafN);
+            C = expand(pc, L.root() + 4u, 4u, 0u, actv, leafN, tcur, kofs);
         else SF_COUNT(4, 1);
     }
 
@@ -1318,9 +1319,10 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             d += 1u;
             actv = avx;
             SF_STAMP(1);
-            C = expand(pc, tcur + SF_LDS_PLANE + 3u * c, SF_LDS_COLS, d, avx, leafN);
+            const float* const col = tcur + SF_LDS_PLANE + 3u * c;   // the entered child's axis columns
             tcur += SF_LDS_LEVEL;
             kofs += 1u << 5;
+            C = expand(pc, col, SF_LDS_COLS, d, avx, leafN, tcur, kofs);
             R2c = depth_consts_at(K, kofs).x;
             if (COMPACT && C != 0u) {
                 // ---- Active-ray compaction of sparse nodes (north star: "wavefront ballot / prefix-sum active-ray
