@@ -34,8 +34,8 @@
 #define SF_LDS_CONE 8                     // the wave's ray cone {ax, ay, az, cosT, sinT, -, -, -}
 // plane 0: {centre, cc} float4 of each of the 9 children (36 floats), 2 floats of skew, then planes 1..3:
 // column j (xyz, float3) of each child. The skew puts the column stores of the 27 column builders (lanes
-// 0..26, dwords 38 + 3l..) on other banks than child 0's centre store in the same 32-lane LDS group (lane 31,
-// dwords 0..3): the table build is free of bank conflicts (sf_kernels.hip, the builder lanes)
+// 0..26, dwords 38 + 3l..) on other banks than child 0's centre store repeated in the same 32-lane LDS group
+// (lanes 27..31, dwords 0..3): the table build is free of bank conflicts (sf_kernels.hip, the builder lanes)
 #define SF_LDS_PLANE 38
 #define SF_LDS_COLS 27                    // planes 1..3: column j (xyz, float3) of each of the 9 children
 #define SF_LDS_TABLE (SF_LDS_PLANE + 3 * SF_LDS_COLS)   // the 9 child transforms of the node open at a level

@@ -460,12 +460,12 @@ __device__ __forceinline__ void stage_root(float* __restrict__ Lbase, const floa
 // PW: packet width of the semantics (0 per ray, 8 (AVX) or 4 (SSE) frame-less packets); PIPE: the latency
 // variant of the per-ray child loop (small frames, whose heaviest tiles' serial DFS is the frame)
 // This lane's column of the cooperative child build (see traverse): unit child frame bi = lane % 9 (lanes
-// 0..26; centre lanes 31 + i: child i), column bc. Loaded once per wave, before any tile loop: a global load
+// 0..26; centre lanes 32 + i: child i), column bc. Loaded once per wave, before any tile loop: a global load
 // in every traversal would wait (vmcnt, in order on this ISA) for the previous tile's G-buffer stores.
 __device__ __forceinline__ float4 build_column(const DeviceConsts* __restrict__ K)
 {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 0u : 1u + ((lane - 32u) & 7u);
+    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 0u : (lane - 32u) % 9u;
     const uint32_t bc = lane < 27u ? lane / 9u : 3u;
     const float4 r = make_float4(K->child[bi][4u * bc + 0u], K->child[bi][4u * bc + 1u], K->child[bi][4u * bc + 2u],
                                  K->child[bi][4u * bc + 3u]);
@@ -539,15 +539,15 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
 
     // This lane's column of the cooperative child build. The 27 axis columns (column c = lane / 9 of child
     // i = lane % 9) are built by lanes 0..26 of the first 32-lane LDS bank group, the 9 centres (column 3)
-    // by lanes 31 + i: child 0's by lane 31 of the first group, children 1..8 by lanes 32..39 of the second.
-    // With the column planes skewed by 2 floats (SF_LDS_PLANE) no store of the table build has two distinct
-    // addresses on one bank in a group; every other lane repeats a builder of its own group (27..30: child 0's
-    // centre; 40..63: children 1..8 again) -- the same address and value, merged by the LDS, not a conflict.
-    // (Round 2's layout -- centres on lanes 27..35, lanes 36..63 mirroring 0..27 -- put 4.9 M extra cycles per
-    // 1080p frame into bank conflicts, 40 % of the LDS instruction cycles.) No divergent region; the build's
-    // VALU cost is per wave either way. Lanes 31..39 hold the 9 child centres (read back by v_readlane) and
-    // one ballot yields a per-child mask (bits 31..39).
-    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 0u : 1u + ((lane - 32u) & 7u);
+    // by lanes 32 + i of the second group. With the column planes skewed by 2 floats (SF_LDS_PLANE) no store of
+    // the table build has two distinct addresses on one bank in a group; every other lane repeats a builder
+    // (27..31: child 0's centre; 41..63: children (lane - 32) % 9 again) -- the same address and value, merged by
+    // the LDS, not a conflict. (Round 2's layout -- centres on lanes 27..35, lanes 36..63 mirroring 0..27 -- put
+    // 4.9 M extra cycles per 1080p frame into bank conflicts, 40 % of the LDS instruction cycles.) No divergent
+    // region; the build's VALU cost is per wave either way. Lanes 32..40 hold the 9 child centres (read back by
+    // v_readlane), and a ballot's per-child mask is bits 0..8 of its high word: one scalar AND (round 3 had the
+    // centres on lanes 31..39, whose mask straddled the two words: a 64-bit shift and an AND per ballot).
+    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 0u : (lane - 32u) % 9u;
     const uint32_t bc = lane < 27u ? lane / 9u : 3u;
     // The leaf-threshold skip bounds t from below for every ray. In packet semantics a lane with tca < 0
     // can also pass LOD through another lane's bounding hit (negative t, SIMD_AVX.h:254), which that
@@ -658,7 +658,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         const float R2b = dtc.x;
         const float T = dtc.w;
         const float Tfar = depth_far(K, d + 1u);
-        // Cone cull of child bi (centre c in lanes 31..39): no ray of the wave's cone can hit its bounding
+        // Cone cull of child bi (centre c in lanes 32..40): no ray of the wave's cone can hit its bounding
         // sphere. With ca = c.a, q = c - ca a, every lane's angle phi to c is >= alpha - theta, so its
         // line passes at distance |c| sin(phi) >= |q| cosT - ca sinT from c. A float hit
         // (tca >= 0, cc - tca^2 <= R^2, SIMD_AVX.h:247-258) needs |c| sin(phi) <= sqrt(R^2 + dl),
@@ -690,7 +690,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         // a > b exactly when fl(a - b) > 0; every operand is finite): the kept children straight from a ballot
         const float mk = __builtin_fminf(__builtin_fminf(ca, w - 2.0f * (R2b + dl)), lhs - rhs);
 #endif
-        uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 31) & 0x1ffu;
+        uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 32) & 0x1ffu;
         M = __builtin_amdgcn_readfirstlane(M);
         SF_STAMP(6);
         uint32_t e = 0, pm = 0;
@@ -823,8 +823,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                         const float4 c4 = *reinterpret_cast<const float4*>(ctab + i * 4u);
                         cx = c4.x, cy = c4.y, cz = c4.z, cc = c4.w;
                     } else {
-                        cx = readlane_f(x, 31u + i), cy = readlane_f(y, 31u + i);
-                        cz = readlane_f(z, 31u + i), cc = readlane_f(w, 31u + i);
+                        cx = readlane_f(x, 32u + i), cy = readlane_f(y, 32u + i);
+                        cz = readlane_f(z, 32u + i), cc = readlane_f(w, 32u + i);
                     }
                     test_child(i, cx, cy, cz, cc);
                 }
@@ -851,8 +851,8 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
                     const float4 c4 = *reinterpret_cast<const float4*>(ctab + i * 4u);
                     cx = c4.x, cy = c4.y, cz = c4.z, cc = c4.w;
                 } else {
-                    cx = readlane_f(x, 31u + i), cy = readlane_f(y, 31u + i);
-                    cz = readlane_f(z, 31u + i), cc = readlane_f(w, 31u + i);
+                    cx = readlane_f(x, 32u + i), cy = readlane_f(y, 32u + i);
+                    cz = readlane_f(z, 32u + i), cc = readlane_f(w, 32u + i);
                 }
                 const float tca = (cx * dx + cy * dy) + cz * dz;
                 const float d2 = cc - tca * tca;
@@ -883,14 +883,14 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         }
         pend = pm;
         // children none of whose own children can pass LOD for any ray (sfhost::leaf_threshold of their depth;
-        // |c|^2 of child i is w on lane 31 + i): entered as inline leaves
-        leafm = (uint32_t)(wave_ballot(w > leafc) >> 31) & 0x1ffu;
+        // |c|^2 of child i is w on lane 32 + i): entered as inline leaves
+        leafm = (uint32_t)(wave_ballot(w > leafc) >> 32) & 0x1ffu;
         // front-first order (per-ray, occlusion cull on): bits 9..17 = the children whose centre lies nearer
         // than this node's along the cone axis; they are entered first, so their hits cull the far ones more
         if constexpr (!PACKET) {
             if (front_first) {
                 const float kp = (pc.x * ax + pc.y * ay) + pc.z * az;
-                leafm |= ((uint32_t)(wave_ballot(ca < kp) >> 31) & 0x1ffu) << 9;
+                leafm |= ((uint32_t)(wave_ballot(ca < kp) >> 32) & 0x1ffu) << 9;
             }
         }
         return e;
@@ -1080,7 +1080,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
     }
 
     // this lane's column of the cooperative child build (see traverse)
-    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 0u : 1u + ((lane - 32u) & 7u);
+    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 0u : (lane - 32u) % 9u;
     const uint32_t bc = lane < 27u ? lane / 9u : 3u;
     const float b[4] = { bcol.x, bcol.y, bcol.z, bcol.w };
     const uint32_t slot = bc == 3u ? bi * 4u : SF_LDS_PLANE + bc * SF_LDS_COLS + bi * 3u;
@@ -1175,7 +1175,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             *(bc == 3u ? tb + slot + 3u : L.cone() + 5u) = w;
         }
         const float R2b = dtc.x;
-        // cone cull of child bi (centre lanes 31..39), in squares (see traverse)
+        // cone cull of child bi (centre lanes 32..40), in squares (see traverse)
         const float ax = cn.x, ay = cn.y, az = cn.z, cosT = cn.w;
         const float dl = w * 0x1p-18f;
         const float ca = (x * ax + y * ay) + z * az;
@@ -1183,23 +1183,23 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float X = sq * cosT - ca * sinT;
         const float Y = X * X - (R2b + w * (0x1p-18f + 0x1p-19f));
         const float mk = __builtin_fminf(__builtin_fminf(ca, w - 2.0f * (R2b + dl)), __builtin_fminf(X, Y));
-        uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 31) & 0x1ffu;
+        uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 32) & 0x1ffu;
         M = __builtin_amdgcn_readfirstlane(M);
-        leafm = (uint32_t)(wave_ballot(w > leafc) >> 31) & 0x1ffu;
+        leafm = (uint32_t)(wave_ballot(w > leafc) >> 32) & 0x1ffu;
         // entry order as bit order: the front children (nearer than this node's centre along the cone axis) at
         // bits 0..8, the others at 9..17 -- one find-first-set per child picks the next
         uint32_t front = 0x1ffu;
         if (front_first) {
             const float kp = (pc.x * ax + pc.y * ay) + pc.z * az;
-            front = (uint32_t)(wave_ballot(ca < kp) >> 31) & 0x1ffu;
+            front = (uint32_t)(wave_ballot(ca < kp) >> 32) & 0x1ffu;
         }
         if (d + 1u >= levels) {
             const float T = dtc.w, Tfar = depth_word_at(K, ko, 6u);   // depth_far(K, d + 1)
             while (M) {
                 const uint32_t i = __builtin_ctz(M);
                 M &= ~(1u << i);
-                const float cx = readlane_f(x, 31u + i), cy = readlane_f(y, 31u + i);
-                const float cz = readlane_f(z, 31u + i), cc = readlane_f(w, 31u + i);
+                const float cx = readlane_f(x, 32u + i), cy = readlane_f(y, 32u + i);
+                const float cz = readlane_f(z, 32u + i), cc = readlane_f(w, 32u + i);
                 const float tca = (cx * dx + cy * dy) + cz * dz;
                 const float d2 = cc - tca * tca;
                 const float xs = R2b - d2;
