@@ -1148,6 +1148,8 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
     // left to test; leafm = its inline-leaf children | its front children << 9. At the deepest provisioned level
     // (no table for the children's children) the children are tested here, from the centre lanes: any that some
     // lane expands flags the tile for the deeper re-trace, and none is entered.
+    const uint32_t lv32 = __builtin_amdgcn_readfirstlane(levels << 5);   // levels, in depth-constant offset units
+    const uint32_t index_order = front_first ? 0u : 0x1ffu;
     // (tb: table(d), ko: d + 1's constants offset -- the caller's carried values, not formed here again)
     auto expand = [&](const float4 pc, const float* col, uint32_t cs, uint32_t d, float actv, uint32_t& leafm,
                       float* tb, uint32_t ko) -> uint32_t {
@@ -1170,7 +1172,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float y = ((p0.y * b0 + p1.y * b1) + p2.y * b2) + pc.y * b[3];
         const float z = ((p0.z * b0 + p1.z * b1) + p2.z * b2) + pc.z * b[3];
         const float w = (x * x + y * y) + z * z;
-        if (d + 1u < levels) {
+        if (ko < lv32) {   // (d + 1 < levels)
             *reinterpret_cast<float3*>(tb + slot) = make_float3(x, y, z);
             *(bc == 3u ? tb + slot + 3u : L.cone() + 5u) = w;
         }
@@ -1188,12 +1190,10 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         leafm = (uint32_t)(wave_ballot(w > leafc) >> 32) & 0x1ffu;
         // entry order as bit order: the front children (nearer than this node's centre along the cone axis) at
         // bits 0..8, the others at 9..17 -- one find-first-set per child picks the next
-        uint32_t front = 0x1ffu;
-        if (front_first) {
-            const float kp = (pc.x * ax + pc.y * ay) + pc.z * az;
-            front = (uint32_t)(wave_ballot(ca < kp) >> 32) & 0x1ffu;
-        }
-        if (d + 1u >= levels) {
+        // (index order, front_first false: every child "front" -- an OR with a per-traversal mask, not a branch)
+        const float kp = (pc.x * ax + pc.y * ay) + pc.z * az;
+        const uint32_t front = ((uint32_t)(wave_ballot(ca < kp) >> 32) & 0x1ffu) | index_order;
+        if (ko >= lv32) {   // (d + 1 >= levels)
             const float T = dtc.w, Tfar = depth_word_at(K, ko, 6u);   // depth_far(K, d + 1)
             while (M) {
                 const uint32_t i = __builtin_ctz(M);
