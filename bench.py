@@ -115,6 +115,7 @@ def frames_in_flight(requested, cus, width, height, band_rows, n):
 
 GATHER_TIMEOUT_S = 180.0             # the RCCL-gathered leg (multi-GPU) runs last, under a watchdog
 
+ENQ_TRACE = os.environ.get("SF_BENCH_ENQ_TRACE") == "1"   # diagnostics: per-frame enqueue times in the line
 LONG_SETTLE_MS = 30.0               # before the steady-period loop (the GPU was idle only for the timed loop's readouts)
 SETTLE_MS = 150.0                    # the shader clock ramps from ~2075 to ~2370 MHz over the first ~60 ms of load
                                      # (profiles/r3/ramp.txt): warm-up lasts at least this long. (Under sustained load
@@ -670,11 +671,14 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
         # (no Python garbage collection inside the timed region: a collection pause on the host between two
         # enqueues starves a pipeline only ~3 frames deep -- one 20-step loop in six measured +0.15 ms)
         gc.disable()
+        enq = [] if ENQ_TRACE else None
         try:
             t0 = time.perf_counter()
             for i in range(n):
                 d.SetView(*view_of(i))
                 render()
+                if enq is not None:
+                    enq.append(time.perf_counter())
             d.Synchronize()
             torch.cuda.synchronize(dev)
             ctl.barrier()
@@ -682,6 +686,9 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
             dt = time.perf_counter() - t0
         finally:
             gc.enable()
+        if enq is not None:   # diagnostics (SF_BENCH_ENQ_TRACE=1): host time at each frame's enqueue, and the end
+            out.setdefault("enqueue_trace_us", []).append(
+                [round((t - t0) * 1e6, 1) for t in enq] + [round(dt * 1e6, 1)])
         return ctl.max(dt)
 
     out["t_step"] = timed(steps, lambda i: views[warmup + i]) / steps
@@ -1009,6 +1016,8 @@ def main():
                 "(its time - the timed loop's) / the extra frames; fill_ms = the timed loop's time beyond steps x "
                 "steady_frame_ms (its first frames run with no frame in flight), so ms_per_step = steady_frame_ms + "
                 "fill_ms / steps"))
+        if "enqueue_trace_us" in r:
+            out["enqueue_trace_us"] = r["enqueue_trace_us"]
         if check:
             out["check"] = {"bit_exact": checks_ok, **checks,
                             "note": "outside the timed region; this rank's rows (rank 0's bands on N > 1): the last "

@@ -773,10 +773,14 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             // on its heaviest tiles' serial traversal: one frame alone 0.175 -> 0.151-0.164 ms at 1080p, and the
             // driver's 20-step loop 0.0871 -> 0.0846 ms per frame (mean of 4 interleaved runs a side,
             // profiles/r4/order_ab.txt). Frames between half and twice the grid (1280x720) measured slower with it
-            // (0.0358 -> 0.0388 ms) and keep the row-major order.
+            // (0.0358 -> 0.0388 ms) and keep the row-major order. End of round 4, with the faster kernel: large
+            // frames take the order WITHOUT splits -- the split parts re-traverse their tile's shared upper levels,
+            // and with frames in flight only the loop's last frame gains from them: the 20-step loop 0.0759-0.0782
+            // -> 0.0748-0.0766 ms, one frame alone 0.133-0.136 -> 0.129-0.139, steady period unchanged (5
+            // interleaved runs a side, profiles/r4/split0_ab.txt).
             const bool large = !small && band_count == 1u;
             const bool use_order = c->order_mode > 0 || (c->order_mode < 0 && (tiny || large));
-            const uint32_t split_buckets = (large && !c->split_env) ? SF_SPLIT_MODEL : c->split_buckets;
+            const uint32_t split_buckets = (large && !c->split_env) ? 0u : c->split_buckets;
             // work units: tiles, or up to `split_parts` per tile when the schedule may split tiles
             const uint32_t units_max = (use_order && split_buckets != 0u) ? c->split_parts * ntiles : ntiles;
             const uint32_t need = (units_max + wpb - 1) / wpb;
