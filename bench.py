@@ -15,12 +15,13 @@ costs); `fixed_camera` repeats the timed loop on one unchanging view; `frame_lat
 rendered and waited for alone.
 
 Default mode `dist` (sf_dist_*, csrc/sf_dist.hip): `--slots` frames in flight (frame i on slot i % slots, each
-slot its own context, stream and G-buffer), so a frame's persistent trace grid fills the wave slots the previous
-frame's heaviest tiles leave idle -- the reference's workers likewise trace continuously. Multi-GPU (`--gpus N`,
+slot its own context, stream and G-buffer; default 3, or 4 for a rank's share that leaves most of the persistent
+grid idle -- frames_in_flight), so a frame's persistent trace grid fills the wave slots the previous frame's
+heaviest tiles leave idle -- the reference's workers likewise trace continuously. Multi-GPU (`--gpus N`,
 launched by torch.distributed.run, one process per GPU): ONE frame per step split over the N GPUs in interleaved
 8-row bands, every rank tracing its bands into its own HBM -- the frame's G-buffer distributed over the GPUs,
 `scaling: "strong"` (the frame is fixed, N GPUs share it): `value`. `gathered_on_rank0` times the same frames
-assembled on rank 0 (ranks k > 0 send packed slabs, 16 B/pixel, over RCCL/xGMI; rank 0 unpacks them beside its
+assembled on rank 0 (ranks k > 0 send packed slabs, 4 or 16 B/pixel, over RCCL/xGMI; rank 0 unpacks them beside its
 own bands): what a consumer on rank 0 sees, a transfer bound by the links into rank 0, reported beside `value`
 as the D2H copy is. torch.distributed (gloo) is only the control plane: the RCCL ids, barriers and the max over
 ranks of the timed region. `independent_frames` adds the weak-scaling figure (every rank its own frames).
