@@ -680,13 +680,14 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
                 render()
                 if enq is not None:
                     enq.append(time.perf_counter())
-            d.Synchronize()
+            # the device synchronize waits for every stream of the process, the slots' own included; the dist's
+            # Synchronize (its stats copy and error check) follows the timed region
             torch.cuda.synchronize(dev)
             ctl.barrier()
-            torch.cuda.synchronize(dev)
             dt = time.perf_counter() - t0
         finally:
             gc.enable()
+        d.Synchronize()
         if enq is not None:   # diagnostics (SF_BENCH_ENQ_TRACE=1): host time at each frame's enqueue, and the end
             out.setdefault("enqueue_trace_us", []).append(
                 [round((t - t0) * 1e6, 1) for t in enq] + [round(dt * 1e6, 1)])
