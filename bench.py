@@ -55,7 +55,7 @@ from sphereflake_amd import shard  # noqa: E402
 W, H, K = 1920, 1080, 0.25          # BASELINE configs[2]
 BYTES_PER_RAY = 32                  # two float4 G-buffer stores
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
-TRACE_KERNEL = "sf_trace_queue2"    # the dominant kernel (persistent wave-coherent trace, 2 waves/workgroup)
+TRACE_KERNEL = "sf_trace_queue1"    # the dominant kernel (persistent wave-coherent trace, 1 wave per workgroup)
 
 
 def parse():

@@ -23,6 +23,6 @@ if [ "${PMC:-0}" = "1" ]; then
     i=$((i+1))
     SF_LIB_PARTIAL=1 SF_FLAGS=$F SF_LIB=$R/$L timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $OUT/pmc$i -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras $ARGS > $OUT/pmc$i.log 2>&1
     echo "== $LF"
-    python3 $R/scripts/pmc_summary.py $OUT/pmc$i | grep -A12 "sf_trace_queue2 " || true
+    python3 $R/scripts/pmc_summary.py $OUT/pmc$i | grep -A12 "sf_trace_queue[12] " || true
   done
 fi

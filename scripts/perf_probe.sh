@@ -12,4 +12,4 @@ for cfg in "" "--width 640 --height 360 --K 1.0"; do
 done
 cd /tmp && export TMPDIR=/tmp
 env "$@" timeout -k 10 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS SQ_INSTS_SMEM -d $OUT/pmc -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extras > $OUT/pmc.log 2>&1
-python3 $R/scripts/pmc_summary.py $OUT/pmc | grep -A10 "sf_trace_queue2"
+python3 $R/scripts/pmc_summary.py $OUT/pmc | grep -A10 "sf_trace_queue[12] "

@@ -18,5 +18,5 @@ for line in open(path):
                   r"ScratchSize \[bytes/lane\]): (\d+)", line)
     if m and cur:
         out[cur][m.group(1).split(" [")[0]] = int(m.group(2))
-for k in sys.argv[1:] or ["sf_trace_queue2", "sf_trace_queue2p", "sf_progressive_trace"]:
+for k in sys.argv[1:] or ["sf_trace_queue1", "sf_trace_queue2", "sf_trace_queue2p", "sf_progressive_trace"]:
     print(k, out.get(k))

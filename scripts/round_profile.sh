@@ -31,7 +31,7 @@ grep '^{' $OUT/stats.log | tail -1 > $OUT/bench_under_rocprof.json
 # timed loop of the default bench: 1 code-object warm-up + 1 first render + 30 warmup + the settle frames,
 # then 200 timed dispatches
 SKIP=$(python3 -c "import json; print(32 + json.load(open('$OUT/bench_under_rocprof.json'))['settle']['frames'])")
-python3 $R/scripts/trace_avg.py $(find $OUT/stats -name "*kernel_trace.csv") sf_trace_queue2 200 $SKIP | tee $OUT/trace_avg.txt
+python3 $R/scripts/trace_avg.py $(find $OUT/stats -name "*kernel_trace.csv") sf_trace_queue1 200 $SKIP | tee $OUT/trace_avg.txt
 cd $R
 if [ $# -gt 0 ]; then REPS=0 PMC=1 scripts/lib_ab.sh $TAG/lds "" sphereflake-raytracer_amd/build/libsphereflake_hip.so "$@"; fi
 exit $rc

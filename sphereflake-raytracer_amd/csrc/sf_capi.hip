@@ -517,6 +517,8 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if (const char* ev = std::getenv("SF_TRACE_WAVES")) {
         const int w = std::atoi(ev);
         c->waves_per_block = (w == 1 || w == 2 || w == 4) ? (uint32_t)w : SF_TRACE_WAVES;
+    } else if (c->compact || c->pipe == 1) {
+        c->waves_per_block = 2;   // the compaction and pipelined (latency) variants are 2-wave kernels
     }
     if (const char* ev = std::getenv("SF_LEVELS")) {
         const int l = std::atoi(ev);

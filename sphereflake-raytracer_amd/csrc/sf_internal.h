@@ -24,7 +24,9 @@
 #define SF_WAVES_PER_EU 8      // occupancy target of the persistent trace kernels (waves per SIMD)
 #endif
 #ifndef SF_TRACE_WAVES
-#define SF_TRACE_WAVES 2       // independent waves per workgroup of the wave kernels
+#define SF_TRACE_WAVES 1       // independent waves per workgroup of the wave kernels (round 4: 1 -- 1080p 0.0718-0.0723
+                               // -> 0.0697-0.0707 ms against 2, profiles/r4/waves_ab.txt; the pipelined and compaction
+                               // variants exist at 2 and take 2)
 #endif
 // Wave-coherent traversal LDS image, per wave (units: floats):
 //   [root: 16][cone: 8][(levels - 1) x (table 144 | E 32)]
