@@ -541,8 +541,11 @@ def check_tile_order(W, H, split, parts, units, cost):
         assert nsplit == 0   # auto: more tiles than resident waves, nothing split
     elif split is None and W * H <= 100 * 60:
         assert nsplit == np.count_nonzero(cost_bucket(cost) >= 1)   # few tiles: every splittable one
-    else:
+    elif W * H > 100 * 60:
         assert nsplit > 0
+    # (a 100x60 frame's 104 tiles with an explicit bucket count: its top bucket may hold more than the eighth of
+    # the tiles that may split -- with the one-wave kernel its costs are flat enough -- and then none is split;
+    # the schedule still equals the restatement, asserted above)
 
 
 @pytest.mark.parametrize("parts", [2, 4])
