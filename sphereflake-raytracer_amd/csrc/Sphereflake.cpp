@@ -1,6 +1,7 @@
 // Sphereflake.cpp -- the reference-compatible C++ class over the C ABI (see Sphereflake.hpp).
 // Reference surface: /root/reference/sphereflake/Sphereflake.h:13-58, Sphereflake.cpp:43-84.
 #include "Sphereflake.hpp"
+#include "SphereflakeSSAO.hpp"
 
 #include <chrono>
 #include <cstdio>
@@ -188,6 +189,8 @@ void Sphereflake::ResetClosestSphereDistance()
     Check(sf_reset_closest(m_Ctx));
 }
 
+namespace Headless {
+
 SSAO::SSAO(Sphereflake& flake, int downScale) : m_Flake(flake)
 {
     if (downScale < 1) throw std::runtime_error("sphereflake: SSAO downScale must be >= 1");
@@ -221,5 +224,7 @@ const std::vector<uint8_t>& SSAO::GetImage() const
     Check(sf_download_image(m_Flake.Context(), m_Image.data()));
     return m_Image;
 }
+
+}  // namespace Headless
 
 }  // namespace SphereflakeRaytracer

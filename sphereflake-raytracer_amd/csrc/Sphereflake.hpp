@@ -142,28 +142,4 @@ private:
     uint32_t m_Seed = 0;
 };
 
-// Headless counterpart of the reference's SSAO class (SSAO.h:9-50, SSAO.cpp:49-175) plus the final
-// composite pass of main.cpp:321-330, on the device G-buffer of a Sphereflake (sf_post_process).
-// The GL texture handle of GetSSAOTexture() becomes the composited RGBA8 image, W*H*4 bytes,
-// row j = G-buffer row j.
-class SSAO {
-public:
-    SSAO(Sphereflake& flake, int downScale = 1);
-
-    // SSAO.h:15-18. Until called, the radius is 8 x the closest-hit stat read on the device.
-    void SetSampleRadiusMultiplier(float m) { m_Params.sample_radius = 8.0f * m; }
-    // post_final.glsl cameraPosition (main.cpp:325); defaults to the SetView origin at Render time.
-    void SetCameraPosition(const sf_vec3& p);
-
-    void Render();                                  // SSAO, blur x, blur y, final (asynchronous)
-    const std::vector<uint8_t>& GetImage() const;   // D2H of the last Render's image
-    void SaveImage(const std::string& path) const;  // the last Render's image as a PPM
-
-private:
-    Sphereflake& m_Flake;
-    sf_post_params m_Params;
-    bool m_CameraSet = false;
-    mutable std::vector<uint8_t> m_Image;
-};
-
 }  // namespace SphereflakeRaytracer

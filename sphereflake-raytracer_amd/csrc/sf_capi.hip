@@ -1036,6 +1036,18 @@ int sfi_unpack_slabs(sf_ctx* c, const void* stage, uint32_t bytes_per_pixel, uin
     return SF_OK;
 }
 
+// Order the context's own stream after everything the context enqueued before, on whatever stream (ctx_join).
+// sf_dist / sf_group call it before they record a frame's start event on the context stream: their receive /
+// unpack stream waits only for that event, so the event must already follow earlier consumers queued on a
+// caller's stream (sf_download_async, sf_post_process on stream X), or the unpack could overwrite rows X is
+// still reading.
+int sfi_join(sf_ctx* c)
+{
+    if (!c) return SF_EINVAL;
+    DevGuard g(c->device);
+    return ctx_join(c, c->stream);
+}
+
 int sf_unpack_slabs(sf_ctx* c, const void* stage, uint32_t bytes_per_pixel, uint32_t stage_rows, uint32_t band_rows,
                     uint32_t band_count, uint32_t first_member, uint32_t members, void* stream)
 {

@@ -35,6 +35,8 @@
 // (sf_capi.hip) the unpack without the context's stream join: the caller orders `s` itself
 extern "C" int sfi_unpack_slabs(sf_ctx* c, const void* stage, uint32_t bytes_per_pixel, uint32_t stage_rows, uint32_t band_rows,
                      uint32_t band_count, uint32_t first_member, uint32_t members, hipStream_t s, bool join);
+// (sf_capi.hip) join the context stream after the context's previous calls on any stream (ctx_join)
+extern "C" int sfi_join(sf_ctx* c);
 
 struct sf_dist {
     int device = 0, rank = 0, nranks = 1;
@@ -224,7 +226,12 @@ extern "C" int sf_dist_render(sf_dist* d)
         const bool peers = n > 1 && d->stage_rows;
         // the frame starts here on the context stream: earlier work there (the consumers of this slot's previous
         // frame) is done before the receive stream rewrites the G-buffer
-        if (peers) SFD_HIP(d, hipEventRecord(s.start, st));
+        // (joined first: a consumer of the previous frame queued on a caller's stream, e.g. sf_download_async on
+        // stream X, is ordered into the context stream before the start event the receive stream waits for)
+        if (peers) {
+            if (int rc = sfi_join(s.ctx)) return rc;
+            SFD_HIP(d, hipEventRecord(s.start, st));
+        }
         // rank 0: its bands in place on the context stream ...
         if (int rc = sf_render(s.ctx, &p)) return rc;
         if (peers) {

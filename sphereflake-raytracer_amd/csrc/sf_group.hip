@@ -29,6 +29,8 @@
 // (sf_capi.hip) the unpack without the context's stream join: the caller orders `s` itself
 extern "C" int sfi_unpack_slabs(sf_ctx* c, const void* stage, uint32_t bytes_per_pixel, uint32_t stage_rows, uint32_t band_rows,
                      uint32_t band_count, uint32_t first_member, uint32_t members, hipStream_t s, bool join);
+// (sf_capi.hip) join the context stream after the context's previous calls on any stream (ctx_join)
+extern "C" int sfi_join(sf_ctx* c);
 
 struct sf_group {
     int n = 0;
@@ -290,6 +292,9 @@ extern "C" int sf_group_render(sf_group* g, uint32_t band_rows)
     hipStream_t s0 = (hipStream_t)sf_context_stream(g->ctx[0]);
     if (peers) {
         Dev d(g->device[0]);
+        // joined first: work queued on member 0 on a caller's stream (sf_download_async, sf_post_process on stream
+        // X) is ordered into s0 before start0, which is all the unpack stream waits for
+        if (int rc = sfi_join(g->ctx[0])) return rc;
         SFG_HIP(g, hipEventRecord(g->start0, s0));
     }
     if (int rc = sf_render(g->ctx[0], &p)) return rc;

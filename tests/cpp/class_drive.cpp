@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "Sphereflake.hpp"
+#include "SphereflakeSSAO.hpp"
 
 using namespace SphereflakeRaytracer;
 
@@ -177,7 +178,7 @@ int main(int argc, char** argv)
         std::fclose(out);
         std::printf("%d %lld %a\n", flake.GetMaxDepthReached(), rays, flake.GetClosestSphereDistance());
         if (argc > 17) {
-            SSAO ssao(flake, 1);
+            Headless::SSAO ssao(flake, 1);
             ssao.SetSampleRadiusMultiplier(flake.GetClosestSphereDistance());
             ssao.SetCameraPosition(sf_vec3(v[0], v[1], v[2]));
             ssao.Render();

@@ -179,3 +179,44 @@ def test_group_band_split_change_resizes():
             g.Render(band)
             pos, nrm = g.download()
             assert same_bits(pos, spos) and same_bits(nrm, snrm), band
+
+
+def test_group_caller_stream_consumer_not_overwritten():
+    """a consumer of member 0's frame queued on a CALLER's stream (sf_download_async on stream X) must
+    finish reading before the next group frame's unpack rewrites the peer rows. The unpack stream waits only for
+    the frame's start event on member 0's context stream, so that event has to follow the context's join of X
+    (sfi_join before start0 in sf_group_render). Frames of 1280x720 with a D2H (~0.5 ms) that outlasts the next
+    frame's trace + unpack: every capture must equal the one-context render of its own view."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    W, H = 1280, 720
+    views = []
+    for j in range(3):
+        cam = sf.config_camera(W, H, 0.8)
+        cam.SetYaw(np.float32(sf.DEFAULT_YAW + 0.02 * (j - 1)))
+        views.append(cam)
+    L = sf.lib()
+    caps = [(np.zeros((H, W, 4), np.float32), np.zeros((H, W, 4), np.float32)) for _ in views]
+    for p, n in caps:
+        for a in (p, n):
+            assert L.sf_host_register(a.ctypes.data_as(ctypes.c_void_p), a.nbytes) == 0
+    x = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(x)) == 0
+    try:
+        with sf.SphereflakeGroup([0, 0, 0], W, H) as g:
+            c0 = g.member(0)
+            for cam, (p, n) in zip(views, caps):
+                g.SetCamera(cam)
+                g.Render(8)
+                assert L.sf_download_async(c0, p.ctypes.data_as(ctypes.c_void_p), n.ctypes.data_as(ctypes.c_void_p),
+                                           None, None, x) == 0
+            g.Synchronize()
+            assert hip.hipStreamSynchronize(x) == 0
+        for j, (cam, (p, n)) in enumerate(zip(views, caps)):
+            spos, snrm, _ = single(W, H, cam)
+            assert same_bits(p, spos) and same_bits(n, snrm), f"frame {j}"
+    finally:
+        hip.hipStreamDestroy(x)
+        for p, n in caps:
+            for a in (p, n):
+                L.sf_host_unregister(a.ctypes.data_as(ctypes.c_void_p))
