@@ -1,0 +1,290 @@
+/* wave_sim.c -- CPU model of the product kernel's wave-coherent traversal (traverse_ray in
+ * sphereflake-raytracer_amd/csrc/sf_kernels.hip), for counting its work per 8x8 tile (experiment, not product).
+ *
+ * One 8x8 tile = one wave of 64 lanes. The DFS visits a node iff some lane visits it; per lane the reference's
+ * per-ray semantics (Sphereflake.h:86-226) are kept through lane masks, exactly as the kernel does:
+ *   root bounding + LOD, root self test, expand (child frames, tile-cone cull, inline-leaf bits, front bits),
+ *   then the children in entry order (front children first): bounding test of the visiting lanes, LOD,
+ *   max-depth update, occlusion cull, self test (pre-order, ancestor tie rule), and a push for non-leaves.
+ * It counts what the kernel pays for: expansions, child-loop iterations (and those no lane passes), entries,
+ * inline leaves, active lanes per iteration -- per depth -- and checks minT / hit index against the oracle.
+ *
+ * Variants (mode bits) model candidate kernel changes so they can be priced before they are written:
+ *   1: per-node cone -- the cone cull of a node's children uses the half-angle of the lanes visiting the node
+ *      (around the tile axis) instead of the whole tile's.
+ * Built by scripts/experiments/wave_sim.py against oracle/sf_oracle.c (included).
+ */
+#include <stdlib.h>
+#include <float.h>
+#include "../../oracle/sf_oracle.c"
+
+#define NST 32
+#define SF_OCCL_MARGIN_SIM 0x1.8p-9f
+
+/* the kernel's per-depth constants (sf_capi.hip upload_consts, sf_setup.cpp depth_tables / leaf_threshold) */
+static float lod_thr(float r, float C)
+{
+    uint32_t lo = 0, hi = 0x7f800000u;
+    while (hi - lo > 1) {
+        uint32_t mid = lo + (hi - lo) / 2;
+        float t; memcpy(&t, &mid, 4);
+        if (sqrtf(t / r) < C || t < 0.0f) lo = mid; else hi = mid;
+    }
+    float t; memcpy(&t, &hi, 4);
+    return t;
+}
+void wsim_depth8(float lod_constant, float* out /* NST x 8 */)
+{
+    float r2b[NST + 1], r2s[NST + 1], sc[NST + 1], T[NST + 1];
+    float p = 3.0f;
+    for (int d = 0; d <= NST; ++d) {
+        float r = p / 3.0f; p = r;
+        float dr = r * 2.0f;
+        r2b[d] = dr * dr; r2s[d] = r * r; sc[d] = (4.0f / 3.0f) * r; T[d] = lod_thr(r, lod_constant);
+    }
+    for (int d = 0; d < NST; ++d) {
+        float* e = out + 8 * d;
+        e[0] = r2b[d]; e[1] = r2s[d]; e[2] = sc[d]; e[3] = T[d];
+        double Tn = T[d + 1], R = sqrt((double)r2b[d + 1]), s = sc[d];
+        double th = (Tn * (1.0 + 0x1p-12) + 2.0 * R + s * (1.0 + 0x1p-8)) / (1.0 - 0x1p-7);
+        e[4] = (float)(th * th * (1.0 + 0x1p-10));
+        e[5] = nextafterf((float)(sqrt((double)e[0]) * (1.0 + 2.0 * (double)SF_OCCL_MARGIN_SIM)), FLT_MAX);
+        e[6] = nextafterf((float)((double)e[3] + sqrt((double)e[0]) * (1.0 + 0x1p-18)), FLT_MAX);
+        e[7] = 0.0f;
+    }
+}
+typedef struct {
+    long long exp[NST], iter[NST], miss[NST], lodnone[NST], occlnone[NST], entered[NST], leaf[NST], push[NST];
+    long long act[NST], hitl[NST];   /* active lanes summed over iterations; bounding-hit lanes summed */
+    long long tiles, mismatch, ties, maxd;
+    long long cone_tested[NST], cone_culled[NST];
+    long long skip_exp[NST], skip_lost[NST];   /* expansions the useless-cone predicate skips; culls lost by it */
+} sim_stats_t;
+
+typedef struct {
+    const float* child;
+    const uint32_t* lut;
+    float r2b[NST], r2s[NST], scale[NST], T[NST], leaf[NST], cull[NST], far_[NST];
+    int mode;
+    float skip_k, skip_f;
+    /* tile */
+    float D[64][3];
+    float ax[3], cosT, sinT;
+    float s2[64];            /* per lane |d x a|^2 (mode 1) */
+    float minT[64];
+    uint64_t idx[64];
+    int hdepth[64];
+    int maxd;
+    float cull_t;
+    sim_stats_t* st;
+} wsim_t;
+
+static int is_anc(uint64_t a, uint64_t n)
+{
+    while (n > a) n = (n - 1) / 9;
+    return n == a;
+}
+
+static float near_root_f(float tca, float d2, float R2)
+{
+    float thc = sqrtf(R2 - d2);
+    float t0 = tca + thc, t1 = tca - thc;
+    return (t0 <= t1) ? t0 : t1;
+}
+
+/* self test of sphere (centre C, cc) at depth dd, heap index id, for the lanes of m */
+static void self_test(wsim_t* S, const float C[3], float cc, int dd, uint64_t id, uint64_t m)
+{
+    for (int l = 0; l < 64; ++l) {
+        if (!((m >> l) & 1)) continue;
+        const float* D = S->D[l];
+        float tca = (C[0] * D[0] + C[1] * D[1]) + C[2] * D[2];
+        float d2 = cc - tca * tca;
+        float R2 = S->r2s[dd];
+        if (!(tca >= 0.0f && d2 <= R2)) continue;
+        float ts = near_root_f(tca, d2, R2);
+        if (ts < S->minT[l]) {
+            S->minT[l] = ts; S->idx[l] = id; S->hdepth[l] = dd;
+        } else if (ts == S->minT[l]) {
+            if (S->hdepth[l] >= 0 && is_anc(S->idx[l], id)) { S->minT[l] = ts; S->idx[l] = id; S->hdepth[l] = dd; }
+            else S->st->ties++;
+        }
+    }
+}
+
+/* the node at depth d with frame M (16 floats) is entered by the lanes of A (already self-tested) and expands */
+static void expand_node(wsim_t* S, const float* M, int d, uint64_t node, uint64_t A)
+{
+    sim_stats_t* st = S->st;
+    st->exp[d]++;
+    const int dc = d + 1;
+    float W[9][16];
+    float cc[9];
+    int front[9], culled[9], leaf[9];
+    const float* P = M + 12;
+    const float* ax = S->ax;
+    const float kp = (P[0] * ax[0] + P[1] * ax[1]) + P[2] * ax[2];
+    float sinT = S->sinT, cosT = S->cosT;
+    if (S->mode & 1) {   /* per-node cone: max over the visiting lanes */
+        float smax = 0.0f;
+        for (int l = 0; l < 64; ++l)
+            if ((A >> l) & 1) smax = S->s2[l] > smax ? S->s2[l] : smax;
+        float sm = sqrtf(smax) * (1.0f + 0x1p-16f) + 0x1p-16f;
+        sinT = 1.0f; cosT = 0.0f;
+        if (sm < 0.5f) { sinT = sm; cosT = sqrtf(1.0f - sm * sm) * (1.0f - 0x1p-16f); }
+    }
+    /* predicate: the cone (plus the float tests' slack) is as wide as the node's bounding ball seen from the camera */
+    const float pw = (P[0] * P[0] + P[1] * P[1]) + P[2] * P[2];
+    const float sk = sinT + S->skip_k;
+    const int skip = pw * sk * sk >= S->skip_f * S->r2b[d];
+    if (skip) st->skip_exp[d]++;
+    for (int i = 0; i < 9; ++i) {
+        float T[16];
+        memcpy(T, S->child + 16 * i, sizeof T);
+        float s = S->scale[d];
+        T[12] = T[12] * s; T[13] = T[13] * s; T[14] = T[14] * s;
+        matmul(M, T, W[i]);
+        const float* C = W[i] + 12;
+        float w = (C[0] * C[0] + C[1] * C[1]) + C[2] * C[2];
+        cc[i] = w;
+        const float R2b = S->r2b[dc];
+        float dl = w * 0x1p-18f;
+        float ca = (C[0] * ax[0] + C[1] * ax[1]) + C[2] * ax[2];
+        float q = w - ca * ca; if (q < 0.0f) q = 0.0f;
+        float sq = sqrtf(q);
+        float X = sq * cosT - ca * sinT;
+        float Y = X * X - (R2b + w * (0x1p-18f + 0x1p-19f));
+        float a1 = ca < w - 2.0f * (R2b + dl) ? ca : w - 2.0f * (R2b + dl);
+        float a2 = X < Y ? X : Y;
+        float mk = a1 < a2 ? a1 : a2;
+        culled[i] = mk > 0.0f;
+        leaf[i] = w > S->leaf[dc];
+        front[i] = ca < kp;
+        st->cone_tested[d]++;
+        st->cone_culled[d] += culled[i];
+        if (skip && culled[i]) st->skip_lost[d]++;
+        if (skip && (S->mode & 2)) culled[i] = 0;
+    }
+    int order[18], n = 0;
+    for (int i = 0; i < 9; ++i) if (!culled[i] && front[i]) order[n++] = i;
+    for (int i = 0; i < 9; ++i) if (!culled[i] && !front[i]) order[n++] = i;
+    for (int k = 0; k < n; ++k) {
+        const int c = order[k];
+        const float* C = W[c] + 12;
+        st->iter[d]++;
+        st->act[d] += __builtin_popcountll(A);
+        uint64_t hb = 0, ex = 0;
+        for (int l = 0; l < 64; ++l) {
+            if (!((A >> l) & 1)) continue;
+            const float* D = S->D[l];
+            float tca = (C[0] * D[0] + C[1] * D[1]) + C[2] * D[2];
+            float d2 = cc[c] - tca * tca;
+            if (!(tca >= 0.0f && d2 <= S->r2b[dc])) continue;
+            hb |= 1ull << l;
+            float t = near_root_f(tca, d2, S->r2b[dc]);
+            if (t < S->T[dc]) ex |= 1ull << l;
+        }
+        st->hitl[d] += __builtin_popcountll(hb);
+        if (!hb) { st->miss[d]++; continue; }
+        if (!ex) { st->lodnone[d]++; continue; }
+        if (dc > S->maxd) { S->maxd = dc; S->cull_t = S->T[dc + 1]; }
+        uint64_t am = ex;
+        for (int l = 0; l < 64; ++l) {
+            if (!((ex >> l) & 1)) continue;
+            const float* D = S->D[l];
+            float tca = (C[0] * D[0] + C[1] * D[1]) + C[2] * D[2];
+            float v1 = tca - S->minT[l], v2 = tca - S->cull_t;
+            float v = v1 < v2 ? v1 : v2;
+            if (v - SF_OCCL_MARGIN_SIM * tca > S->cull[dc]) am &= ~(1ull << l);
+        }
+        if (!am) { st->occlnone[d]++; continue; }
+        st->entered[d]++;
+        const uint64_t id = 9 * node + 1 + (uint64_t)c;
+        self_test(S, C, cc[c], dc, id, am);
+        if (leaf[c]) { st->leaf[d]++; continue; }
+        st->push[d]++;
+        expand_node(S, W[c], dc, id, am);
+    }
+}
+
+int wsim_tiles(uint32_t W, uint32_t H, const float o[3], const float tl[3], const float tr[3], const float bl[3],
+               const float root[16], const float child[9 * 16], const uint32_t* lut, const float* depth8,
+               uint32_t t0, uint32_t t1, int mode, const float* ref_minT, const uint32_t* ref_idx, sim_stats_t* st)
+{
+    wsim_t S;
+    memset(&S, 0, sizeof S);
+    S.child = child; S.lut = lut; S.mode = mode; S.st = st;
+    S.skip_k = 0x1p-9f; S.skip_f = 4.0f;
+    if (getenv("SKIP_K")) S.skip_k = strtof(getenv("SKIP_K"), NULL);
+    if (getenv("SKIP_F")) S.skip_f = strtof(getenv("SKIP_F"), NULL);
+    for (int d = 0; d < NST; ++d) {
+        S.r2b[d] = depth8[8 * d + 0]; S.r2s[d] = depth8[8 * d + 1]; S.scale[d] = depth8[8 * d + 2];
+        S.T[d] = depth8[8 * d + 3]; S.leaf[d] = depth8[8 * d + 4]; S.cull[d] = depth8[8 * d + 5];
+        S.far_[d] = depth8[8 * d + 6];
+    }
+    const float fw = (float)W, fh = (float)H;
+    const float dh[3] = { tr[0] - tl[0], tr[1] - tl[1], tr[2] - tl[2] };
+    const float dv[3] = { bl[0] - tl[0], bl[1] - tl[1], bl[2] - tl[2] };
+    const uint32_t tw = (W + 7) / 8;
+    for (uint32_t t = t0; t < t1; ++t) {
+        const uint32_t tx = t % tw, ty = t / tw;
+        uint64_t valid = 0;
+        for (int l = 0; l < 64; ++l) {
+            uint32_t x = tx * 8 + (l & 7), y = ty * 8 + (l >> 3);
+            float u = (float)x / fw, v = (float)y / fh;
+            float* D = S.D[l];
+            D[0] = ((tl[0] + dh[0] * u) + dv[0] * v) - o[0];
+            D[1] = ((tl[1] + dh[1] * u) + dv[1] * v) - o[1];
+            D[2] = ((tl[2] + dh[2] * u) + dv[2] * v) - o[2];
+            normalize3(D, lut);
+            if (x < W && y < H) valid |= 1ull << l;
+            S.minT[l] = FLT_MAX; S.idx[l] = 0xffffffffu; S.hdepth[l] = -1;
+        }
+        /* tile cone around lane 36's ray */
+        memcpy(S.ax, S.D[36], sizeof S.ax);
+        float smax = 0.0f;
+        for (int l = 0; l < 64; ++l) {
+            const float* D = S.D[l];
+            const float* a = S.ax;
+            float c0 = D[1] * a[2] - D[2] * a[1], c1 = D[2] * a[0] - D[0] * a[2], c2 = D[0] * a[1] - D[1] * a[0];
+            float s2 = (c0 * c0 + c1 * c1) + c2 * c2;
+            int fwd = (D[0] * a[0] + D[1] * a[1]) + D[2] * a[2] > 0.0f;
+            float s2m = fwd ? s2 : 1.0f;
+            S.s2[l] = s2m;
+            if (s2m > smax) smax = s2m;
+        }
+        float sm = sqrtf(smax) * (1.0f + 0x1p-16f) + 0x1p-16f;
+        S.sinT = 1.0f; S.cosT = 0.0f;
+        if (sm < 0.5f) { S.sinT = sm; S.cosT = sqrtf(1.0f - sm * sm) * (1.0f - 0x1p-16f); }
+        /* root */
+        const float* C = root + 12;
+        const float rcc = (C[0] * C[0] + C[1] * C[1]) + C[2] * C[2];
+        uint64_t ex0 = 0;
+        for (int l = 0; l < 64; ++l) {
+            if (!((valid >> l) & 1)) continue;
+            const float* D = S.D[l];
+            float tca = (C[0] * D[0] + C[1] * D[1]) + C[2] * D[2];
+            float d2 = rcc - tca * tca;
+            if (tca >= 0.0f && d2 <= S.r2b[0] && near_root_f(tca, d2, S.r2b[0]) < S.T[0]) ex0 |= 1ull << l;
+        }
+        st->tiles++;
+        if (ex0) {
+            S.maxd = 0;
+            S.cull_t = S.T[1];
+            self_test(&S, C, rcc, 0, 0, ex0);
+            if (!(rcc > S.leaf[0])) expand_node(&S, root, 0, 0, ex0);
+            if (S.maxd > st->maxd) st->maxd = S.maxd;
+        }
+        if (ref_minT) {
+            for (int l = 0; l < 64; ++l) {
+                uint32_t x = tx * 8 + (l & 7), y = ty * 8 + (l >> 3);
+                if (x >= W || y >= H) continue;
+                size_t p = (size_t)y * W + x;
+                uint32_t a, b;
+                memcpy(&a, &S.minT[l], 4); memcpy(&b, &ref_minT[p], 4);
+                if (a != b || (uint32_t)S.idx[l] != ref_idx[p]) st->mismatch++;
+            }
+        }
+    }
+    return 0;
+}

@@ -297,6 +297,14 @@ __device__ __forceinline__ uint32_t writelane_u(uint32_t v, uint32_t l, uint32_t
     return (threadIdx.x & 63u) == l ? v : old;
 }
 
+// Lane l of `old` := v (uniform v and l): one v_writelane_b32 (traverse_ray's push; a select costs v_cmp, v_mov and
+// v_cndmask per word)
+__device__ int sf_amdgcn_writelane(int v, int l, int old) __asm("llvm.amdgcn.writelane.i32");   // (no clang builtin)
+__device__ __forceinline__ uint32_t writelane_s(uint32_t v, uint32_t l, uint32_t old)
+{
+    return (uint32_t)sf_amdgcn_writelane((int)v, (int)l, (int)old);
+}
+
 // One lane's 64-bit global atomic add on behalf of the wave (EXEC forced to lane 0 inside the asm).
 __device__ __forceinline__ void wave_atomic_add_u64(uint64_t* p, uint64_t v)
 {
@@ -1152,7 +1160,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
     const uint32_t index_order = front_first ? 0u : 0x1ffu;
     // (tb: table(d), ko: d + 1's constants offset -- the caller's carried values, not formed here again)
     auto expand = [&](const float4 pc, const float* col, uint32_t cs, uint32_t d, float actv, uint32_t& leafm,
-                      float* tb, uint32_t ko) -> uint32_t {
+                      float* tb, uint32_t ko, float kp) -> uint32_t {
         d = __builtin_amdgcn_readfirstlane(d);
         SF_COUNT(0, 1);
         SF_COUNT(7, __builtin_popcountll(wave_ballot(actv >= 0.0f)));   // (COUNTS builds: lanes visiting the node)
@@ -1177,21 +1185,26 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             *(bc == 3u ? tb + slot + 3u : L.cone() + 5u) = w;
         }
         const float R2b = dtc.x;
-        // cone cull of child bi (centre lanes 32..40), in squares (see traverse)
+        // cone cull of child bi (centre lanes 32..40), in squares (see traverse). The test is this kernel's own
+        // arithmetic, not the reference's, so it fuses: ca, |c|^2 - ca^2, X and Y by fma -- each fused step rounds
+        // once where the unfused one rounded twice, so the error bounds behind the slack (traverse) still hold --
+        // and the regime condition |c|^2 > 2 (R^2 + 2^-18 |c|^2) as w (1 - 2^-16) > 2 R^2, a slightly stronger
+        // one. 15 VALU instead of 23 per expansion. (w itself stays the reference's |c|^2: it is the table's cc.)
         const float ax = cn.x, ay = cn.y, az = cn.z, cosT = cn.w;
-        const float dl = w * 0x1p-18f;
-        const float ca = (x * ax + y * ay) + z * az;
-        const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaxf(w - ca * ca, 0.0f));
-        const float X = sq * cosT - ca * sinT;
-        const float Y = X * X - (R2b + w * (0x1p-18f + 0x1p-19f));
-        const float mk = __builtin_fminf(__builtin_fminf(ca, w - 2.0f * (R2b + dl)), __builtin_fminf(X, Y));
+        const float ca = __builtin_fmaf(x, ax, __builtin_fmaf(y, ay, z * az));
+        const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaxf(__builtin_fmaf(-ca, ca, w), 0.0f));
+        const float X = __builtin_fmaf(sq, cosT, -(ca * sinT));
+        const float Y = __builtin_fmaf(X, X, -(R2b + w * (0x1p-18f + 0x1p-19f)));
+        const float reg = __builtin_fmaf(w, 1.0f - 0x1p-16f, -2.0f * R2b);
+        const float mk = __builtin_fminf(__builtin_fminf(ca, reg), __builtin_fminf(X, Y));
         uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 32) & 0x1ffu;
         M = __builtin_amdgcn_readfirstlane(M);
         leafm = (uint32_t)(wave_ballot(w > leafc) >> 32) & 0x1ffu;
         // entry order as bit order: the front children (nearer than this node's centre along the cone axis) at
         // bits 0..8, the others at 9..17 -- one find-first-set per child picks the next
         // (index order, front_first false: every child "front" -- an OR with a per-traversal mask, not a branch)
-        const float kp = (pc.x * ax + pc.y * ay) + pc.z * az;
+        // (kp = (pc.x ax + pc.y ay) + pc.z az, the node's own projection: the caller passes the axis lane's tca of the
+        // node, the same operations on the same operands -- the cone axis IS that lane's direction)
         const uint32_t front = ((uint32_t)(wave_ballot(ca < kp) >> 32) & 0x1ffu) | index_order;
         if (ko >= lv32) {   // (d + 1 >= levels)
             const float T = dtc.w, Tfar = depth_word_at(K, ko, 6u);   // depth_far(K, d + 1)
@@ -1232,7 +1245,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float d2 = pc.w - tca * tca;
         self_test(pc, tca, d2, 0u, actv, 0u, depth_consts(K, 0u).y);
         if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u)))))
-            C = expand(pc, L.root() + 4u, 4u, 0u, actv, leafN, tcur, kofs);
+            C = expand(pc, L.root() + 4u, 4u, 0u, actv, leafN, tcur, kofs, readlane_f(tca, axl));
         else SF_COUNT(4, 1);
     }
 
@@ -1243,7 +1256,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         SF_STAMP(0);
         if (C) {
             const uint32_t p = __builtin_ctz(C);
-            C &= C - 1u;
+            __asm__("s_bitset0_b32 %0, %1" : "+s"(C) : "s"(p));   // (one scalar op; C &= C - 1 is two)
             const uint32_t c = min(p, p - 9u);   // (p < 9: front child p; else child p - 9)
             // the children's depth constants (scalar loads, in flight with the centre's LDS read)
             const float4 dc = depth_consts_at(K, kofs);
@@ -1307,8 +1320,8 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
                 continue;
             }
             // push the open node, open child c
-            stk_pc = writelane_u(C | (leafN << 18), d, stk_pc);
-            stk_ix = writelane_u(idxB, d, stk_ix);
+            stk_pc = writelane_s(C | (leafN << 18), d, stk_pc);
+            stk_ix = writelane_s(idxB, d, stk_ix);
             {
                 const uint32_t bit = 2u << d;   // level d + 1
                 uint32_t ab = actbits & ~bit;
@@ -1322,7 +1335,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             const float* const col = tcur + SF_LDS_PLANE + 3u * c;   // the entered child's axis columns
             tcur += SF_LDS_LEVEL;
             kofs += 1u << 5;
-            C = expand(pc, col, SF_LDS_COLS, d, avx, leafN, tcur, kofs);
+            C = expand(pc, col, SF_LDS_COLS, d, avx, leafN, tcur, kofs, readlane_f(tca, axl));
             R2c = depth_consts_at(K, kofs).x;
             if (COMPACT && C != 0u) {
                 // ---- Active-ray compaction of sparse nodes (north star: "wavefront ballot / prefix-sum active-ray
