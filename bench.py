@@ -198,7 +198,9 @@ def pmc_valu(c, frame_ms, clock_mhz, cus=256):
     (one launch = one frame) against the issue slots of one frame period at the live shader clock -- VALU: CUs x 4
     SIMDs x cycles / 2 (one wave64 VALU instruction issues over 2 cycles), SALU: one scalar instruction per CU per
     cycle. `lone_dispatch` keeps the PMC pass's own view: the passes serialise dispatches, so there one launch runs
-    alone (its duration GRBM_GUI_ACTIVE / 8 XCDs cycles), with the occupancy it reached."""
+    alone; its cycles are its profiled duration x the live shader clock of the bench's own renders (`clock_mhz`,
+    from the kernel's s_memtime / s_memrealtime probe). (Round 4 divided GRBM_GUI_ACTIVE / 8 by the duration, which
+    counts GPU-busy cycles outside the kernel and read 2521 MHz, above the gfx950 maximum of 2400.)"""
     if c is None:
         return None
     try:
@@ -210,12 +212,15 @@ def pmc_valu(c, frame_ms, clock_mhz, cus=256):
             out["valu_issue_frac"] = round(c["SQ_INSTS_VALU"] / (cus * 4 * fcyc / 2.0), 4)
             out["salu_issue_frac"] = round(c["SQ_INSTS_SALU"] / (cus * fcyc), 4)
             out["basis"] = "per launch / issue slots of one frame period (ms_per_step) at clock_mhz_live"
-        cycles = c["GRBM_GUI_ACTIVE"] / 8.0
+        if not clock_mhz:
+            return out
+        cycles = c["profiled_dispatch_us"] * clock_mhz
         # wavefront occupancy: SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md), summed over the
         # chip -> mean resident waves; against the gfx950 peak of 8 waves per SIMD
         waves = 4.0 * c["SQ_WAVE_CYCLES"] / cycles
         peak_waves = cus * 4 * 8
-        lone = {"dispatch_us": round(c["profiled_dispatch_us"], 2), "clock_mhz": round(cycles / c["profiled_dispatch_us"], 1),
+        lone = {"dispatch_us": round(c["profiled_dispatch_us"], 2), "clock_mhz": round(clock_mhz, 1),
+                "clock_basis": "clock_mhz_live of the bench's renders (the kernel's own clock probe)",
                 "valu_issue_frac": round(c["SQ_INSTS_VALU"] / (cus * 4 * cycles / 2.0), 4),
                 "salu_issue_frac": round(c["SQ_INSTS_SALU"] / (cus * cycles), 4),
                 "occupancy": {"mean_waves": round(waves, 1), "peak_waves": peak_waves, "frac": round(waves / peak_waves, 4)}}

@@ -59,6 +59,7 @@ typedef struct {
     long long tiles, mismatch, ties, maxd;
     long long cone_tested[NST], cone_culled[NST];
     long long skip_exp[NST], skip_lost[NST];   /* expansions the useless-cone predicate skips; culls lost by it */
+    long long cache_hit[NST];                  /* expansions whose level table already holds their children */
 } sim_stats_t;
 
 typedef struct {
@@ -77,6 +78,7 @@ typedef struct {
     int maxd;
     float cull_t;
     sim_stats_t* st;
+    uint64_t owner[NST];     /* level-table cache: node whose children the wave's table(d) holds (mode 4 reuses it) */
 } wsim_t;
 
 static int is_anc(uint64_t a, uint64_t n)
@@ -117,6 +119,8 @@ static void expand_node(wsim_t* S, const float* M, int d, uint64_t node, uint64_
 {
     sim_stats_t* st = S->st;
     st->exp[d]++;
+    if (S->owner[d] == node) st->cache_hit[d]++;
+    S->owner[d] = node;
     const int dc = d + 1;
     float W[9][16];
     float cc[9];
@@ -226,8 +230,11 @@ int wsim_tiles(uint32_t W, uint32_t H, const float o[3], const float tl[3], cons
     const float dh[3] = { tr[0] - tl[0], tr[1] - tl[1], tr[2] - tl[2] };
     const float dv[3] = { bl[0] - tl[0], bl[1] - tl[1], bl[2] - tl[2] };
     const uint32_t tw = (W + 7) / 8;
+    for (int k = 0; k < NST; ++k) S.owner[k] = ~0ull;
+    const uint32_t run = (mode & 8) ? 4u : (mode & 16) ? 2u : 1u;   /* tiles per wave run (cache kept within a run) */
     for (uint32_t t = t0; t < t1; ++t) {
         const uint32_t tx = t % tw, ty = t / tw;
+        if ((t - t0) % run == 0) for (int k = 0; k < NST; ++k) S.owner[k] = ~0ull;
         uint64_t valid = 0;
         for (int l = 0; l < 64; ++l) {
             uint32_t x = tx * 8 + (l & 7), y = ty * 8 + (l >> 3);

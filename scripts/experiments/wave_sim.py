@@ -26,7 +26,8 @@ TAIL = ["tiles", "mismatch", "ties", "maxd"]
 class Stats(ctypes.Structure):
     _fields_ = [(f, ctypes.c_longlong * NST) for f in FIELDS] + [(f, ctypes.c_longlong) for f in TAIL] + \
                [("cone_tested", ctypes.c_longlong * NST), ("cone_culled", ctypes.c_longlong * NST),
-                ("skip_exp", ctypes.c_longlong * NST), ("skip_lost", ctypes.c_longlong * NST)]
+                ("skip_exp", ctypes.c_longlong * NST), ("skip_lost", ctypes.c_longlong * NST),
+                ("cache_hit", ctypes.c_longlong * NST)]
 
 
 fp = ctypes.POINTER(ctypes.c_float)
@@ -64,7 +65,7 @@ def run(name="c3", tile_step=1, mode=0, check=True):
                      ctypes.byref(parts[k]))
     with ThreadPoolExecutor(8) as ex:
         list(ex.map(work, range(len(trows))))
-    tot = {f: np.sum([np.array(getattr(p, f)[:]) for p in parts], 0) for f in FIELDS + ["cone_tested", "cone_culled", "skip_exp", "skip_lost"]}
+    tot = {f: np.sum([np.array(getattr(p, f)[:]) for p in parts], 0) for f in FIELDS + ["cone_tested", "cone_culled", "skip_exp", "skip_lost", "cache_hit"]}
     for f in TAIL:
         tot[f] = max(getattr(p, f) for p in parts) if f == "maxd" else sum(getattr(p, f) for p in parts)
     tot["scale"] = tile_step
@@ -81,7 +82,8 @@ def report(t, label=""):
         it = t["iter"][d]
         print(f"{d:2d} {t['exp'][d]*sc:7d} {it*sc:8d} {t['miss'][d]*sc:7d} {t['lodnone'][d]*sc:7d} {t['occlnone'][d]*sc:7d}"
               f" {t['entered'][d]*sc:7d} {t['leaf'][d]*sc:7d} {t['push'][d]*sc:7d} {t['act'][d]/max(it,1):6.1f}"
-              f"  {t['cone_culled'][d]/max(t['cone_tested'][d],1):.3f}  {t['skip_exp'][d]*sc:7d} {t['skip_lost'][d]*sc:6d}")
+              f"  {t['cone_culled'][d]/max(t['cone_tested'][d],1):.3f}  {t['skip_exp'][d]*sc:7d} {t['skip_lost'][d]*sc:6d}"
+              f"  hit {t['cache_hit'][d]/max(t['exp'][d],1):.2f}")
     tot = lambda f: int(t[f].sum()) * sc
     print(f"all {tot('exp'):8d} {tot('iter'):8d} {tot('miss'):7d} {tot('lodnone'):7d} {tot('occlnone'):7d} {tot('entered'):7d}"
           f" {tot('leaf'):7d} {tot('push'):7d} {t['act'].sum()/max(t['iter'].sum(),1):6.1f}")

@@ -1471,8 +1471,11 @@ __device__ __forceinline__ void write_pixel(const FrameArgs& a, const Tile& t, f
             // 4 B: the hit's heap index; the receiver rebuilds the rest. (The host selects this format only where
             // no hit can lie deeper than SF_INDEX_SLAB_DEPTH, whose heap indices are below 2^32; a deeper one would
             // be ambiguous and is written as SF_SLAB_BAD instead.)
-            reinterpret_cast<uint32_t*>(a.pos)[o] = !h.hit ? SF_SLAB_MISS
-                                                  : h.depth > SF_INDEX_SLAB_DEPTH ? SF_SLAB_BAD : h.index;
+            const bool bad = h.hit && h.depth > SF_INDEX_SLAB_DEPTH;
+            reinterpret_cast<uint32_t*>(a.pos)[o] = !h.hit ? SF_SLAB_MISS : bad ? SF_SLAB_BAD : h.index;
+            // such a pixel counts as unresolved (stats[2]): sf_synchronize then reports SF_EDEPTH instead of the gather
+            // silently carrying a NaN pixel (the host's depth proof and the device must never disagree)
+            if (bad) atomicAdd(reinterpret_cast<uint32_t*>(a.stats) + 2, 1u);
             return;
         }
         reinterpret_cast<float4*>(a.pos)[o] = make_float4(nx, ny, nz, h.minT);
@@ -1849,10 +1852,10 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
                                                                                at.counters + at.parity, part,
                                                ticket, again ? (at.flags | SF_FLAG_NO_FRONT_FIRST | SF_FLAG_REDO_PASS)
                                                              : at.flags);
-        if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace) {   // diagnostics only (uniform words)
-            // (g & SF_UNIT_TILE_MASK: a re-trace pass's ticket word carries bit 31 and the part; masked, its record
-            // lands in range -- on its tile's slot -- without keeping a flag live across the traversal)
-            uint64_t* ut = at.tile_trace + 3u * (at.tiles_x * at.tile_rows) + SF_DIAG_SLOTS + 3u * (g & SF_UNIT_TILE_MASK);
+        if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace && (g >> 31) == 0u) {   // diagnostics only (uniform words)
+            // (slot g: the unit's position in the order. A re-trace pass -- its ticket word carries bit 31 -- records
+            // nothing: its word is no position, and the slot of the unit it repeats already holds that unit's record)
+            uint64_t* ut = at.tile_trace + 3u * (at.tiles_x * at.tile_rows) + SF_DIAG_SLOTS + 3u * g;
             ut[0] = u_start;
             ut[1] = __builtin_amdgcn_s_memrealtime();
             ut[2] = t | (part << SF_UNIT_PART_SHIFT);

@@ -52,7 +52,11 @@ def test_issue_fractions_on_the_frame_period():
     assert v["frame_cycles"] == round(fc)
     assert abs(v["valu_issue_frac"] - 59.5e6 / (1024 * fc / 2)) < 1e-4
     assert abs(v["salu_issue_frac"] - 33.0e6 / (256 * fc)) < 1e-4
-    assert v["lone_dispatch"]["valu_issue_frac"] == round(59.5e6 / (1024 * 300000.0 / 2), 4)
+    # the lone dispatch's cycles: its duration at the live clock (never a clock above the gfx950 maximum)
+    lc = 130.0 * 2370.0
+    assert v["lone_dispatch"]["clock_mhz"] == 2370.0
+    assert v["lone_dispatch"]["valu_issue_frac"] == round(59.5e6 / (1024 * lc / 2), 4)
+    assert v["lone_dispatch"]["occupancy"]["mean_waves"] == round(4.0 * 3.5e8 / lc, 1)
     assert bench.pmc_valu(None, 0.078, 2370.0) is None
 
 
