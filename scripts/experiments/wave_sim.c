@@ -79,6 +79,11 @@ typedef struct {
     float cull_t;
     sim_stats_t* st;
     uint64_t owner[NST];     /* level-table cache: node whose children the wave's table(d) holds (mode 4 reuses it) */
+    int split_k, split_p;    /* subtree split model: depth-k nodes n to part n % P */
+    int part;                /* pixel part of the tile traced (kernel's SF_PART_*; 0 whole) */
+    int cur_part;            /* part owning the current subtree (-1 above depth k) */
+    double part_work[8];     /* this tile's work per part (child iterations + 6 per expansion) */
+    double shared_work;      /* work above depth k (every part repeats it) */
 } wsim_t;
 
 static int is_anc(uint64_t a, uint64_t n)
@@ -121,6 +126,10 @@ static void expand_node(wsim_t* S, const float* M, int d, uint64_t node, uint64_
     st->exp[d]++;
     if (S->owner[d] == node) st->cache_hit[d]++;
     S->owner[d] = node;
+    const int saved_part = S->cur_part;
+    if (S->split_p > 0 && d == S->split_k) S->cur_part = (int)(node % (uint64_t)S->split_p);
+#define SIM_WORK(w) do { if (S->cur_part < 0) S->shared_work += (w); else S->part_work[S->cur_part] += (w); } while (0)
+    SIM_WORK(6.0);
     const int dc = d + 1;
     float W[9][16];
     float cc[9];
@@ -176,6 +185,7 @@ static void expand_node(wsim_t* S, const float* M, int d, uint64_t node, uint64_
         const int c = order[k];
         const float* C = W[c] + 12;
         st->iter[d]++;
+        SIM_WORK(1.0);
         st->act[d] += __builtin_popcountll(A);
         uint64_t hb = 0, ex = 0;
         for (int l = 0; l < 64; ++l) {
@@ -209,16 +219,19 @@ static void expand_node(wsim_t* S, const float* M, int d, uint64_t node, uint64_
         st->push[d]++;
         expand_node(S, W[c], dc, id, am);
     }
+    S->cur_part = saved_part;
 }
 
 int wsim_tiles(uint32_t W, uint32_t H, const float o[3], const float tl[3], const float tr[3], const float bl[3],
                const float root[16], const float child[9 * 16], const uint32_t* lut, const float* depth8,
-               uint32_t t0, uint32_t t1, int mode, const float* ref_minT, const uint32_t* ref_idx, sim_stats_t* st)
+               uint32_t t0, uint32_t t1, int mode, const float* ref_minT, const uint32_t* ref_idx, sim_stats_t* st,
+               int split_k, int split_p, double* tile_work /* per tile: total, shared, max part (NULL: none) */)
 {
     wsim_t S;
     memset(&S, 0, sizeof S);
     S.child = child; S.lut = lut; S.mode = mode; S.st = st;
     S.skip_k = 0x1p-9f; S.skip_f = 4.0f;
+    S.part = (mode >> 8) & 7;
     if (getenv("SKIP_K")) S.skip_k = strtof(getenv("SKIP_K"), NULL);
     if (getenv("SKIP_F")) S.skip_f = strtof(getenv("SKIP_F"), NULL);
     for (int d = 0; d < NST; ++d) {
@@ -244,7 +257,10 @@ int wsim_tiles(uint32_t W, uint32_t H, const float o[3], const float tl[3], cons
             D[1] = ((tl[1] + dh[1] * u) + dv[1] * v) - o[1];
             D[2] = ((tl[2] + dh[2] * u) + dv[2] * v) - o[2];
             normalize3(D, lut);
-            if (x < W && y < H) valid |= 1ull << l;
+            int in = 1;   /* part units (the kernel's tile_of): 1/2 rows 0-3 / 4-7, 3..6 the 4x4 quarters */
+            if (S.part >= 1 && S.part <= 2) in = (l >> 5) + 1 == S.part;
+            if (S.part >= 3) { int q = S.part - 3; in = (l >> 5) == (q >> 1) && ((l >> 2) & 1) == (q & 1); }
+            if (x < W && y < H && in) valid |= 1ull << l;
             S.minT[l] = FLT_MAX; S.idx[l] = 0xffffffffu; S.hdepth[l] = -1;
         }
         /* tile cone around lane 36's ray */
@@ -264,6 +280,8 @@ int wsim_tiles(uint32_t W, uint32_t H, const float o[3], const float tl[3], cons
         S.sinT = 1.0f; S.cosT = 0.0f;
         if (sm < 0.5f) { S.sinT = sm; S.cosT = sqrtf(1.0f - sm * sm) * (1.0f - 0x1p-16f); }
         /* root */
+        S.split_k = split_k; S.split_p = split_p; S.cur_part = -1; S.shared_work = 0.0;
+        for (int q = 0; q < 8; ++q) S.part_work[q] = 0.0;
         const float* C = root + 12;
         const float rcc = (C[0] * C[0] + C[1] * C[1]) + C[2] * C[2];
         uint64_t ex0 = 0;
@@ -281,6 +299,13 @@ int wsim_tiles(uint32_t W, uint32_t H, const float o[3], const float tl[3], cons
             self_test(&S, C, rcc, 0, 0, ex0);
             if (!(rcc > S.leaf[0])) expand_node(&S, root, 0, 0, ex0);
             if (S.maxd > st->maxd) st->maxd = S.maxd;
+        }
+        if (tile_work) {
+            double tot = S.shared_work, mx = 0.0;
+            for (int q = 0; q < 8; ++q) { tot += S.part_work[q]; if (S.part_work[q] > mx) mx = S.part_work[q]; }
+            tile_work[3 * (t - t0) + 0] = tot;
+            tile_work[3 * (t - t0) + 1] = S.shared_work;
+            tile_work[3 * (t - t0) + 2] = mx;
         }
         if (ref_minT) {
             for (int l = 0; l < 64; ++l) {

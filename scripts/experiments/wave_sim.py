@@ -33,11 +33,12 @@ class Stats(ctypes.Structure):
 fp = ctypes.POINTER(ctypes.c_float)
 up = ctypes.POINTER(ctypes.c_uint32)
 L.wsim_tiles.argtypes = [ctypes.c_uint32, ctypes.c_uint32, fp, fp, fp, fp, fp, fp, up, fp, ctypes.c_uint32,
-                         ctypes.c_uint32, ctypes.c_int, fp, up, ctypes.POINTER(Stats)]
+                         ctypes.c_uint32, ctypes.c_int, fp, up, ctypes.POINTER(Stats), ctypes.c_int, ctypes.c_int,
+                         ctypes.POINTER(ctypes.c_double)]
 L.wsim_depth8.argtypes = [ctypes.c_float, fp]
 
 
-def run(name="c3", tile_step=1, mode=0, check=True):
+def run(name="c3", tile_step=1, mode=0, check=True, split=(0, 0)):
     s = pyoracle.load_setup(name)
     W, H = int(s["W"]), int(s["H"])
     lut = np.ascontiguousarray(pyoracle.load_lut(), np.uint32)
@@ -55,6 +56,7 @@ def run(name="c3", tile_step=1, mode=0, check=True):
         ref_m = np.ascontiguousarray(ref["minT"], np.float32)
         ref_i = np.ascontiguousarray(ref["index"], np.uint32)
     parts = [Stats() for _ in trows]
+    works = [np.zeros(3 * tw) for _ in trows]
 
     def work(k):
         ty = trows[k]
@@ -62,13 +64,14 @@ def run(name="c3", tile_step=1, mode=0, check=True):
                      root.ctypes.data_as(fp), child.ctypes.data_as(fp), lut.ctypes.data_as(up), d8.ctypes.data_as(fp),
                      ty * tw, (ty + 1) * tw, mode,
                      ref_m.ctypes.data_as(fp) if check else None, ref_i.ctypes.data_as(up) if check else None,
-                     ctypes.byref(parts[k]))
+                     ctypes.byref(parts[k]), split[0], split[1], works[k].ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
     with ThreadPoolExecutor(8) as ex:
         list(ex.map(work, range(len(trows))))
     tot = {f: np.sum([np.array(getattr(p, f)[:]) for p in parts], 0) for f in FIELDS + ["cone_tested", "cone_culled", "skip_exp", "skip_lost", "cache_hit"]}
     for f in TAIL:
         tot[f] = max(getattr(p, f) for p in parts) if f == "maxd" else sum(getattr(p, f) for p in parts)
     tot["scale"] = tile_step
+    tot["tile_work"] = np.concatenate(works).reshape(-1, 3)
     return tot
 
 

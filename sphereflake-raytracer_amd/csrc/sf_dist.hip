@@ -231,11 +231,11 @@ extern "C" int sf_dist_render(sf_dist* d)
         if (peers) {
             if (int rc = sfi_join(s.ctx)) return rc;
             SFD_HIP(d, hipEventRecord(s.start, st));
-        }
-        // rank 0: its bands in place on the context stream ...
-        if (int rc = sf_render(s.ctx, &p)) return rc;
-        if (peers) {
-            // ... while the peers' slabs land and unpack on the receive stream
+            // The receive is posted BEFORE rank 0's own trace: the persistent trace grid takes every wave slot, and a
+            // kernel dispatched behind it gets one only as the grid drains -- a one-wave kernel launched after a 1080p
+            // trace started 69 us into its 100-us span, one launched before it at once (scripts/slot_residency_probe.py,
+            // profiles/r5/slot_residency.txt). Posted after, the peers' ncclSend (and their next frames queued behind it
+            // on their slot streams) would wait for most of rank 0's trace.
             SFD_HIP(d, hipStreamWaitEvent(s.recv, s.start, 0));
             const size_t cnt = (size_t)d->stage_rows * W * words;   // 32-bit words per peer of the stage
             SFD_NCCL(d, ncclGroupStart());
@@ -246,6 +246,11 @@ extern "C" int sf_dist_render(sf_dist* d)
                                      (int)k, s.comm, s.recv));
             }
             SFD_NCCL(d, ncclGroupEnd());
+        }
+        // rank 0: its bands in place on the context stream ...
+        if (int rc = sf_render(s.ctx, &p)) return rc;
+        if (peers) {
+            // ... while the peers' slabs land and unpack on the receive stream
             if (int rc = sfi_unpack_slabs(s.ctx, s.stage, bytes, d->stage_rows, d->band_rows, n, 1, n - 1, s.recv, false))
                 return rc;
             SFD_HIP(d, hipEventRecord(s.done, s.recv));
