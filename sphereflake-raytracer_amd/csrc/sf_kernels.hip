@@ -2478,8 +2478,12 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y)
     return y;
 }
 // One twist in LDS: nb = the block after ob (both 624 words); 227 threads run the chains (words j, j + 227,
-// j + 454), word 623 after a barrier. Returns after a barrier (nb complete).
-__device__ __forceinline__ void mt_twist(const uint32_t* ob, uint32_t* nb)
+// j + 454) and thread 0 also word 623 = f(ob[623], nb[0], nb[396]): nb[396] is thread 169's second word, which
+// thread 0 forms again from ob (two more f) instead of waiting for it behind a barrier. Returns after ONE barrier
+// (nb complete), with this thread's words in w[0..2] (w[3]: word 623 on thread 0) for callers that store them
+// straight from registers. (Round 4: a barrier before word 623 and a second after it, and the callers re-read nb
+// from LDS for their global stores: sf_mt_raw 16.8 us for 33 twists, profiles/r4/final3.)
+__device__ __forceinline__ void mt_twist(const uint32_t* ob, uint32_t* nb, uint32_t w[4])
 {
     const uint32_t j = threadIdx.x;
     if (j < 227u) {
@@ -2487,10 +2491,19 @@ __device__ __forceinline__ void mt_twist(const uint32_t* ob, uint32_t* nb)
         nb[j] = a;
         const uint32_t b = mt_f(ob[j + 227u], ob[j + 228u], a);
         nb[j + 227u] = b;
-        if (j < 169u) nb[j + 454u] = mt_f(ob[j + 454u], ob[j + 455u], b);
+        w[0] = a;
+        w[1] = b;
+        if (j < 169u) {
+            w[2] = mt_f(ob[j + 454u], ob[j + 455u], b);
+            nb[j + 454u] = w[2];
+        }
+        if (j == 0u) {
+            const uint32_t a169 = mt_f(ob[169], ob[170], ob[566]);
+            const uint32_t b169 = mt_f(ob[396], ob[397], a169);   // nb[396]
+            w[3] = mt_f(ob[623], a, b169);
+            nb[623] = w[3];
+        }
     }
-    __syncthreads();
-    if (j == 0u) nb[623] = mt_f(ob[623], nb[0], nb[396]);
     __syncthreads();
 }
 }  // namespace
@@ -2507,9 +2520,17 @@ extern "C" __global__ __launch_bounds__(SF_MT_PAR_THREADS) void sf_mt_raw(const 
         raw[i] = state[i];
     }
     __syncthreads();
+    const uint32_t j = threadIdx.x;
     for (uint32_t b = 1; b < blocks; ++b) {
-        mt_twist(buf[(b - 1u) & 1u], buf[b & 1u]);
-        for (uint32_t i = threadIdx.x; i < 624u; i += SF_MT_PAR_THREADS) raw[b * 624u + i] = buf[b & 1u][i];
+        uint32_t w[4];
+        mt_twist(buf[(b - 1u) & 1u], buf[b & 1u], w);
+        uint32_t* rb = raw + b * 624u;   // this thread's new words, from registers
+        if (j < 227u) {
+            rb[j] = w[0];
+            rb[j + 227u] = w[1];
+            if (j < 169u) rb[j + 454u] = w[2];
+            if (j == 0u) rb[623] = w[3];
+        }
     }
 }
 
@@ -2608,10 +2629,17 @@ extern "C" __global__ __launch_bounds__(SF_MT_PAR_THREADS) void sf_mt_segments(c
     __syncthreads();
     uint32_t cur = 0, done = 0;
     while (done < cnt) {
-        mt_twist(buf[cur], buf[cur ^ 1u]);
+        uint32_t w[4];
+        mt_twist(buf[cur], buf[cur ^ 1u], w);
         cur ^= 1u;
         const uint32_t take = min(624u, cnt - done);
-        for (uint32_t k = tid; k < take; k += SF_MT_PAR_THREADS) out[r + s0 + done + k] = mt_temper(buf[cur][k]);
+        uint32_t* ob = out + r + s0 + done;   // this thread's new words, tempered from registers
+        if (tid < 227u) {
+            if (tid < take) ob[tid] = mt_temper(w[0]);
+            if (tid + 227u < take) ob[tid + 227u] = mt_temper(w[1]);
+            if (tid < 169u && tid + 454u < take) ob[tid + 454u] = mt_temper(w[2]);
+            if (tid == 0u && 623u < take) ob[623] = mt_temper(w[3]);
+        }
         done += take;
     }
     if (s0 + cnt == m) {   // the last draw of the batch: the state for the next batch
