@@ -467,13 +467,23 @@ __device__ __forceinline__ void stage_root(float* __restrict__ Lbase, const floa
 
 // PW: packet width of the semantics (0 per ray, 8 (AVX) or 4 (SSE) frame-less packets); PIPE: the latency
 // variant of the per-ray child loop (small frames, whose heaviest tiles' serial DFS is the frame)
-// This lane's column of the cooperative child build (see traverse): unit child frame bi = lane % 9 (lanes
-// 0..26; centre lanes 32 + i: child i), column bc. Loaded once per wave, before any tile loop: a global load
-// in every traversal would wait (vmcnt, in order on this ISA) for the previous tile's G-buffer stores.
+// Lane -> (child bi, column bc) of the cooperative child build: lanes 0..26 the axis columns of child lane % 9
+// (bc = lane / 9), lanes 27..63 centres (bc = 3) -- lanes 32 + i child i (the ballot lanes), lanes 27..31 child 8,
+// the rest repeats. (Lanes 27..31 build child 8 so that traverse_ray can store child 8's centre from the low lane
+// group: the centres are 16-B aligned, child i's x at bank 4 i mod 32, so child 8's and child 0's stores from one
+// lane group of ds_write_b32 were a 2-way bank conflict on every table store of every expansion.)
+__device__ __forceinline__ uint32_t build_child(uint32_t lane)
+{
+    return lane < 27u ? lane % 9u : lane < 32u ? 8u : (lane - 32u) % 9u;
+}
+
+// This lane's column of the cooperative child build (see build_child). Loaded once per wave, before any tile
+// loop: a global load in every traversal would wait (vmcnt, in order on this ISA) for the previous tile's
+// G-buffer stores.
 __device__ __forceinline__ float4 build_column(const DeviceConsts* __restrict__ K)
 {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 0u : (lane - 32u) % 9u;
+    const uint32_t bi = build_child(lane);
     const uint32_t bc = lane < 27u ? lane / 9u : 3u;
     const float4 r = make_float4(K->child[bi][4u * bc + 0u], K->child[bi][4u * bc + 1u], K->child[bi][4u * bc + 2u],
                                  K->child[bi][4u * bc + 3u]);
@@ -555,7 +565,7 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
     // region; the build's VALU cost is per wave either way. Lanes 32..40 hold the 9 child centres (read back by
     // v_readlane), and a ballot's per-child mask is bits 0..8 of its high word: one scalar AND (round 3 had the
     // centres on lanes 31..39, whose mask straddled the two words: a 64-bit shift and an AND per ballot).
-    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 0u : (lane - 32u) % 9u;
+    const uint32_t bi = build_child(lane);
     const uint32_t bc = lane < 27u ? lane / 9u : 3u;
     // The leaf-threshold skip bounds t from below for every ray. In packet semantics a lane with tca < 0
     // can also pass LOD through another lane's bounding hit (negative t, SIMD_AVX.h:254), which that
@@ -1088,10 +1098,14 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
     }
 
     // this lane's column of the cooperative child build (see traverse)
-    const uint32_t bi = lane < 27u ? lane % 9u : lane < 32u ? 0u : (lane - 32u) % 9u;
+    const uint32_t bi = build_child(lane);
     const uint32_t bc = lane < 27u ? lane / 9u : 3u;
     const float b[4] = { bcol.x, bcol.y, bcol.z, bcol.w };
-    const uint32_t slot = bc == 3u ? bi * 4u : SF_LDS_PLANE + bc * SF_LDS_COLS + bi * 3u;
+    // child 8's centre is stored by lanes 27..31; the high group's child-8 lanes store into the level's E words,
+    // which this traversal does not use, at a float offset of 2 mod 4 (the levels are 32-B aligned): store k then
+    // hits bank 2 + k mod 4, no centre store's 4 i + k
+    const uint32_t slot = bc == 3u ? (lane >= 32u && bi == 8u ? (uint32_t)SF_LDS_TABLE + 3u : bi * 4u)
+                                   : SF_LDS_PLANE + bc * SF_LDS_COLS + bi * 3u;
 
     uint32_t d = 0;      // uniform: depth of the open node
     uint32_t idxB = 1;   // uniform: the heap index of the open node's child 0 (9 n + 1)
