@@ -299,11 +299,12 @@ int sf_set_tile_trace(sf_ctx* ctx, int enable);
 int sf_get_tile_trace(sf_ctx* ctx, uint64_t* out, size_t n);   /* n >= 3 * tiles; synchronises */
 /* Heavy-first tile schedule: the work units the next persistent render takes in order (computed from
    the last render's per-tile costs, heaviest cost bucket first, stable within a bucket; a unit is
-   tile | part << 29: part 0 = the whole 8x8 tile, 1/2 = its pixel rows 0-3/4-7, 3..6 = its 4x4 quarters --
-   the tiles of the heaviest buckets may be traced as 2 or 4 part units, env SF_SPLIT_BUCKETS /
-   SF_SPLIT_PARTS) and those costs (shader cycles, one per tile; a split tile's slowest part, scaled).
-   Either pointer may be NULL; n >= 4 * tiles (order) or tiles (cost only). Returns the unit count,
-   0 when no order exists yet, or a negative SF_E*. Synchronises. */
+   tile | part << 29: part 0 = the whole 8x8 tile, 1/2 = its pixel rows 0-3/4-7, 3..6 = its 4x4 quarters,
+   or with env SF_SPLIT_PARTS=subtree its 4 subtree parts -- the tiles of the heaviest buckets may be traced
+   as 2 or 4 part units, env SF_SPLIT_BUCKETS / SF_SPLIT_PARTS) and those costs (shader cycles, one per tile
+   of the render the order was built for -- a band share's tiles when that render was one; a split tile's
+   slowest part, scaled). Either pointer may be NULL; n >= 4 * tiles (order) or tiles (cost only), tiles of
+   the whole frame. Returns the unit count, 0 when no order exists yet, or a negative SF_E*. Synchronises. */
 int sf_get_tile_order(sf_ctx* ctx, uint32_t* order, uint32_t* cost, size_t n);
 
 /* --- measurement ---------------------------------------------------------- */

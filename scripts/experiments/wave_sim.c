@@ -84,6 +84,7 @@ typedef struct {
     int cur_part;            /* part owning the current subtree (-1 above depth k) */
     double part_work[8];     /* this tile's work per part (child iterations + 6 per expansion) */
     double shared_work;      /* work above depth k (every part repeats it) */
+    int solo;                /* >= 0: trace only part `solo` of the subtree split (its own wave: no other part's hits) */
 } wsim_t;
 
 static int is_anc(uint64_t a, uint64_t n)
@@ -184,6 +185,8 @@ static void expand_node(wsim_t* S, const float* M, int d, uint64_t node, uint64_
     for (int k = 0; k < n; ++k) {
         const int c = order[k];
         const float* C = W[c] + 12;
+        if (S->solo >= 0 && S->split_p > 0 && dc == S->split_k &&
+            (int)((9 * node + 1 + (uint64_t)c) % (uint64_t)S->split_p) != S->solo) continue;
         st->iter[d]++;
         SIM_WORK(1.0);
         st->act[d] += __builtin_popcountll(A);
@@ -232,6 +235,7 @@ int wsim_tiles(uint32_t W, uint32_t H, const float o[3], const float tl[3], cons
     S.child = child; S.lut = lut; S.mode = mode; S.st = st;
     S.skip_k = 0x1p-9f; S.skip_f = 4.0f;
     S.part = (mode >> 8) & 7;
+    S.solo = getenv("SOLO") ? atoi(getenv("SOLO")) : -1;
     if (getenv("SKIP_K")) S.skip_k = strtof(getenv("SKIP_K"), NULL);
     if (getenv("SKIP_F")) S.skip_f = strtof(getenv("SKIP_F"), NULL);
     for (int d = 0; d < NST; ++d) {

@@ -23,6 +23,7 @@ extern "C" __global__ void sf_trace_wave1(FrameArgs a, uint32_t* overflow_list, 
 extern "C" __global__ void sf_trace_wave2(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
 extern "C" __global__ void sf_trace_wave4(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
 extern "C" __global__ void sf_trace_queue1(FrameArgs a);
+extern "C" __global__ void sf_trace_queue1s(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2(FrameArgs a);
 extern "C" __global__ void sf_trace_queue4(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2p(FrameArgs a);
@@ -31,7 +32,7 @@ extern "C" __global__ void sf_order_scan(uint32_t* chunk_cnt, uint32_t nc, uint3
                                          uint32_t split_buckets, uint32_t parts, uint32_t spare, uint32_t waves,
                                          uint32_t prio_buckets,
                                          uint32_t* chunk_off, uint32_t* order_meta, const uint32_t* fuse_cost,
-                                         uint32_t* fuse_order);
+                                         uint32_t* fuse_order, uint32_t split_cap);
 extern "C" __global__ void sf_order_scatter(const uint32_t* cost, uint32_t n, uint32_t* chunk_cnt,
                                             const uint32_t* chunk_off, const uint32_t* order_meta, uint32_t* order,
                                             uint32_t* rank_out);
@@ -227,6 +228,11 @@ struct sf_ctx {
     uint32_t split_parts = 4;          // env SF_SPLIT_PARTS = 2 (halves) | 4 (quarters); 640x360: 0.122 -> 0.097 ms with quarters
     uint32_t* part_cost = nullptr;     // per tile: slowest part of a split tile (zeroed, reset by the last part)
     uint32_t* part_done = nullptr;     // per tile: parts finished (zeroed, reset by the last part)
+    // env SF_SPLIT_PARTS=subtree: split tiles traced as 4 subtree parts (SF_FLAG_SUBTREE) instead of pixel quarters;
+    // part_rec holds their per-pixel results (SF_SPLIT_CAP split slots), split_depth_env the depth they divide
+    // (0: the view's deepest LOD-passable depth - 2)
+    uint64_t* part_rec = nullptr;
+    uint32_t split_depth_env = 0;
     uint32_t order_n = 0;              // tile count the current tile_order is a permutation of (0: none)
     // Stream ordering across calls: every call that enqueues work on the context's buffers first joins
     // the stream of the previous such call (ctx_join), so renders, frame-less batches, post-processing
@@ -367,6 +373,7 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->order_meta);
     (void)hipFree(c->part_cost);
     (void)hipFree(c->part_done);
+    (void)hipFree(c->part_rec);
     (void)hipFree(c->noise);
     (void)hipFree(c->ao);
     (void)hipFree(c->blur_h);
@@ -510,7 +517,12 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
         c->split_buckets = std::strcmp(ev, "model") == 0 ? SF_SPLIT_MODEL
                          : std::strcmp(ev, "auto") == 0 ? SF_SPLIT_AUTO : (uint32_t)std::atoi(ev);
     if (std::getenv("SF_SPLIT_BUCKETS")) c->split_env = true;
-    if (const char* ev = std::getenv("SF_SPLIT_PARTS")) c->split_parts = std::atoi(ev) == 4 ? 4u : 2u;
+    bool subtree = false;
+    if (const char* ev = std::getenv("SF_SPLIT_PARTS")) {
+        subtree = std::strcmp(ev, "subtree") == 0;
+        c->split_parts = (subtree || std::atoi(ev) == 4) ? 4u : 2u;
+    }
+    if (const char* ev = std::getenv("SF_SPLIT_DEPTH")) c->split_depth_env = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_MAX_BLOCKS")) c->max_blocks = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_PRIO_BUCKETS")) c->prio_buckets = (uint32_t)std::atoi(ev);
     if (const char* ev = std::getenv("SF_FLAGS")) c->flags = (uint32_t)std::strtoul(ev, nullptr, 0);
@@ -554,6 +566,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if ((e = hipMalloc(&c->part_done, ntiles * 4)) != hipSuccess) return fail(e);
     if ((e = hipMemsetAsync(c->part_cost, 0, ntiles * 4, c->stream)) != hipSuccess) return fail(e);
     if ((e = hipMemsetAsync(c->part_done, 0, ntiles * 4, c->stream)) != hipSuccess) return fail(e);
+    if (subtree && (e = hipMalloc(&c->part_rec, (size_t)SF_SPLIT_CAP * 4u * 192u * 8u)) != hipSuccess) return fail(e);
     const size_t nchunks = (ntiles + 63) / 64;
     if ((e = hipMalloc(&c->chunk_cnt, nchunks * SF_ORDER_BUCKETS * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->chunk_off, nchunks * SF_ORDER_BUCKETS * 4)) != hipSuccess) return fail(e);
@@ -813,6 +826,11 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 a.chunk_cnt = rebuild ? c->chunk_cnt : nullptr;
                 a.part_cost = c->part_cost;
                 a.part_done = c->part_done;
+                if (c->part_rec && split_buckets != 0u && wpb == 1u) {   // split tiles are traced as subtree parts
+                    a.part_rec = c->part_rec;
+                    a.split_depth = c->split_depth_env ? c->split_depth_env : (levels > 3u ? levels - 3u : 1u);
+                    a.flags |= SF_FLAG_SUBTREE;
+                }
                 a.tile_order = c->order_n == ntiles ? c->tile_order : nullptr;   // ordered by ctx_join
                 a.order_meta = c->order_meta;
             }
@@ -826,7 +844,8 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             // tiles' serial DFS is the frame, and the pipelined child loop shortens it (640x360 -4 %); full
             // grids are throughput-bound, where it costs more instructions than it hides (1080p +1.7 %)
             const bool pipe = c->pipe >= 0 ? c->pipe == 1 : small;
-            if (wpb == 1) hipLaunchKernelGGL(sf_trace_queue1, grid, block, lds, s, a);
+            if (wpb == 1 && (a.flags & SF_FLAG_SUBTREE)) hipLaunchKernelGGL(sf_trace_queue1s, grid, block, lds, s, a);
+            else if (wpb == 1) hipLaunchKernelGGL(sf_trace_queue1, grid, block, lds, s, a);
             else if (wpb == 2 && pipe) hipLaunchKernelGGL(sf_trace_queue2p, grid, block, 2 * lds, s, a);
             else if (wpb == 2 && c->compact) hipLaunchKernelGGL(sf_trace_queue2c, grid, block, 2 * lds, s, a);
             else if (wpb == 2) hipLaunchKernelGGL(sf_trace_queue2, grid, block, 2 * lds, s, a);
@@ -847,7 +866,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, c->chunk_cnt, nc, ntiles,
                                    split_buckets, c->split_parts, spare, waves, c->prio_buckets, c->chunk_off,
                                    c->order_meta, fuse ? (const uint32_t*)c->tile_cost : nullptr,
-                                   fuse ? c->tile_order : nullptr);
+                                   fuse ? c->tile_order : nullptr, c->part_rec ? SF_SPLIT_CAP : 0xffffffffu);
                 SF_HIP(c, hipGetLastError());
                 if (!fuse) {
                     hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost, ntiles,
@@ -1281,7 +1300,7 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
                                    c->bin_chunk_cnt);
                 hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, c->bin_chunk_cnt, nc, nbins,
                                    0u, 2u, 0u, 0u, 0u, c->bin_chunk_off, c->bin_meta, (const uint32_t*)nullptr,
-                                   (uint32_t*)nullptr);
+                                   (uint32_t*)nullptr, 0xffffffffu);
                 hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->bin_cost, nbins,
                                    c->bin_chunk_cnt, (const uint32_t*)c->bin_chunk_off, (const uint32_t*)c->bin_meta,
                                    c->bin_order, c->bin_rank);
@@ -1591,12 +1610,12 @@ int sf_get_tile_order(sf_ctx* c, uint32_t* order, uint32_t* cost, size_t n)
     const size_t ntiles = (size_t)((c->W + 7) / 8) * ((c->H + 7) / 8);
     if (n < ntiles || (!order && !cost)) return SF_EINVAL;
     if (int rc_ = ctx_drain(c)) return rc_;
-    if (c->order_n != ntiles) return 0;
+    if (c->order_n == 0u) return 0;   // (a band share's order covers its own c->order_n tiles)
     uint32_t meta[2];
     SF_HIP(c, hipMemcpy(meta, c->order_meta, sizeof(meta), hipMemcpyDeviceToHost));
     if (order && n < meta[0]) return SF_EINVAL;
     if (order) SF_HIP(c, hipMemcpy(order, c->tile_order, (size_t)meta[0] * 4, hipMemcpyDeviceToHost));
-    if (cost) SF_HIP(c, hipMemcpy(cost, c->tile_cost, ntiles * 4, hipMemcpyDeviceToHost));
+    if (cost) SF_HIP(c, hipMemcpy(cost, c->tile_cost, (size_t)c->order_n * 4, hipMemcpyDeviceToHost));
     return (int)meta[0];
 }
 

@@ -92,6 +92,11 @@
 // (kernel-internal) the index-order re-trace pass of such a tile: its writes replace the first pass's, its cost is
 // not recorded
 #define SF_FLAG_REDO_PASS 0x1000u
+// set by the host (env SF_SPLIT_PARTS=subtree): the 4 part units of a split tile are SUBTREE parts -- each traces the
+// whole 8x8 tile but enters, below FrameArgs.split_depth - 1, only the depth-split_depth nodes whose heap index is its
+// part number mod 4; the part that finishes last merges the 4 per-pixel results (nearest, the reference's tie rule)
+// and writes the tile (trace_tile). Quarter units (pixel parts) otherwise.
+#define SF_FLAG_SUBTREE 0x2000u
 
 struct DepthTables {
     float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)
@@ -165,6 +170,9 @@ struct FrameArgs {
     uint64_t* clock_probe;            // measurement (NULL = off): the first wave of blocks 0..SF_CLOCK_WAVES-1
                                       // writes {s_memtime, s_memrealtime} at its start and at its end
     uint32_t tpb_magic;               // floor((2^32 - 1) / tiles_per_band) (tile_of)
+    uint64_t* part_rec;               // SF_FLAG_SUBTREE: per split slot x part, 3 x 64 u64 -- each lane's
+                                      // {minT | cx}, {cy | cz}, {index | depth} (merged by the last part)
+    uint32_t split_depth;             // SF_FLAG_SUBTREE: depth of the nodes the parts divide (>= 1)
 };
 #define SF_CLOCK_WAVES 8u             // live shader clock samples per timed render (one per XCD group)
 
@@ -243,6 +251,8 @@ struct PostArgs {
 // env SF_SPLIT_BUCKETS=model: split the buckets a makespan model of the last render's costs says shorten the
 // frame (sf_order_scan) -- also on full grids, where the heaviest tile exceeds the slots' fair share
 #define SF_SPLIT_MODEL 0xfffffffeu
+// split tiles per render at most (sf_order_scan; the subtree parts' records are per split slot)
+#define SF_SPLIT_CAP 4096u
 // Parts a split tile is traced as (env SF_SPLIT_PARTS): 2 halves or 4 quarters. A split tile's cost for
 // the next schedule is its slowest part's, scaled to whole-tile terms (measured: the slowest half takes
 // ~0.68 of the whole tile, the slowest quarter ~0.5).

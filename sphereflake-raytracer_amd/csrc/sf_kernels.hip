@@ -1042,12 +1042,23 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
 // push, no load at the pop). A node keeps on the VGPR stack its untested children (the cone-culled mask,
 // front children first, as before) instead of its pending ones, and its visiting lanes as one bit per level
 // (`actbits`).
-template <bool PIPE = false, bool COMPACT = false>
+// Entry-order mask (bits c and 9 + c, see traverse_ray) of the children c of a node whose child 0 has heap index
+// idxB that belong to subtree part q: (idxB + c) mod 4 == q.
+__device__ __forceinline__ uint32_t split_mask(uint32_t q, uint32_t idxB)
+{
+    const uint32_t m9 = (0x111u << ((q - idxB) & 3u)) & 0x1ffu;
+    return m9 | (m9 << 9);
+}
+
+// SPLIT: a subtree part unit (SF_FLAG_SUBTREE): of the nodes at depth split_depth, only those whose heap index is
+// split_q mod 4 are entered (their own sphere and their subtree); everything above is traced as for the whole tile.
+template <bool PIPE = false, bool COMPACT = false, bool SPLIT = false>
 __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K, const float* root, float* __restrict__ Lbase,
                                              const float4 bcol, uint32_t levels, float dx, float dy, float dz, bool valid,
                                              HitState& h, int32_t& maxd, uint32_t& status, uint32_t K_flags,
                                              uint64_t* phase_sums = nullptr, uint32_t axl = 36u,
-                                             uint64_t* tile_counts = nullptr)
+                                             uint64_t* tile_counts = nullptr, uint32_t split_q = 0u,
+                                             uint32_t split_depth = 0u)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const TraverseLds L{ Lbase };
@@ -1261,6 +1272,9 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u)))))
             C = expand(pc, L.root() + 4u, 4u, 0u, actv, leafN, tcur, kofs, readlane_f(tca, axl));
         else SF_COUNT(4, 1);
+        if constexpr (SPLIT) {
+            if (split_depth == 1u) C &= split_mask(split_q, 1u);
+        }
     }
 
     // (the scalar unit is shared by the CU's four SIMDs and measured ~3x a VALU op per instruction here: the child
@@ -1350,6 +1364,9 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             tcur += SF_LDS_LEVEL;
             kofs += 1u << 5;
             C = expand(pc, col, SF_LDS_COLS, d, avx, leafN, tcur, kofs, readlane_f(tca, axl));
+            if constexpr (SPLIT) {   // (the children are at depth d + 1)
+                if (d + 1u == split_depth) C &= split_mask(split_q, idxB);
+            }
             R2c = depth_consts_at(K, kofs).x;
             if (COMPACT && C != 0u) {
                 // ---- Active-ray compaction of sparse nodes (north star: "wavefront ballot / prefix-sum active-ray
@@ -1600,17 +1617,38 @@ struct NoPrefetch {
 // `pre` runs right after the traversal, before the tile's shading and stores: the persistent kernel takes
 // its next queue ticket there, so the atomic's round trip overlaps the shading instead of following the
 // G-buffer stores (whose completion a later wait would otherwise include: vmcnt counts in order).
-template <bool FIXUP, bool PIPE = false, class Prefetch = NoPrefetch, bool COMPACT = false>
+// Heap index a is n or an ancestor of n (child i of node m is 9 m + 1 + i; indices of depth <= 10, whose heap
+// indices fit the 32 bits HitState keeps).
+__device__ __forceinline__ bool heap_ancestor(uint32_t a, uint32_t n)
+{
+    while (n > a) n = (n - 1u) / 9u;
+    return n == a;
+}
+
+// Subtree part records (SF_FLAG_SUBTREE): part q of split slot s at part_rec + (4 s + q) x 192 u64, three 64-lane
+// planes. Stored and loaded with agent scope (sc1: past the writer's and the reader's caches), so that the part that
+// adds last to the tile's counter -- after every part's stores have completed (s_waitcnt vmcnt(0)) -- reads them.
+__device__ __forceinline__ uint64_t* part_record(const FrameArgs& a, uint32_t slot, uint32_t q)
+{
+    return a.part_rec + (size_t)(slot * 4u + q) * 192u;
+}
+
+template <bool FIXUP, bool PIPE = false, class Prefetch = NoPrefetch, bool COMPACT = false, bool SPLIT = false>
 __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __restrict__ L, const float4 bcol, uint32_t tile,
                                                 uint32_t levels, uint32_t* overflow_list, uint32_t* overflow_count,
-                                                uint32_t part = 0u, const Prefetch& pre = Prefetch(), uint32_t fl = ~0u)
+                                                uint32_t part = 0u, const Prefetch& pre = Prefetch(), uint32_t fl = ~0u,
+                                                uint32_t slot = 0u)
 {
     // (fl: the launch's flags, with SF_FLAG_REDO_PASS | SF_FLAG_NO_FRONT_FIRST on a re-trace pass; ~0u: flags)
+    // (slot: a subtree part unit's split slot -- its position in the unit order / 4)
     const uint32_t flags = fl == ~0u ? a.flags : fl;
     const DeviceConsts* __restrict__ K = a.consts;
     const uint32_t lane = threadIdx.x & 63u;
     if (flags & SF_FLAG_DIAG_HALF) part = (flags & SF_FLAG_DIAG_HALF_SEL) ? 2u : 1u;
-    const Tile t = tile_of(a, tile, lane, part);
+    // a subtree part unit: all 64 pixels, the depth-split_depth subtrees of heap index q mod 4 (SF_FLAG_SUBTREE)
+    // (only the SPLIT kernel, sf_trace_queue1s, carries the split logic)
+    const bool sub = SPLIT && !FIXUP && (flags & SF_FLAG_SUBTREE) != 0u && part >= SF_PART_QUARTER0;
+    const Tile t = tile_of(a, tile, lane, sub ? 0u : part);
     const uint64_t t_start = a.tile_trace ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const uint64_t c_start = (!FIXUP && a.tile_cost) ? __builtin_amdgcn_s_memtime() : 0ull;
     float dx, dy, dz;
@@ -1624,9 +1662,15 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
     // that order flags the tile like an overflow, and the fixup re-traces it in index order -- the reference's
     // tie rule (see traverse). The fixup kernel always traces in index order.
 #ifndef SF_OLD_TRAVERSE
-    traverse_ray<PIPE, COMPACT>(K, a.root, L, bcol, levels, dx, dy, dz, t.valid, h, maxd, status,
-                       FIXUP ? (flags | SF_FLAG_NO_FRONT_FIRST) : flags,
-                       FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
+    if constexpr (SPLIT)   // one traversal: the split depth never matches on whole units
+        traverse_ray<PIPE, COMPACT, true>(K, a.root, L, bcol, levels, dx, dy, dz, t.valid, h, maxd, status,
+                                          FIXUP ? (flags | SF_FLAG_NO_FRONT_FIRST) : flags,
+                                          FIXUP ? nullptr : a.phase_sums, part_axis_lane(sub ? 0u : part), &tile_counts,
+                                          sub ? part - SF_PART_QUARTER0 : 0u, sub ? a.split_depth : 0xffffffffu);
+    else
+        traverse_ray<PIPE, COMPACT>(K, a.root, L, bcol, levels, dx, dy, dz, t.valid, h, maxd, status,
+                                    FIXUP ? (flags | SF_FLAG_NO_FRONT_FIRST) : flags,
+                                    FIXUP ? nullptr : a.phase_sums, part_axis_lane(part), &tile_counts);
 #else
     traverse<0, PIPE>(K, a.root, L, bcol, levels, dx, dy, dz, t.valid, h, maxd, status,
                       FIXUP ? (flags | SF_FLAG_NO_FRONT_FIRST) : flags,
@@ -1634,6 +1678,79 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
 #endif
     if (!FIXUP && (flags & (SF_FLAG_DIAG_FORCE_RETRACE | SF_FLAG_REDO_PASS)) == SF_FLAG_DIAG_FORCE_RETRACE)
         status |= SF_STATUS_TIE;
+    bool merger = true;   // this wave writes the tile (a subtree part: only the part that merges)
+    if (sub) {
+        // ---- subtree part: publish this part's per-pixel result; the part that finishes last merges the four
+        // and goes on as a whole tile would (re-trace decision, scheduling cost, G-buffer write)
+        const bool rec_cost = a.tile_cost != nullptr && !(flags & SF_FLAG_DIAG_HALF);
+        if (rec_cost) {   // the slowest part, in whole-tile terms (x 2, as for quarters)
+            const uint64_t cyc = __builtin_amdgcn_s_memtime() - c_start;
+            wave_atomic_max(a.part_cost + tile, cyc > 0x7fffffffull ? 0xffffffffu : 2u * (uint32_t)cyc);
+        }
+        const uint32_t q = part - SF_PART_QUARTER0;
+        uint64_t* const R = part_record(a, slot, q);
+        __hip_atomic_store(R + lane, ((uint64_t)__float_as_uint(h.cx) << 32) | __float_as_uint(h.minT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(R + 64u + lane, ((uint64_t)__float_as_uint(h.cz) << 32) | __float_as_uint(h.cy),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(R + 128u + lane, ((uint64_t)(uint32_t)h.depth << 32) | h.index,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // counter: parts done (low byte), parts that flagged an overflow (byte 1), a tie (byte 2)
+        const uint32_t add = 1u | ((status & SF_STATUS_OVERFLOW) ? 0x100u : 0u) | ((status & SF_STATUS_TIE) ? 0x10000u : 0u);
+        const uint32_t st0 = status;
+        const uint32_t old = wave_fetch_add(a.part_done + tile, add);
+        merger = (old & 0xffu) == 3u;   // the last part; the others are done with this tile (no write, no flag)
+        status = 0u;
+      if (merger) {
+        a.part_done[tile] = 0u;   // for the next render (uniform value and address)
+        // merge: per pixel the nearest sphere over the parts. An exact tie between two parts' spheres is the
+        // reference's ancestor rule where one is the other's ancestor (a node's sphere is tested before its
+        // subtree, and a tie with an ancestor is accepted, self_test) -- the parts share every node above
+        // split_depth, so each part's own result already holds it against the shared spheres -- and otherwise a
+        // tie the index-order re-trace resolves, as within a traversal.
+        bool tie = false;
+#pragma unroll 1
+        for (uint32_t p = 0u; p < 4u; ++p) {   // (one part at a time: few registers live)
+            if (p == q) continue;
+            const uint64_t* const Rp = part_record(a, slot, p);
+            const uint64_t r0 = __hip_atomic_load(Rp + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t r1 = __hip_atomic_load(Rp + 64u + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t r2 = __hip_atomic_load(Rp + 128u + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const float m = __uint_as_float((uint32_t)r0);
+            const uint32_t idx = (uint32_t)r2;
+            const int32_t dep = (int32_t)(uint32_t)(r2 >> 32);
+            bool take = m < h.minT;
+            if (m == h.minT && idx != h.index) {
+                const bool both = h.depth >= 0 && dep >= 0 && h.depth <= 10 && dep <= 10;
+                if (both && heap_ancestor(h.index, idx)) take = true;          // the deeper sphere wins the tie
+                else if (!(both && heap_ancestor(idx, h.index))) tie = true;   // unrelated spheres: re-trace
+            }
+            if (take) {
+                h.minT = m;
+                h.cx = __uint_as_float((uint32_t)(r0 >> 32));
+                h.cy = __uint_as_float((uint32_t)r1);
+                h.cz = __uint_as_float((uint32_t)(r1 >> 32));
+                h.index = idx;
+                h.depth = dep;
+            }
+        }
+        h.hit = h.depth >= 0;
+        status = st0;
+        if ((old & 0xff00u) != 0u) status |= SF_STATUS_OVERFLOW;
+        if ((old & 0xff0000u) != 0u || wave_ballot(tie) != 0ull) status |= SF_STATUS_TIE;
+        if (rec_cost) {
+            const uint32_t cost = __builtin_amdgcn_readfirstlane(
+                (int)__hip_atomic_load(a.part_cost + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            a.part_cost[tile] = 0u;
+            a.tile_cost[tile] = cost;
+            if (a.chunk_cnt) {
+                const uint32_t cs = __builtin_amdgcn_readfirstlane((tile >> 6) * SF_ORDER_BUCKETS + cost_bucket(cost));
+                wave_atomic_inc_nowait(a.chunk_cnt + cs);
+            }
+        }
+      }
+    }
     const bool overflowed = status != 0u;
     // a tie under the front-first order with the levels proven (SF_FLAG_TIE_INLINE): this wave re-traces the unit
     // in index order right after (trace_queue_body, told by `pre`); anything else flagged goes to the overflow list
@@ -1657,7 +1774,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
 #endif
     }
 
-    if (!FIXUP && a.tile_cost && !(flags & (SF_FLAG_DIAG_HALF | SF_FLAG_REDO_PASS))) {
+    if (!FIXUP && !sub && a.tile_cost && !(flags & (SF_FLAG_DIAG_HALF | SF_FLAG_REDO_PASS))) {
         // scheduling hint for the next render (sf_order_scan / sf_order_scatter); uniform values.
         const uint64_t cyc = __builtin_amdgcn_s_memtime() - c_start;
         uint32_t cost = cyc > 0xffffffffull ? 0xffffffffu : (uint32_t)cyc;
@@ -1689,7 +1806,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
         const uint32_t slot = wave_fetch_add(overflow_count, 1u);
         overflow_list[slot] = tile;   // uniform value and address
     }
-    if (t.valid) write_pixel(a, t, dx, dy, dz, h, K->lut);
+    if (t.valid && merger) write_pixel(a, t, dx, dy, dz, h, K->lut);
 
     // stats: max depth reached, closest sphere distance (Sphereflake.h:157-160, Sphereflake.cpp:197-200)
     TileStats st;
@@ -1750,7 +1867,7 @@ extern "C" __global__ __launch_bounds__(256) void sf_trace_wave4(FrameArgs a, ui
 // atomic queue until it runs dry. Dynamic balancing: tile costs vary ~100x (sky vs. deep flake),
 // and the in-order workgroup dispatcher otherwise idles CUs behind long tiles. counters: [0,1]
 // overflow counts, [2,3] tile queues, alternating per render (this render zeroes the next one's).
-template <int WAVES, bool PIPE = false, bool COMPACT = false>
+template <int WAVES, bool PIPE = false, bool COMPACT = false, bool SPLIT = false>
 __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 {
     extern __shared__ float lds[];
@@ -1858,14 +1975,16 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
         // the next unit's ticket, taken when this tile's traversal ends (see trace_tile)
         // (an agent-coherent load of the queue word before the atomic, to skip dry queues, made the frame
         // 1.7x slower: it contends with the atomics on the line)
+        // (a subtree part's re-trace is its whole tile's: the part that merged the tile takes it, as part 0)
         auto ticket = [&](bool retrace) {
-            first = retrace ? (0x80000000u | (part << SF_UNIT_PRIO_SHIFT) | t)
+            const uint32_t rp = ((at.flags & SF_FLAG_SUBTREE) && part >= SF_PART_QUARTER0) ? 0u : part;
+            first = retrace ? (0x80000000u | (rp << SF_UNIT_PRIO_SHIFT) | t)
                             : nwaves + wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u) * nq + k;   // uniform
         };
-        const TileStats st = trace_tile<false, PIPE, decltype(ticket), COMPACT>(at, L, bcol, t, at.max_depth, at.overflow_list,
+        const TileStats st = trace_tile<false, PIPE, decltype(ticket), COMPACT, SPLIT>(at, L, bcol, t, at.max_depth, at.overflow_list,
                                                                                at.counters + at.parity, part,
                                                ticket, again ? (at.flags | SF_FLAG_NO_FRONT_FIRST | SF_FLAG_REDO_PASS)
-                                                             : at.flags);
+                                                             : at.flags, g >> 2);
         if ((at.flags & SF_FLAG_DIAG_UNITS) && at.tile_trace && (g >> 31) == 0u) {   // diagnostics only (uniform words)
             // (slot g: the unit's position in the order. A re-trace pass -- its ticket word carries bit 31 -- records
             // nothing: its word is no position, and the slot of the unit it repeats already holds that unit's record)
@@ -1909,6 +2028,11 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue1(FrameArgs a)
 {
     trace_queue_body<1>(a);
+}
+// the same with subtree-split units (SF_FLAG_SUBTREE): renders whose unit order holds split tiles
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue1s(FrameArgs a)
+{
+    trace_queue_body<1, false, false, true>(a);
 }
 extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue2(FrameArgs a)
 {
@@ -1977,7 +2101,7 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(uint32_t* __res
                                                                    uint32_t* __restrict__ chunk_off,
                                                                    uint32_t* __restrict__ order_meta,
                                                                    const uint32_t* __restrict__ fuse_cost,
-                                                                   uint32_t* __restrict__ fuse_order)
+                                                                   uint32_t* __restrict__ fuse_order, uint32_t split_cap)
 {
     // fuse_cost / fuse_order not NULL: this workgroup also does sf_order_scatter's work afterwards (its 16 waves
     // over the chunks), one launch instead of two -- for frames of few chunks, where the second launch's host
@@ -2072,6 +2196,12 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(uint32_t* __res
             // then drop buckets from the bottom of the range while more than an eighth of the tiles split
             const uint64_t ok = __builtin_amdgcn_ballot_w64((int)l >= b0 && l < SF_ORDER_BUCKETS && 8u * S <= n_tiles);
             bs = ok ? __builtin_ctzll(ok) : (int)SF_ORDER_BUCKETS;
+        }
+        // at most split_cap split tiles (the subtree parts' records are per split slot): S(l) is non-increasing
+        {
+            const uint64_t capok = __builtin_amdgcn_ballot_w64(l < SF_ORDER_BUCKETS && S <= split_cap);
+            const int bcap = capok ? __builtin_ctzll(capok) : (int)SF_ORDER_BUCKETS;
+            if (bs < bcap) bs = bcap;
         }
         // the top `prio_buckets` occupied cost buckets run at raised wave priority next render (their
         // serial DFS is the frame's critical path)

@@ -30,14 +30,21 @@ def random_view(rng, k):
     return W, H, K, cam
 
 
-@pytest.mark.parametrize("variant", ["avx", "sse", "compact"])
+@pytest.mark.parametrize("variant", ["avx", "sse", "compact", "subtree", "subtree_d2"])
 @pytest.mark.parametrize("seed", range(16))
 def test_random_view_bit_exact(seed, variant, monkeypatch):
     """("compact": the AVX variant traced by the opt-in active-ray compaction kernel, SF_COMPACT=1 with the
-    throughput variant forced, SF_PIPE=0, since these small frames would take the latency variant.)"""
+    throughput variant forced, SF_PIPE=0, since these small frames would take the latency variant. "subtree":
+    the AVX variant with the split tiles traced as subtree parts, SF_SPLIT_PARTS=subtree, at the default split
+    depth and at depth 2 -- these frames leave idle waves, so renders 2 and 3 split their heaviest tiles.)"""
     if variant == "compact":
         monkeypatch.setenv("SF_COMPACT", "1")
         monkeypatch.setenv("SF_PIPE", "0")
+        variant = "avx"
+    elif variant.startswith("subtree"):
+        monkeypatch.setenv("SF_SPLIT_PARTS", "subtree")
+        if variant == "subtree_d2":
+            monkeypatch.setenv("SF_SPLIT_DEPTH", "2")
         variant = "avx"
     rng = np.random.default_rng(1000 + seed)
     W, H, K, cam = random_view(rng, seed)
