@@ -214,6 +214,10 @@ struct sf_ctx {
     int32_t* h_depth = nullptr;
     int32_t* h_stats = nullptr;        // pinned: the stats words, copied on the stream by sf_synchronize
     bool stats_dirty = true;           // work was enqueued since the last sf_synchronize checked the stats
+    // the stats' unresolved word may have changed since that check: every enqueuing call but a persistent trace
+    // with its levels proven and its ties re-traced inline, which adds 0 to it (its max-depth / closest words are
+    // read by sf_get_stats, not here) -- after only such traces sf_synchronize needs no stats copy, just the wait
+    bool stats_unknown = true;
     int32_t unresolved = 0;            // the stats' unresolved-tile count at the last check
     uint64_t* tile_trace = nullptr;    // diagnostics: per tile {start, end, hw id}
     // Heavy-first tile scheduling: every persistent render records per-tile cycles; sf_tile_order
@@ -292,6 +296,7 @@ struct sf_ctx {
 static int ctx_join(sf_ctx* c, hipStream_t s)
 {
     c->stats_dirty = true;   // (every call that enqueues work joins first)
+    c->stats_unknown = true;   // (a trace that cannot change the unresolved word restores it, launch())
     hipStream_t last = c->last_stream ? c->last_stream : c->stream;
     if (s == last) return SF_OK;
     if (last == c->stream) SF_HIP(c, hipEventRecord(c->join_ev, c->stream));   // (the context's own stream)
@@ -686,10 +691,12 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
     hipStream_t s = p.stream ? (hipStream_t)p.stream : c->stream;
     DevGuard g(c->device);
     if (tile_rows == 0) return SF_OK;
+    const bool unknown_before = c->stats_unknown;
     if (int rc = ctx_join(c, s)) return rc;
     StreamMark mark_(c, s);
 
     FrameArgs a = frame_args(c);
+    bool unresolved_safe = false;   // this launch adds nothing to the unresolved word (see sf_ctx::stats_unknown)
     a.tile_rows = tile_rows;
     a.tiles_per_band = tpb;
     a.tpb_magic = 0xffffffffu / tpb;
@@ -887,6 +894,8 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
         // levels proven sufficient (persistent kernel) only an exact tie under the front-first child order can
         // flag a tile -- never seen on the BASELINE views --: its own wave re-traces it (tie_inline), or with
         // SF_TIE_INLINE=0 the fixup's small grid.
+        // (no fixup after the trace: nothing is counted as unresolved)
+        unresolved_safe = bounded && c->persistent && !(front_first && !tie_inline);
         if (!(bounded && c->persistent) || (front_first && !tie_inline)) {
             const size_t lds_fix = (size_t)SF_LDS_WAVE_FLOATS(SF_MAX_DEPTH_LIMIT) * 4;
             const uint32_t fb = (bounded && c->persistent) ? 8u : 4u * (uint32_t)c->fixup_blocks;
@@ -904,6 +913,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
         rows += y1 - y0;
     }
     c->rays += (int64_t)rows * c->W;
+    if (unresolved_safe) c->stats_unknown = unknown_before;
     return SF_OK;
 }
 
@@ -1379,21 +1389,22 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
 // The stats words ride the stream in a small copy to pinned memory, queued behind the context's work, so the host
 // waits once (a synchronous hipMemcpy after the drain was a second round trip, ~10-20 us per call: per slot of a
 // dist, at the end of every timed loop and every lone frame); a context with nothing enqueued since the last call
-// only drains.
+// only drains, and so does one whose work since then was only persistent traces that cannot add to the unresolved
+// word (round 5: the copy was a blit dispatch of ~4 us behind every lone frame's trace, plus its launch gap).
 int sf_synchronize(sf_ctx* c)
 {
     if (!c) return SF_EINVAL;
     DevGuard g(c->device);
-    const bool check = c->stats_dirty;
+    // (after only traces that cannot change the unresolved word, the last check's value stands: no copy)
+    const bool check = c->stats_dirty && c->stats_unknown;
     if (check) {
         if (int rc_ = ctx_join(c, c->stream)) return rc_;
         SF_HIP(c, hipMemcpyAsync(c->h_stats, c->stats, 12, hipMemcpyDeviceToHost, c->stream));
     }
     if (int rc_ = ctx_drain(c)) return rc_;
-    if (check) {
-        c->stats_dirty = false;
-        c->unresolved = ((volatile int32_t*)c->h_stats)[2];
-    }
+    c->stats_dirty = false;
+    c->stats_unknown = false;
+    if (check) c->unresolved = ((volatile int32_t*)c->h_stats)[2];
     if (c->unresolved != 0) return SF_EDEPTH;
     return SF_OK;
 }
