@@ -44,7 +44,7 @@ extern "C" __global__ void sf_band_unpack(FrameArgs a, const float4* stage, uint
 extern "C" __global__ void sf_node_table(FrameArgs a, float4* table, uint32_t nodes);
 extern "C" __global__ void sf_slab_unpack4(FrameArgs a, const uint32_t* stage, const float4* table, uint32_t table_depth,
                                            uint32_t stage_rows, uint32_t band_rows, uint32_t n, uint32_t first,
-                                           uint32_t members, uint32_t row0);
+                                           uint32_t members);
 extern "C" __global__ void sf_post_ssao(PostArgs a);
 extern "C" __global__ void sf_post_blur(PostArgs a, uint32_t dir);
 extern "C" __global__ void sf_post_final(PostArgs a);
@@ -1049,16 +1049,22 @@ int sfi_unpack_slabs(sf_ctx* c, const void* stage, uint32_t bytes_per_pixel, uin
             c->table_gen = c->consts_gen;
         }
     }
-    for (uint32_t r0 = 0; r0 < stage_rows; r0 += 65535u) {
+    if (bytes_per_pixel == 4u) {
+        // resident workgroups over the 256-pixel segments (each stages the per-lane constants in LDS once): 8 per CU,
+        // or fewer when the slabs have fewer segments
+        const uint64_t items = (uint64_t)members * stage_rows * ((c->W + 255u) / 256u);
+        const uint64_t cap = 8ull * (uint64_t)c->cus;
+        const dim3 grid((uint32_t)(items < cap ? items : cap));
+        hipLaunchKernelGGL(sf_slab_unpack4, grid, dim3(256), 0, s, a, reinterpret_cast<const uint32_t*>(stage),
+                           (const float4*)c->node_table, SF_NODE_TABLE_DEPTH, stage_rows, band_rows, band_count,
+                           first_member, members);
+        SF_HIP(c, hipGetLastError());
+    }
+    for (uint32_t r0 = 0; bytes_per_pixel == 16u && r0 < stage_rows; r0 += 65535u) {
         const uint32_t rows = stage_rows - r0 < 65535u ? stage_rows - r0 : 65535u;
         const dim3 grid((c->W + 255u) / 256u, rows, members);
-        if (bytes_per_pixel == 4u)
-            hipLaunchKernelGGL(sf_slab_unpack4, grid, dim3(256), 0, s, a, reinterpret_cast<const uint32_t*>(stage),
-                               (const float4*)c->node_table, SF_NODE_TABLE_DEPTH, stage_rows, band_rows, band_count,
-                               first_member, members, r0);
-        else
-            hipLaunchKernelGGL(sf_band_unpack, grid, dim3(256), 0, s, a, reinterpret_cast<const float4*>(stage),
-                               stage_rows, band_rows, band_count, first_member, members, r0);
+        hipLaunchKernelGGL(sf_band_unpack, grid, dim3(256), 0, s, a, reinterpret_cast<const float4*>(stage),
+                           stage_rows, band_rows, band_count, first_member, members, r0);
         SF_HIP(c, hipGetLastError());
     }
     if (join && s != c->stream) SF_HIP(c, hipEventRecord(c->join_ev, s));   // (StreamMark)

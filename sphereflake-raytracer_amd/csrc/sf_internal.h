@@ -187,9 +187,10 @@ struct FrameArgs {
 #define SF_INDEX_SLAB_DEPTH 10
 #define SF_SLAB_MISS 0xffffffffu
 #define SF_SLAB_BAD 0xfffffffeu
-// node table of the index unpack: the frames of every node of depth <= SF_NODE_TABLE_DEPTH (3 float4 each)
-#define SF_NODE_TABLE_DEPTH 5u
-#define SF_NODE_TABLE_NODES 66430u    // (9^6 - 1) / 8
+// node table of the index unpack: the frames of every node of depth <= SF_NODE_TABLE_DEPTH (3 float4 each; 28.7 MB,
+// rebuilt when the root transform changes)
+#define SF_NODE_TABLE_DEPTH 6u
+#define SF_NODE_TABLE_NODES 597871u   // (9^7 - 1) / 8
 
 // Headless SSAO post-process (Shaders/post_ssao.glsl, post_ssao_blur.glsl,
 // post_final.glsl, SSAO.cpp:106-142). Textures are modelled, not emulated: NEAREST/LINEAR filtering

@@ -118,13 +118,15 @@ __device__ __forceinline__ float near_root(float tca, float d2, float R2)
 // frame of child i of a depth-p node whose frame is P, both as 3 x 4 {column-major xyz} (xf[3 c + r]). The child's
 // unit frame has its translation column scaled by (4/3) r_p. The per-ray kernel and the slab unpack both chain
 // with it, so a node's frame is the same float values whichever computes it.
-__device__ __forceinline__ void child_frame(const DeviceConsts* __restrict__ K, uint32_t p, uint32_t i,
+// (child: the 9 unit child frames, scale: the per-depth child translation scales -- from the constant block, or an
+// LDS image of them in the slab unpack)
+__device__ __forceinline__ void child_frame(const float (*child)[16], const float* scale, uint32_t p, uint32_t i,
                                             const float* P, float* out)
 {
-    const float s = K->dt.scale[p];
+    const float s = scale[p];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const float* B = K->child[i] + 4 * c;
+        const float* B = child[i] + 4 * c;
         const float b0 = c == 3 ? B[0] * s : B[0];
         const float b1 = c == 3 ? B[1] * s : B[1];
         const float b2 = c == 3 ? B[2] * s : B[2];
@@ -133,6 +135,11 @@ __device__ __forceinline__ void child_frame(const DeviceConsts* __restrict__ K, 
         for (int r = 0; r < 3; ++r)
             out[3 * c + r] = ((P[r] * b0 + P[3 + r] * b1) + P[6 + r] * b2) + P[9 + r] * b3;
     }
+}
+__device__ __forceinline__ void child_frame(const DeviceConsts* __restrict__ K, uint32_t p, uint32_t i,
+                                            const float* P, float* out)
+{
+    child_frame(K->child, K->dt.scale, p, i, P, out);
 }
 
 struct HitState {
@@ -2330,75 +2337,124 @@ extern "C" __global__ __launch_bounds__(256) void sf_node_table(FrameArgs a, flo
 // slabs of uint32 heap indices (SF_SLAB_MISS: no hit) laid out as sf_band_unpack's. A hit's pixel is rebuilt with
 // the tracer's own operations: the sphere's frame from the node table (its ancestor at depth <= table_depth) and
 // child_frame for the levels below, then the node's self test (Sphereflake.h:174-224: tca, d2, the near root with
-// r_d^2) gives minT, and shade's position dir * minT and normal Normalize(position - centre). One thread per
-// staged pixel along a slab row: coalesced 4-B reads, 2 x 16-B writes.
-extern "C" __global__ __launch_bounds__(256) void sf_slab_unpack4(FrameArgs a, const uint32_t* __restrict__ stage,
+// r_d^2) gives minT, and shade's position dir * minT and normal Normalize(position - centre). Coalesced 4-B reads
+// along a slab row, 2 x 16-B writes per pixel.
+// Round 5: a grid of resident workgroups, each first copying into LDS the constants every pixel reads at a lane-
+// dependent index -- the rsqrtps table (ray_dir, shade), the 9 unit child frames, the depth scales and self radii^2 --
+// then taking 256-pixel segments (member, slab row, x / 256) in turn. Read through the constant block they were ~15
+// dependent global loads per pixel (PMC, 4K: 57 % of the wave cycles waiting on memory against VALU issue ~0.5).
+struct UnpackLds {
+    uint32_t lut[2048];
+    float child[9][16];
+    float scale[SF_DEPTH_TABLE];
+    float r2_self[SF_DEPTH_TABLE];
+};
+
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_slab_unpack4(
+    FrameArgs a, const uint32_t* __restrict__ stage,
                                                                    const float4* __restrict__ table,
                                                                    uint32_t table_depth, uint32_t stage_rows,
                                                                    uint32_t band_rows, uint32_t n, uint32_t first,
-                                                                   uint32_t members, uint32_t row0)
+                                                                   uint32_t members)
 {
-    const uint32_t x = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t sr = row0 + blockIdx.y;
-    const uint32_t m = blockIdx.z;
-    if (x >= a.W || m >= members) return;
-    const uint32_t k = first + m, i = sr / band_rows, r = sr % band_rows;
-    const uint32_t y = (i * n + k) * band_rows + r;
-    if (y >= a.H) return;
-    const uint32_t idx = stage[((size_t)m * stage_rows + sr) * a.W + x];
-    const size_t o = (size_t)y * a.W + x;
-    if (idx >= SF_SLAB_BAD) {   // a miss: (0, 0, 0, 1) twice; SF_SLAB_BAD (never made by a correct split): NaN
-        const float v = idx == SF_SLAB_MISS ? 0.0f : __builtin_nanf("");
-        reinterpret_cast<float4*>(a.pos)[o] = make_float4(v, v, v, 1.0f);
-        reinterpret_cast<float4*>(a.nrm)[o] = make_float4(v, v, v, 1.0f);
-        return;
-    }
-    const DeviceConsts* __restrict__ K = a.consts;
-    uint64_t path;
-    const uint32_t d = heap_path(idx, path);
-    const uint32_t td = d < table_depth ? d : table_depth;
-    uint32_t anc = idx;
-    for (uint32_t j = td; j < d; ++j) anc = (anc - 1u) / 9u;
-    float xf[12], nx[12];
+    __shared__ UnpackLds S;
     {
-        const float4 c0 = table[3u * anc], c1 = table[3u * anc + 1u], c2 = table[3u * anc + 2u];
-        xf[0] = c0.x; xf[1] = c0.y; xf[2] = c0.z; xf[3] = c0.w;
-        xf[4] = c1.x; xf[5] = c1.y; xf[6] = c1.z; xf[7] = c1.w;
-        xf[8] = c2.x; xf[9] = c2.y; xf[10] = c2.z; xf[11] = c2.w;
+        const DeviceConsts* __restrict__ K = a.consts;
+        for (uint32_t i = threadIdx.x; i < 2048u; i += 256u) S.lut[i] = K->lut[i];
+        if (threadIdx.x < 144u) S.child[threadIdx.x >> 4][threadIdx.x & 15u] = K->child[threadIdx.x >> 4][threadIdx.x & 15u];
+        if (threadIdx.x < SF_DEPTH_TABLE) {
+            S.scale[threadIdx.x] = K->dt.scale[threadIdx.x];
+            S.r2_self[threadIdx.x] = K->dt.r2_self[threadIdx.x];
+        }
     }
-    // the frames down to the parent, then only the sphere's centre: child_frame's translation column (the same
-    // operations on the same operands)
-    for (uint32_t j = td; j + 1u < d; ++j) {
-        child_frame(K, j, (uint32_t)(path >> (4u * (d - 1u - j))) & 15u, xf, nx);
+    __syncthreads();
+    const uint32_t segs = (a.W + 255u) >> 8;
+    const uint32_t items = members * stage_rows * segs;   // (< 2^32: 16384^2 frames give 2^22)
+    // item -> this lane's pixel (x, frame row y) and slab word; false past the frame (rows past a member's slab)
+    auto locate = [&](uint32_t it, uint32_t& x, uint32_t& y, size_t& w) {
+        const uint32_t seg = it % segs, rest = it / segs;   // (uniform)
+        const uint32_t sr = rest % stage_rows, m = rest / stage_rows;
+        x = (seg << 8) + threadIdx.x;
+        const uint32_t k = first + m, i = sr / band_rows, r = sr % band_rows;
+        y = (i * n + k) * band_rows + r;
+        w = ((size_t)m * stage_rows + sr) * a.W + x;
+        return x < a.W && y < a.H;
+    };
+    // the next item's slab word is loaded while this one is rebuilt (its HBM latency off the chain)
+    uint32_t x, y;
+    size_t w;
+    bool ok = blockIdx.x < items && locate(blockIdx.x, x, y, w);
+    uint32_t idx_next = ok ? stage[w] : SF_SLAB_MISS;
+    for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const uint32_t idx = idx_next;
+        const bool cur = ok;
+        const uint32_t cx_ = x, cy_ = y;
+        ok = it + gridDim.x < items && locate(it + gridDim.x, x, y, w);
+        if (ok) idx_next = stage[w];
+        if (!cur) continue;
+        const uint32_t px_ = cx_, py_ = cy_;
+        float dx, dy, dz;
+        ray_dir(a, (float)px_, (float)py_, dx, dy, dz, S.lut);   // (independent of idx: in flight with its load)
+        const size_t o = (size_t)py_ * a.W + px_;
+        if (idx >= SF_SLAB_BAD) {   // a miss: (0, 0, 0, 1) twice; SF_SLAB_BAD (never made by a correct split): NaN
+            const float v = idx == SF_SLAB_MISS ? 0.0f : __builtin_nanf("");
+            reinterpret_cast<float4*>(a.pos)[o] = make_float4(v, v, v, 1.0f);
+            reinterpret_cast<float4*>(a.nrm)[o] = make_float4(v, v, v, 1.0f);
+            continue;
+        }
+        // the depth from the index (the first heap index of depth k is (9^k - 1) / 8), then only the child digits
+        // below the table's depth, bottom-up: the deepest lands in the highest nibble, depth td + 1's in the lowest
+        uint32_t d = 0u;
 #pragma unroll
-        for (int q = 0; q < 12; ++q) xf[q] = nx[q];
+        for (uint32_t k = 1u, f = 1u; k <= 10u; ++k, f = 9u * f + 1u) d += idx >= f ? 1u : 0u;
+        d += idx >= 3922632451u ? 1u : 0u;   // (depth 11: (9^11 - 1) / 8)
+        const uint32_t td = d < table_depth ? d : table_depth;
+        uint32_t anc = idx, path = 0u;
+        for (uint32_t j = d; j > td; --j) {
+            const uint32_t q = (anc - 1u) / 9u;
+            path = (path << 4) | (anc - 1u - 9u * q);
+            anc = q;
+        }
+        float xf[12], nx[12];
+        {
+            const float4 c0 = table[3u * anc], c1 = table[3u * anc + 1u], c2 = table[3u * anc + 2u];
+            xf[0] = c0.x; xf[1] = c0.y; xf[2] = c0.z; xf[3] = c0.w;
+            xf[4] = c1.x; xf[5] = c1.y; xf[6] = c1.z; xf[7] = c1.w;
+            xf[8] = c2.x; xf[9] = c2.y; xf[10] = c2.z; xf[11] = c2.w;
+        }
+        // the frames down to the parent, then only the sphere's centre: child_frame's translation column (the same
+        // operations on the same operands)
+        for (uint32_t j = td; j + 1u < d; ++j) {
+            child_frame(S.child, S.scale, j, path & 15u, xf, nx);
+            path >>= 4;
+#pragma unroll
+            for (int q = 0; q < 12; ++q) xf[q] = nx[q];
+        }
+        float cx = xf[9], cy = xf[10], cz = xf[11];
+        if (d > td) {
+            const uint32_t ci = path & 15u;
+            const float sc = S.scale[d - 1u];
+            const float* B = S.child[ci] + 12;
+            const float b0 = B[0] * sc, b1 = B[1] * sc, b2 = B[2] * sc, b3 = B[3];
+            cx = ((xf[0] * b0 + xf[3] * b1) + xf[6] * b2) + xf[9] * b3;
+            cy = ((xf[1] * b0 + xf[4] * b1) + xf[7] * b2) + xf[10] * b3;
+            cz = ((xf[2] * b0 + xf[5] * b1) + xf[8] * b2) + xf[11] * b3;
+        }
+        const float tca = (cx * dx + cy * dy) + cz * dz;
+        const float d2 = ((cx * cx + cy * cy) + cz * cz) - tca * tca;
+        HitState h;
+        h.minT = near_root(tca, d2, S.r2_self[d]);
+        h.cx = cx;
+        h.cy = cy;
+        h.cz = cz;
+        h.index = idx;
+        h.depth = (int32_t)d;
+        h.hit = true;
+        float px, py, pz, qx, qy, qz;
+        shade(dx, dy, dz, h, S.lut, px, py, pz, qx, qy, qz);
+        reinterpret_cast<float4*>(a.pos)[o] = make_float4(px, py, pz, 1.0f);
+        reinterpret_cast<float4*>(a.nrm)[o] = make_float4(qx, qy, qz, 1.0f);
     }
-    float cx = xf[9], cy = xf[10], cz = xf[11];
-    if (d > td) {
-        const uint32_t i = (uint32_t)path & 15u;
-        const float s = K->dt.scale[d - 1u];
-        const float* B = K->child[i] + 12;
-        const float b0 = B[0] * s, b1 = B[1] * s, b2 = B[2] * s, b3 = B[3];
-        cx = ((xf[0] * b0 + xf[3] * b1) + xf[6] * b2) + xf[9] * b3;
-        cy = ((xf[1] * b0 + xf[4] * b1) + xf[7] * b2) + xf[10] * b3;
-        cz = ((xf[2] * b0 + xf[5] * b1) + xf[8] * b2) + xf[11] * b3;
-    }
-    float dx, dy, dz;
-    ray_dir(a, (float)x, (float)y, dx, dy, dz, K->lut);
-    const float tca = (cx * dx + cy * dy) + cz * dz;
-    const float d2 = ((cx * cx + cy * cy) + cz * cz) - tca * tca;
-    HitState h;
-    h.minT = near_root(tca, d2, K->dt.r2_self[d]);
-    h.cx = cx;
-    h.cy = cy;
-    h.cz = cz;
-    h.index = idx;
-    h.depth = (int32_t)d;
-    h.hit = true;
-    float px, py, pz, qx, qy, qz;
-    shade(dx, dy, dz, h, K->lut, px, py, pz, qx, qy, qz);
-    reinterpret_cast<float4*>(a.pos)[o] = make_float4(px, py, pz, 1.0f);
-    reinterpret_cast<float4*>(a.nrm)[o] = make_float4(qx, qy, qz, 1.0f);
 }
 
 // Re-traces flagged tiles with SF_MAX_LEVELS levels. Grid-stride over the list; reads this
