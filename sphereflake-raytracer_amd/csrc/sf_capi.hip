@@ -245,7 +245,7 @@ struct sf_ctx {
     hipEvent_t join_ev = nullptr;      // the point later calls order after (see ctx_join / StreamMark)
     // Heavy-first tile order: -1 (default) on whole frames whose tiles fill at most half the persistent grid's
     // waves (640x360: rebuilt after every 3rd render, costs recorded by every render) and on whole frames of more
-    // than twice its waves (1080p and up: rebuilt after every 16th render from that render's costs only, model
+    // than twice its waves (1080p and up: rebuilt after every 64th render (16th until round 5) from that render's costs only, model
     // splits: no steady-state cost, shorter frame ends); row-major between (1280x720) and on multi-GPU shares, where
     // with frames in flight the order measured slower (round 3); env SF_ORDER=0 never, SF_ORDER=1 always
     int order_mode = -1;
@@ -788,7 +788,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             // over 8 GPUs: 0.0212 vs 0.0204 ms per frame, `profiles/r3/share2/r3aw.txt`).
             const bool tiny = 2u * ntiles <= nblk * wpb && band_count == 1u;
             // Round 4: whole frames of more than twice the grid's waves (1080p and up) take the order too, in a form
-            // that costs the steady state nothing: rebuilt after every 16th render from that render's tile costs
+            // that costs the steady state nothing: rebuilt after every 16th render (64th since round 5, below) from that render's tile costs
             // alone (the renders between record nothing), heavy tiles split by the makespan model. With 3 frames in
             // flight the steady frame period is unchanged (1080p 0.0787 vs 0.0792 ms, 4K 0.373 vs 0.373), but a
             // frame whose successors are not yet queued -- the last of a timed loop, a lone frame -- no longer ends
@@ -823,7 +823,11 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             // order costs the trace nothing measurable while the two order kernels are ~5 us of a ~80 us
             // frame, so by default they are rebuilt after every 3rd render (640x360 -6 %, 1280x720 -4 %);
             // full grids are throughput-bound and a stale order costs more than the kernels (1080p).
-            const uint32_t every = c->order_every ? c->order_every : (small ? 3u : large ? 16u : 1u);
+            // (large frames: every 64th since round 5 -- the rebuild's scan is one 16-wave workgroup, which waits for
+            // wave slots behind the frames in flight, 64 us median and up to 1.6 ms in the bench, with its slot's next
+            // frame queued behind it: the driver's 20-step loop 0.0727-0.0743 -> 0.0721-0.0722 ms in two 5-run A/Bs;
+            // a one-wave scan, or the rebuild on a stream of its own, measured slower, profiles/r5/order/)
+            const uint32_t every = c->order_every ? c->order_every : (small ? 3u : large ? 64u : 1u);
             const bool rebuild = use_order && (c->order_n != ntiles || c->order_phase + 1u >= every);
             if (use_order) c->order_phase = rebuild ? 0u : c->order_phase + 1u;
             if (use_order) {

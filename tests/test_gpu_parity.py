@@ -675,7 +675,7 @@ def test_raised_priority_tiles_bit_exact(prio, monkeypatch):
 def test_tile_order_auto_by_frame_size(name, ordered):
     """Default tile order (sf_capi.hip order_mode -1): heavy-first for frames whose tiles fill at most half the
     persistent grid's waves (c1: 3 600 tiles for 8 192 waves) and for frames of more than twice its waves (c3, c4:
-    rebuilt every 16th render, no splits), row-major between (c2: 14 400 tiles, where the order measured
+    rebuilt every 64th render, no splits), row-major between (c2: 14 400 tiles, where the order measured
     slower). Either way every render equals the golden frame."""
     fx = load_frame(name)
     W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
