@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """How long the heavy-first order's kernels hold their slot's queue (diagnostics): from a rocprofv3 kernel trace of a
-bench.py run, every sf_order_scan / sf_order_scatter dispatch -- its duration, and the trace kernel queued behind it on
+bench.py run, every order-rebuild dispatch (sf_order_scan / sf_order_scatter, or since round 5 on large frames
+sf_order_bucket_scan / sf_order_scatter_plan) -- its duration, and the trace kernel queued behind it on
 the same queue: how long after the previous trace on that queue ended it could start. Prints quantiles, and the total
 time the order kernels added to their queues' chains. Usage: order_stall.py <kernel_trace.csv>"""
 import csv
@@ -21,7 +22,7 @@ scan, scat, held = [], [], []
 for q, ks in byq.items():
     for i, r in enumerate(ks):
         name = r["Kernel_Name"]
-        if name.startswith("sf_order_scan"):
+        if name.startswith("sf_order_scan") or name.startswith("sf_order_bucket_scan"):
             scan.append((r["e"] - r["s"]) / 1e3)
             # the trace before it on this queue, and the next trace after it
             prev = next((k for k in reversed(ks[:i]) if k["Kernel_Name"].startswith("sf_trace")), None)
@@ -42,7 +43,7 @@ def qs(x):
             if len(x) else "none")
 
 
-print("sf_order_scan duration:     ", qs(scan))
-print("sf_order_scatter duration:  ", qs(scat))
+print("scan (sf_order_scan / sf_order_bucket_scan) duration:        ", qs(scan))
+print("scatter (sf_order_scatter / sf_order_scatter_plan) duration: ", qs(scat))
 print("trace -> next trace on a queue, across a rebuild:", qs(held))
 print("trace -> next trace on a queue, all:             ", qs(gaps))

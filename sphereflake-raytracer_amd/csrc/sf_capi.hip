@@ -33,6 +33,11 @@ extern "C" __global__ void sf_order_scan(uint32_t* chunk_cnt, uint32_t nc, uint3
                                          uint32_t prio_buckets,
                                          uint32_t* chunk_off, uint32_t* order_meta, const uint32_t* fuse_cost,
                                          uint32_t* fuse_order, uint32_t split_cap);
+extern "C" __global__ void sf_order_bucket_scan(const uint32_t* chunk_cnt, uint32_t nc, uint32_t* chunk_rel, uint32_t* tot);
+extern "C" __global__ void sf_order_scatter_plan(const uint32_t* cost, uint32_t n, uint32_t* chunk_cnt,
+                                                 const uint32_t* chunk_rel, const uint32_t* tot, uint32_t split_buckets,
+                                                 uint32_t parts, uint32_t spare, uint32_t waves, uint32_t prio_buckets,
+                                                 uint32_t split_cap, uint32_t* order_meta, uint32_t* order);
 extern "C" __global__ void sf_order_scatter(const uint32_t* cost, uint32_t n, uint32_t* chunk_cnt,
                                             const uint32_t* chunk_off, const uint32_t* order_meta, uint32_t* order,
                                             uint32_t* rank_out);
@@ -228,6 +233,7 @@ struct sf_ctx {
     uint32_t* chunk_cnt = nullptr;     // per 64-tile chunk x SF_ORDER_BUCKETS (zeroed by sf_order_scatter)
     uint32_t* chunk_off = nullptr;
     uint32_t* order_meta = nullptr;    // [0] work units in tile_order, [1] first split bucket, [2] parts per split tile, [3] first raised-priority bucket
+    uint32_t* order_tot = nullptr;     // per cost bucket: tiles of the rebuilding render (sf_order_bucket_scan)
     uint32_t split_buckets = SF_SPLIT_AUTO;   // env SF_SPLIT_BUCKETS = k: top k buckets (0: never split)
     uint32_t split_parts = 4;          // env SF_SPLIT_PARTS = 2 (halves) | 4 (quarters); 640x360: 0.122 -> 0.097 ms with quarters
     uint32_t* part_cost = nullptr;     // per tile: slowest part of a split tile (zeroed, reset by the last part)
@@ -376,6 +382,7 @@ static void free_ctx(sf_ctx* c)
     (void)hipFree(c->chunk_cnt);
     (void)hipFree(c->chunk_off);
     (void)hipFree(c->order_meta);
+    (void)hipFree(c->order_tot);
     (void)hipFree(c->part_cost);
     (void)hipFree(c->part_done);
     (void)hipFree(c->part_rec);
@@ -567,6 +574,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
     if ((e = hipMalloc(&c->tile_cost, ntiles * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->tile_order, 4 * ntiles * 4)) != hipSuccess) return fail(e);   // <= 4 units per tile
     if ((e = hipMalloc(&c->order_meta, 4 * 4)) != hipSuccess) return fail(e);
+    if ((e = hipMalloc(&c->order_tot, SF_ORDER_BUCKETS * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->part_cost, ntiles * 4)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->part_done, ntiles * 4)) != hipSuccess) return fail(e);
     if ((e = hipMemsetAsync(c->part_cost, 0, ntiles * 4, c->stream)) != hipSuccess) return fail(e);
@@ -874,15 +882,20 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 // few chunks: the scan's workgroup also scatters (one launch: ~3 us less host time and one
                 // dispatch less on the frame's stream); more: one wave per chunk in a launch of its own
                 const bool fuse = nc <= SF_ORDER_FUSE_CHUNKS;
-                hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, c->chunk_cnt, nc, ntiles,
-                                   split_buckets, c->split_parts, spare, waves, c->prio_buckets, c->chunk_off,
-                                   c->order_meta, fuse ? (const uint32_t*)c->tile_cost : nullptr,
-                                   fuse ? c->tile_order : nullptr, c->part_rec ? SF_SPLIT_CAP : 0xffffffffu);
-                SF_HIP(c, hipGetLastError());
-                if (!fuse) {
-                    hipLaunchKernelGGL(sf_order_scatter, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost, ntiles,
-                                       c->chunk_cnt, (const uint32_t*)c->chunk_off, (const uint32_t*)c->order_meta,
-                                       c->tile_order, nullptr);
+                const uint32_t cap = c->part_rec ? SF_SPLIT_CAP : 0xffffffffu;
+                if (fuse) {
+                    hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, c->chunk_cnt, nc, ntiles,
+                                       split_buckets, c->split_parts, spare, waves, c->prio_buckets, c->chunk_off,
+                                       c->order_meta, (const uint32_t*)c->tile_cost, c->tile_order, cap);
+                    SF_HIP(c, hipGetLastError());
+                } else {   // (round 5: one-wave workgroups only -- see sf_order_bucket_scan)
+                    hipLaunchKernelGGL(sf_order_bucket_scan, dim3(SF_ORDER_BUCKETS), dim3(64), 0, s,
+                                       (const uint32_t*)c->chunk_cnt, nc, c->chunk_off, c->order_tot);
+                    SF_HIP(c, hipGetLastError());
+                    hipLaunchKernelGGL(sf_order_scatter_plan, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost,
+                                       ntiles, c->chunk_cnt, (const uint32_t*)c->chunk_off,
+                                       (const uint32_t*)c->order_tot, split_buckets, c->split_parts, spare, waves,
+                                       c->prio_buckets, cap, c->order_meta, c->tile_order);
                     SF_HIP(c, hipGetLastError());
                 }
                 c->order_n = ntiles;

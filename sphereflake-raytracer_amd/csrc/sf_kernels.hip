@@ -2069,16 +2069,15 @@ extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(
 // deterministic. Any permutation gives the same image: only the schedule changes.
 // One 64-item chunk c of the scatter, one wave (lane = item within the chunk).
 // (rank_out, when not NULL: rank_out[i] = item i's position, the inverse permutation; unsplit orders only)
+// (offs: lane b's value is bucket b & 31's output offset for this chunk)
 __device__ __forceinline__ void order_scatter_chunk(uint32_t c, uint32_t lane, const uint32_t* __restrict__ cost,
-                                                    uint32_t n, uint32_t* __restrict__ chunk_cnt,
-                                                    const uint32_t* __restrict__ chunk_off, uint32_t split_from,
-                                                    uint32_t parts, uint32_t pb, uint32_t* __restrict__ order,
-                                                    uint32_t* __restrict__ rank_out)
+                                                    uint32_t n, uint32_t* __restrict__ chunk_cnt, uint32_t offs,
+                                                    uint32_t split_from, uint32_t parts, uint32_t pb,
+                                                    uint32_t* __restrict__ order, uint32_t* __restrict__ rank_out)
 {
     const uint32_t i = c * 64u + lane;
     const uint32_t first = parts == 4u ? SF_PART_QUARTER0 : SF_PART_HALF0;
     const uint32_t bk = i < n ? cost_bucket(cost[i]) : SF_ORDER_BUCKETS;   // sentinel: no tile
-    const uint32_t offs = chunk_off[c * SF_ORDER_BUCKETS + (lane & (SF_ORDER_BUCKETS - 1u))];   // lane b: bucket b
     uint64_t pending = __builtin_amdgcn_ballot_w64(bk < SF_ORDER_BUCKETS);
     while (pending) {   // one round per distinct bucket in the chunk
         const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)bk, (int)__builtin_ctzll(pending));
@@ -2098,6 +2097,95 @@ __device__ __forceinline__ void order_scatter_chunk(uint32_t c, uint32_t lane, c
         pending &= ~m;
     }
     if (lane < SF_ORDER_BUCKETS) chunk_cnt[c * SF_ORDER_BUCKETS + lane] = 0u;   // for the next render
+}
+
+// The order's split and priority decisions and the bucket output offsets, by one wave: lane l holds bucket l's
+// tile count t (lanes 32..63: 0). Returns the first split bucket and the first raised-priority bucket; X_excl = the
+// units of the buckets heavier than l (lane l), units = all the units.
+struct OrderPlan {
+    int bs, bp;
+    uint32_t X_excl, units;
+};
+__device__ __forceinline__ OrderPlan order_decide(uint32_t t, uint32_t l, uint32_t n_tiles, uint32_t split_buckets,
+                                                  uint32_t parts, uint32_t spare, uint32_t waves, uint32_t prio_buckets,
+                                                  uint32_t split_cap)
+{
+    // One wave, lane = bucket (lanes 32..63 hold 0): the split and priority decisions and the bucket
+    // offsets from suffix sums over the buckets (heaviest first), instead of serial loops on one thread.
+    // Split tiles into `parts` units each, heaviest buckets first (bucket 0 never): automatically as
+    // many whole buckets as fit into `spare` idle wave slots, or the top `split_buckets` occupied
+    // buckets (at most an eighth of the tiles).
+    uint32_t S = t;   // S(l) = sum of tot[bb] over bb >= l
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+        const uint32_t up = (uint32_t)__shfl_down((int)S, o, 64);
+        S += l + (uint32_t)o < SF_ORDER_BUCKETS ? up : 0u;
+    }
+    const uint64_t nz = __builtin_amdgcn_ballot_w64(t != 0u);
+    const int btop = nz ? 63 - __builtin_clzll(nz) : 0;   // highest occupied bucket (0 if none)
+    int bs = (int)SF_ORDER_BUCKETS;
+    if (split_buckets == SF_SPLIT_AUTO) {
+        // S is non-increasing in the bucket: the buckets that fit form a suffix
+        const uint64_t ok = __builtin_amdgcn_ballot_w64(l >= 1u && l < SF_ORDER_BUCKETS && S * (parts - 1u) <= spare);
+        if (ok >> (SF_ORDER_BUCKETS - 1u) & 1ull) bs = __builtin_ctzll(ok);
+    } else if (split_buckets == SF_SPLIT_MODEL && waves > 0u) {
+        // Makespan model (LPT list scheduling on `waves` slots, the last render's costs): unsplit, the
+        // frame takes at least max(C / waves, c_top); splitting buckets >= l into `parts` units adds their
+        // work x (parts x rho - 1) and leaves max(the heaviest unsplit bucket, rho x c_top) as the longest
+        // unit (rho: the slowest part's share of its tile, measured 0.6 for quarters, 0.68 for halves).
+        // Take the l of the least estimate when it is >= 10 % below the unsplit one.
+        const float rho = parts == 4u ? 0.6f : 0.68f;
+        const uint32_t e = (l + 16u) >> 1;   // bucket l covers [2^e (1 + m/2), ...) cycles, m = (l + 16) & 1
+        const float c = l < SF_ORDER_BUCKETS ? __builtin_ldexpf((l + 16u) & 1u ? 1.75f : 1.25f, (int)e) : 0.0f;
+        const float w = (float)t * c;   // this bucket's work
+        float A = w;                    // A(l) = work of the buckets >= l
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+            const float up = __shfl_down(A, o, 64);
+            A += l + (uint32_t)o < SF_ORDER_BUCKETS ? up : 0.0f;
+        }
+        const float C = __shfl(A, 0, 64);                 // all the work
+        const float ctop = __shfl(c, btop, 64);
+        const uint64_t below = nz & ((1ull << l) - 1ull);   // occupied buckets under l
+        const float cun = below ? __shfl(c, 63 - __builtin_clzll(below), 64) : 0.0f;
+        const float Tn = fmaxf(C / (float)waves, ctop);
+        float T = fmaxf(fmaxf((C + A * ((float)parts * rho - 1.0f)) / (float)waves, cun), rho * ctop);
+        if (!(l >= 1u && (int)l <= btop)) T = __builtin_inff();
+        float Tm = T;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) Tm = fminf(Tm, __shfl_xor(Tm, o, 64));
+        const uint64_t best = __builtin_amdgcn_ballot_w64(T == Tm);
+        if (Tm < 0.9f * Tn && best) bs = 63 - __builtin_clzll(best);   // (ties: the fewest splits)
+    } else if (split_buckets != 0u) {
+        int b0 = btop - (int)split_buckets + 1;
+        if (b0 < 1) b0 = 1;
+        // then drop buckets from the bottom of the range while more than an eighth of the tiles split
+        const uint64_t ok = __builtin_amdgcn_ballot_w64((int)l >= b0 && l < SF_ORDER_BUCKETS && 8u * S <= n_tiles);
+        bs = ok ? __builtin_ctzll(ok) : (int)SF_ORDER_BUCKETS;
+    }
+    // at most split_cap split tiles (the subtree parts' records are per split slot): S(l) is non-increasing
+    {
+        const uint64_t capok = __builtin_amdgcn_ballot_w64(l < SF_ORDER_BUCKETS && S <= split_cap);
+        const int bcap = capok ? __builtin_ctzll(capok) : (int)SF_ORDER_BUCKETS;
+        if (bs < bcap) bs = bcap;
+    }
+    // the top `prio_buckets` occupied cost buckets run at raised wave priority next render (their
+    // serial DFS is the frame's critical path)
+    const int bp = btop - (int)prio_buckets + 1;
+    // units per bucket -> exclusive offsets, heaviest first: X(l) = sum of units over bb > l
+    const uint32_t x = t * ((int)l >= bs ? parts : 1u);
+    uint32_t X = x;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+        const uint32_t up = (uint32_t)__shfl_down((int)X, o, 64);
+        X += l + (uint32_t)o < SF_ORDER_BUCKETS ? up : 0u;
+    }
+    OrderPlan r;
+    r.bs = bs;
+    r.bp = bp;
+    r.X_excl = X - x;
+    r.units = (uint32_t)__shfl(X, 0, 64);
+    return r;
 }
 
 #define SF_SCAN_BATCH 16   // chunk counts a scan thread loads at once (independent loads, one wait)
@@ -2149,79 +2237,12 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(uint32_t* __res
     __syncthreads();
     __shared__ uint32_t split_from;
     if (tid < 64u) {
-        // One wave, lane = bucket (lanes 32..63 hold 0): the split and priority decisions and the bucket
-        // offsets from suffix sums over the buckets (heaviest first), instead of serial loops on one thread.
-        // Split tiles into `parts` units each, heaviest buckets first (bucket 0 never): automatically as
-        // many whole buckets as fit into `spare` idle wave slots, or the top `split_buckets` occupied
-        // buckets (at most an eighth of the tiles).
         const uint32_t l = tid;
         const uint32_t t = l < SF_ORDER_BUCKETS ? tot[l] : 0u;
-        uint32_t S = t;   // S(l) = sum of tot[bb] over bb >= l
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-            const uint32_t up = (uint32_t)__shfl_down((int)S, o, 64);
-            S += l + (uint32_t)o < SF_ORDER_BUCKETS ? up : 0u;
-        }
-        const uint64_t nz = __builtin_amdgcn_ballot_w64(t != 0u);
-        const int btop = nz ? 63 - __builtin_clzll(nz) : 0;   // highest occupied bucket (0 if none)
-        int bs = (int)SF_ORDER_BUCKETS;
-        if (split_buckets == SF_SPLIT_AUTO) {
-            // S is non-increasing in the bucket: the buckets that fit form a suffix
-            const uint64_t ok = __builtin_amdgcn_ballot_w64(l >= 1u && l < SF_ORDER_BUCKETS && S * (parts - 1u) <= spare);
-            if (ok >> (SF_ORDER_BUCKETS - 1u) & 1ull) bs = __builtin_ctzll(ok);
-        } else if (split_buckets == SF_SPLIT_MODEL && waves > 0u) {
-            // Makespan model (LPT list scheduling on `waves` slots, the last render's costs): unsplit, the
-            // frame takes at least max(C / waves, c_top); splitting buckets >= l into `parts` units adds their
-            // work x (parts x rho - 1) and leaves max(the heaviest unsplit bucket, rho x c_top) as the longest
-            // unit (rho: the slowest part's share of its tile, measured 0.6 for quarters, 0.68 for halves).
-            // Take the l of the least estimate when it is >= 10 % below the unsplit one.
-            const float rho = parts == 4u ? 0.6f : 0.68f;
-            const uint32_t e = (l + 16u) >> 1;   // bucket l covers [2^e (1 + m/2), ...) cycles, m = (l + 16) & 1
-            const float c = l < SF_ORDER_BUCKETS ? __builtin_ldexpf((l + 16u) & 1u ? 1.75f : 1.25f, (int)e) : 0.0f;
-            const float w = (float)t * c;   // this bucket's work
-            float A = w;                    // A(l) = work of the buckets >= l
-#pragma unroll
-            for (int o = 1; o < 32; o <<= 1) {
-                const float up = __shfl_down(A, o, 64);
-                A += l + (uint32_t)o < SF_ORDER_BUCKETS ? up : 0.0f;
-            }
-            const float C = __shfl(A, 0, 64);                 // all the work
-            const float ctop = __shfl(c, btop, 64);
-            const uint64_t below = nz & ((1ull << l) - 1ull);   // occupied buckets under l
-            const float cun = below ? __shfl(c, 63 - __builtin_clzll(below), 64) : 0.0f;
-            const float Tn = fmaxf(C / (float)waves, ctop);
-            float T = fmaxf(fmaxf((C + A * ((float)parts * rho - 1.0f)) / (float)waves, cun), rho * ctop);
-            if (!(l >= 1u && (int)l <= btop)) T = __builtin_inff();
-            float Tm = T;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) Tm = fminf(Tm, __shfl_xor(Tm, o, 64));
-            const uint64_t best = __builtin_amdgcn_ballot_w64(T == Tm);
-            if (Tm < 0.9f * Tn && best) bs = 63 - __builtin_clzll(best);   // (ties: the fewest splits)
-        } else if (split_buckets != 0u) {
-            int b0 = btop - (int)split_buckets + 1;
-            if (b0 < 1) b0 = 1;
-            // then drop buckets from the bottom of the range while more than an eighth of the tiles split
-            const uint64_t ok = __builtin_amdgcn_ballot_w64((int)l >= b0 && l < SF_ORDER_BUCKETS && 8u * S <= n_tiles);
-            bs = ok ? __builtin_ctzll(ok) : (int)SF_ORDER_BUCKETS;
-        }
-        // at most split_cap split tiles (the subtree parts' records are per split slot): S(l) is non-increasing
-        {
-            const uint64_t capok = __builtin_amdgcn_ballot_w64(l < SF_ORDER_BUCKETS && S <= split_cap);
-            const int bcap = capok ? __builtin_ctzll(capok) : (int)SF_ORDER_BUCKETS;
-            if (bs < bcap) bs = bcap;
-        }
-        // the top `prio_buckets` occupied cost buckets run at raised wave priority next render (their
-        // serial DFS is the frame's critical path)
-        const int bp = btop - (int)prio_buckets + 1;
-        // units per bucket -> exclusive offsets, heaviest first: X(l) = sum of units over bb > l
-        const uint32_t x = t * ((int)l >= bs ? parts : 1u);
-        uint32_t X = x;
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-            const uint32_t up = (uint32_t)__shfl_down((int)X, o, 64);
-            X += l + (uint32_t)o < SF_ORDER_BUCKETS ? up : 0u;
-        }
-        if (l < SF_ORDER_BUCKETS) tot[l] = X - x;
+        const OrderPlan pl = order_decide(t, l, n_tiles, split_buckets, parts, spare, waves, prio_buckets, split_cap);
+        const int bs = pl.bs, bp = pl.bp;
+        const uint32_t X = pl.units;
+        if (l < SF_ORDER_BUCKETS) tot[l] = pl.X_excl;
         if (l == 0u) {
             split_from = (uint32_t)bs;
             order_meta[0] = X;              // units of the next render
@@ -2253,7 +2274,8 @@ extern "C" __global__ __launch_bounds__(1024) void sf_order_scan(uint32_t* __res
         __syncthreads();
         const uint32_t pb = order_meta[3];
         for (uint32_t c = tid >> 6; c < nc; c += blockDim.x >> 6)
-            order_scatter_chunk(c, tid & 63u, fuse_cost, n_tiles, chunk_cnt, chunk_off, split_from, parts, pb,
+            order_scatter_chunk(c, tid & 63u, fuse_cost, n_tiles, chunk_cnt,
+                                chunk_off[c * SF_ORDER_BUCKETS + (tid & (SF_ORDER_BUCKETS - 1u))], split_from, parts, pb,
                                 fuse_order, nullptr);
     }
 }
@@ -2266,8 +2288,77 @@ extern "C" __global__ __launch_bounds__(64) void sf_order_scatter(const uint32_t
                                                                     uint32_t* __restrict__ rank_out)
 {
     __builtin_amdgcn_s_setprio(3);   // (see sf_order_scan)
-    order_scatter_chunk(blockIdx.x, threadIdx.x, cost, n, chunk_cnt, chunk_off, order_meta[1], order_meta[2],
-                        order_meta[3], order, rank_out);
+    order_scatter_chunk(blockIdx.x, threadIdx.x, cost, n, chunk_cnt,
+                        chunk_off[blockIdx.x * SF_ORDER_BUCKETS + (threadIdx.x & (SF_ORDER_BUCKETS - 1u))],
+                        order_meta[1], order_meta[2], order_meta[3], order, rank_out);
+}
+
+// The order rebuild of frames of many chunks in one-wave workgroups only (round 5): with frames in flight the
+// persistent trace grids of the other frames refill every wave slot that frees, and sf_order_scan's 16-wave
+// workgroup waited for 16 free slots on one CU -- 64 us median, up to 1.6 ms in the bench, its slot's next frame
+// queued behind it (profiles/r5/order/). sf_order_bucket_scan: workgroup b (one wave) forms bucket b's per-chunk
+// prefix over the chunks (lane l: chunks [l per, (l + 1) per)) and its total; sf_order_scatter_plan: every chunk's
+// wave redoes the 32-lane plan (order_decide) from the totals and scatters its chunk.
+extern "C" __global__ __launch_bounds__(64) void sf_order_bucket_scan(const uint32_t* __restrict__ chunk_cnt, uint32_t nc,
+                                                                        uint32_t* __restrict__ chunk_rel,
+                                                                        uint32_t* __restrict__ tot)
+{
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t b = blockIdx.x, l = threadIdx.x;
+    const uint32_t per = (nc + 63u) / 64u, c0 = l * per, c1 = min(nc, c0 + per);
+    uint32_t s_ = 0u;
+    for (uint32_t cb = c0; cb < c1; cb += SF_SCAN_BATCH) {
+        uint32_t v[SF_SCAN_BATCH];
+#pragma unroll
+        for (int j = 0; j < SF_SCAN_BATCH; ++j) v[j] = cb + j < c1 ? chunk_cnt[(cb + j) * SF_ORDER_BUCKETS + b] : 0u;
+#pragma unroll
+        for (int j = 0; j < SF_SCAN_BATCH; ++j) s_ += v[j];
+    }
+    uint32_t incl = s_;   // inclusive prefix over the lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t up = (uint32_t)__shfl_up((int)incl, o, 64);
+        incl += l >= (uint32_t)o ? up : 0u;
+    }
+    uint32_t off = incl - s_;
+    for (uint32_t cb = c0; cb < c1; cb += SF_SCAN_BATCH) {
+        uint32_t v[SF_SCAN_BATCH];
+#pragma unroll
+        for (int j = 0; j < SF_SCAN_BATCH; ++j) v[j] = cb + j < c1 ? chunk_cnt[(cb + j) * SF_ORDER_BUCKETS + b] : 0u;
+#pragma unroll
+        for (int j = 0; j < SF_SCAN_BATCH; ++j) {
+            if (cb + j < c1) chunk_rel[(cb + j) * SF_ORDER_BUCKETS + b] = off;
+            off += v[j];
+        }
+    }
+    if (l == 63u) tot[b] = incl;
+}
+
+extern "C" __global__ __launch_bounds__(64) void sf_order_scatter_plan(const uint32_t* __restrict__ cost, uint32_t n,
+                                                                         uint32_t* __restrict__ chunk_cnt,
+                                                                         const uint32_t* __restrict__ chunk_rel,
+                                                                         const uint32_t* __restrict__ tot,
+                                                                         uint32_t split_buckets, uint32_t parts,
+                                                                         uint32_t spare, uint32_t waves,
+                                                                         uint32_t prio_buckets, uint32_t split_cap,
+                                                                         uint32_t* __restrict__ order_meta,
+                                                                         uint32_t* __restrict__ order)
+{
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t l = threadIdx.x, c = blockIdx.x, bl = l & (SF_ORDER_BUCKETS - 1u);
+    const uint32_t t = l < SF_ORDER_BUCKETS ? tot[l] : 0u;
+    const uint32_t rel = chunk_rel[c * SF_ORDER_BUCKETS + bl];   // (in flight with the plan)
+    const OrderPlan pl = order_decide(t, l, n, split_buckets, parts, spare, waves, prio_buckets, split_cap);
+    const uint32_t pb = prio_buckets == 0u ? SF_ORDER_BUCKETS : (uint32_t)(pl.bp < 0 ? 0 : pl.bp);
+    if (c == 0u && l == 0u) {
+        order_meta[0] = pl.units;
+        order_meta[1] = (uint32_t)pl.bs;
+        order_meta[2] = parts;
+        order_meta[3] = pb;
+    }
+    const uint32_t base = (uint32_t)__shfl((int)pl.X_excl, (int)bl, 64);
+    const uint32_t offs = base + rel * ((int)bl >= pl.bs ? parts : 1u);
+    order_scatter_chunk(c, l, cost, n, chunk_cnt, offs, (uint32_t)pl.bs, parts, pb, order, nullptr);
 }
 
 // Packed band slabs -> the frame G-buffer (multi-GPU gather). `stage` holds `members` slabs
