@@ -1049,12 +1049,12 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
 // push, no load at the pop). A node keeps on the VGPR stack its untested children (the cone-culled mask,
 // front children first, as before) instead of its pending ones, and its visiting lanes as one bit per level
 // (`actbits`).
-// Entry-order mask (bits c and 9 + c, see traverse_ray) of the children c of a node whose child 0 has heap index
+// Entry-order mask (bits c and 16 + c, see traverse_ray) of the children c of a node whose child 0 has heap index
 // idxB that belong to subtree part q: (idxB + c) mod 4 == q.
 __device__ __forceinline__ uint32_t split_mask(uint32_t q, uint32_t idxB)
 {
     const uint32_t m9 = (0x111u << ((q - idxB) & 3u)) & 0x1ffu;
-    return m9 | (m9 << 9);
+    return m9 | (m9 << 16);
 }
 
 // SPLIT: a subtree part unit (SF_FLAG_SUBTREE): of the nodes at depth split_depth, only those whose heap index is
@@ -1185,13 +1185,13 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
 
     // ---- expand the node with centre/|c|^2 pc at depth d (axis columns at col + j cs): build its 9 child
     // transforms into table(d) and cull the children no ray of the tile's cone can reach. Returns the children
-    // left to test; leafm = its inline-leaf children | its front children << 9. At the deepest provisioned level
+    // left to test, in entry order (front child i at bit i, the others at 16 + i). At the deepest provisioned level
     // (no table for the children's children) the children are tested here, from the centre lanes: any that some
     // lane expands flags the tile for the deeper re-trace, and none is entered.
     const uint32_t lv32 = __builtin_amdgcn_readfirstlane(levels << 5);   // levels, in depth-constant offset units
     const uint32_t index_order = front_first ? 0u : 0x1ffu;
     // (tb: table(d), ko: d + 1's constants offset -- the caller's carried values, not formed here again)
-    auto expand = [&](const float4 pc, const float* col, uint32_t cs, uint32_t d, float actv, uint32_t& leafm,
+    auto expand = [&](const float4 pc, const float* col, uint32_t cs, uint32_t d, float actv,
                       float* tb, uint32_t ko, float kp) -> uint32_t {
         d = __builtin_amdgcn_readfirstlane(d);
         SF_COUNT(0, 1);
@@ -1204,8 +1204,6 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float sinT = L.cone()[4];
         const float4 dtn = depth_consts_at(K, ko - (1u << 5));
         const float4 dtc = depth_consts_at(K, ko);
-        const float leaf1 = depth_word_at(K, ko, 4u);   // depth_leaf(K, d + 1)
-        const float leafc = lod_cull ? leaf1 : __builtin_inff();
         const float sm = bc == 3u ? dtn.z : 1.0f;
         const float b0 = b[0] * sm, b1 = b[1] * sm, b2 = b[2] * sm;
         const float x = ((p0.x * b0 + p1.x * b1) + p2.x * b2) + pc.x * b[3];
@@ -1231,9 +1229,9 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float mk = __builtin_fminf(__builtin_fminf(ca, reg), __builtin_fminf(X, Y));
         uint32_t M = (uint32_t)(wave_ballot(!(mk > 0.0f)) >> 32) & 0x1ffu;
         M = __builtin_amdgcn_readfirstlane(M);
-        leafm = (uint32_t)(wave_ballot(w > leafc) >> 32) & 0x1ffu;
         // entry order as bit order: the front children (nearer than this node's centre along the cone axis) at
-        // bits 0..8, the others at 9..17 -- one find-first-set per child picks the next
+        // bits 0..8, the others at 16..24 -- one find-first-set per child picks the next, and its low 4 bits are
+        // the child's number
         // (index order, front_first false: every child "front" -- an OR with a per-traversal mask, not a branch)
         // (kp = (pc.x ax + pc.y ay) + pc.z az, the node's own projection: the caller passes the axis lane's tca of the
         // node, the same operations on the same operands -- the cone axis IS that lane's direction)
@@ -1257,15 +1255,15 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             }
             return 0u;
         }
-        return (M & front) | ((M & ~front) << 9);
+        return (M & front) | ((M & ~front) << 16);
     };
 
-    uint32_t stk_pc = 0u, stk_ix = 0u;   // VGPR stack, lane k = level k: {untested | leaf << 18}, idxB
+    uint32_t stk_pc = 0u, stk_ix = 0u;   // VGPR stack, lane k = level k: untested children, idxB
     float* tcur = L.table(0u);           // uniform: L.table(d), moved at push / pop (not formed per child)
     uint32_t kofs = 1u << 5;             // uniform: byte offset of depth d + 1's constants, moved likewise
     float R2c = depth_consts_at(K, kofs).x;   // uniform: depth d + 1's bounding radius^2, reloaded likewise
-    uint32_t C = 0u, leafN = 0u;         // uniform: the open node's untested children in entry order (child i at bit
-                                         // i if it is a front child, else at bit 9 + i); its inline-leaf children
+    uint32_t C = 0u;                     // uniform: the open node's untested children in entry order (child i at bit
+                                         // i if it is a front child, else at bit 16 + i)
     float actv;                          // per lane: +inf if the lane visits the open node, -1 otherwise
     uint32_t actbits;                    // per lane: bit k set if the lane visits the open node's level-k ancestor
     {
@@ -1277,7 +1275,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float d2 = pc.w - tca * tca;
         self_test(pc, tca, d2, 0u, actv, 0u, depth_consts(K, 0u).y);
         if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u)))))
-            C = expand(pc, L.root() + 4u, 4u, 0u, actv, leafN, tcur, kofs, readlane_f(tca, axl));
+            C = expand(pc, L.root() + 4u, 4u, 0u, actv, tcur, kofs, readlane_f(tca, axl));
         else SF_COUNT(4, 1);
         if constexpr (SPLIT) {
             if (split_depth == 1u) C &= split_mask(split_q, 1u);
@@ -1292,7 +1290,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         if (C) {
             const uint32_t p = __builtin_ctz(C);
             __asm__("s_bitset0_b32 %0, %1" : "+s"(C) : "s"(p));   // (one scalar op; C &= C - 1 is two)
-            const uint32_t c = min(p, p - 9u);   // (p < 9: front child p; else child p - 9)
+            const uint32_t c = p & 15u;   // (front child p, or child p - 16)
             // the children's depth constants (scalar loads, in flight with the centre's LDS read)
             const float4 dc = depth_consts_at(K, kofs);
             lds_fence();
@@ -1347,7 +1345,11 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             const float avx = sel_mask(-1.0f, __builtin_inff(), amx);
             self_test(pc, tca, d2, d + 1u, avx, idxB + c, dc.y);
             SF_STAMP(4);
-            if ((leafN >> c) & 1u) {   // an inline leaf: its own sphere only (sfhost::leaf_threshold)
+            // an inline leaf -- its own sphere only (sfhost::leaf_threshold): |c|^2 beyond depth d + 1's leaf
+            // threshold; the centre's w is broadcast, so one compare is the branch (round 5: no per-level leaf mask
+            // formed at the expansion and carried through the stack)
+            const float leafc = lod_cull ? depth_word_at(K, kofs, 4u) : __builtin_inff();
+            if (wave_ballot(pc.w > leafc) != 0ull) {
                 SF_COUNT(4, 1);
                 SF_COUNT(8, 1);
                 SF_COUNT(9, __builtin_popcountll(amx));
@@ -1355,7 +1357,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
                 continue;
             }
             // push the open node, open child c
-            stk_pc = writelane_s(C | (leafN << 18), d, stk_pc);
+            stk_pc = writelane_s(C, d, stk_pc);
             stk_ix = writelane_s(idxB, d, stk_ix);
             {
                 const uint32_t bit = 2u << d;   // level d + 1
@@ -1370,7 +1372,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             const float* const col = tcur + SF_LDS_PLANE + 3u * c;   // the entered child's axis columns
             tcur += SF_LDS_LEVEL;
             kofs += 1u << 5;
-            C = expand(pc, col, SF_LDS_COLS, d, avx, leafN, tcur, kofs, readlane_f(tca, axl));
+            C = expand(pc, col, SF_LDS_COLS, d, avx, tcur, kofs, readlane_f(tca, axl));
             if constexpr (SPLIT) {   // (the children are at depth d + 1)
                 if (d + 1u == split_depth) C &= split_mask(split_q, idxB);
             }
@@ -1387,7 +1389,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
                 __builtin_amdgcn_sched_barrier(0);   // (not interleaved with the expansion: register pressure)
                 const uint64_t actm = wave_ballot(avx > 0.0f);
                 const uint32_t na = (uint32_t)__builtin_popcountll(actm);
-                const uint32_t M = (C | (C >> 9)) & 0x1ffu;   // the untested children by index
+                const uint32_t M = (C | (C >> 16)) & 0x1ffu;   // the untested children by index
                 if (na <= 7u && __builtin_popcount(M) >= 3) {
                     const float R2b = depth_consts(K, d + 1u).x;
                     // pack through the level's E words (unused by this traversal): visiting lane of rank k writes its
@@ -1415,7 +1417,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
                     const uint64_t grp = (bal >> (7u * kk)) & 0x7full;
                     const uint32_t hitm = (uint32_t)wave_ballot(ln < 9u && grp != 0ull) & 0x1ffu;
                     const uint32_t keep = __builtin_amdgcn_readfirstlane(hitm);
-                    C &= keep | (keep << 9);
+                    C &= keep | (keep << 16);
                 }
             }
             SF_STAMP(6);
@@ -1430,8 +1432,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         R2c = depth_consts_at(K, kofs).x;
         {
             const uint32_t pw = __builtin_amdgcn_readlane(stk_pc, d);
-            C = pw & 0x3ffffu;
-            leafN = pw >> 18;
+            C = pw;
             idxB = (uint32_t)__builtin_amdgcn_readlane(stk_ix, d);
         }
         actv = ((actbits >> d) & 1u) ? __builtin_inff() : -1.0f;
