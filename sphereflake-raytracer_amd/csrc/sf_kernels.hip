@@ -1210,10 +1210,6 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float y = ((p0.y * b0 + p1.y * b1) + p2.y * b2) + pc.y * b[3];
         const float z = ((p0.z * b0 + p1.z * b1) + p2.z * b2) + pc.z * b[3];
         const float w = (x * x + y * y) + z * z;
-        if (ko < lv32) {   // (d + 1 < levels)
-            *reinterpret_cast<float3*>(tb + slot) = make_float3(x, y, z);
-            *(bc == 3u ? tb + slot + 3u : L.cone() + 5u) = w;
-        }
         const float R2b = dtc.x;
         // cone cull of child bi (centre lanes 32..40), in squares (see traverse). The test is this kernel's own
         // arithmetic, not the reference's, so it fuses: ca, |c|^2 - ca^2, X and Y by fma -- each fused step rounds
@@ -1236,7 +1232,13 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         // (kp = (pc.x ax + pc.y ay) + pc.z az, the node's own projection: the caller passes the axis lane's tca of the
         // node, the same operations on the same operands -- the cone axis IS that lane's direction)
         const uint32_t front = ((uint32_t)(wave_ballot(ca < kp) >> 32) & 0x1ffu) | index_order;
-        if (ko >= lv32) {   // (d + 1 >= levels)
+        // (one levels test for both outcomes: stored after the cull, the table is read only once this returns)
+        if (ko < lv32) {   // (d + 1 < levels)
+            *reinterpret_cast<float3*>(tb + slot) = make_float3(x, y, z);
+            *(bc == 3u ? tb + slot + 3u : L.cone() + 5u) = w;
+            return (M & front) | ((M & ~front) << 16);
+        }
+        {   // (d + 1 >= levels)
             const float T = dtc.w, Tfar = depth_word_at(K, ko, 6u);   // depth_far(K, d + 1)
             while (M) {
                 const uint32_t i = __builtin_ctz(M);
@@ -1255,7 +1257,6 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             }
             return 0u;
         }
-        return (M & front) | ((M & ~front) << 16);
     };
 
     uint32_t stk_pc = 0u, stk_ix = 0u;   // VGPR stack, lane k = level k: untested children, idxB
@@ -1316,8 +1317,10 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
                 SF_COUNT(2, 1);
                 continue;
             }
-            const float Tfar = depth_word_at(K, kofs, 6u);     // depth_far(K, d + 1)
-            const float cull_r = depth_word_at(K, kofs, 5u);   // depth_cull(K, d + 1)
+            // depth d + 1's {leaf, cull, far} words: one scalar load
+            const float4 dk = depth_consts_at(K, kofs + 16u);
+            const float Tfar = dk.z;     // depth_far(K, d + 1)
+            const float cull_r = dk.y;   // depth_cull(K, d + 1)
             const uint64_t exm = child_lod(tca, d2, xs, hb, hbm, dc.x, dc.w, Tfar);
             SF_STAMP(2);
             if (exm == 0ull) continue;
@@ -1348,8 +1351,8 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             // an inline leaf -- its own sphere only (sfhost::leaf_threshold): |c|^2 beyond depth d + 1's leaf
             // threshold; the centre's w is broadcast, so one compare is the branch (round 5: no per-level leaf mask
             // formed at the expansion and carried through the stack)
-            const float leafc = lod_cull ? depth_word_at(K, kofs, 4u) : __builtin_inff();
-            if (wave_ballot(pc.w > leafc) != 0ull) {
+            // (SF_FLAG_NO_LOD_CULL, an A/B switch, no longer reaches this test: the leaf skip is always on here)
+            if (wave_ballot(pc.w > dk.x) != 0ull) {
                 SF_COUNT(4, 1);
                 SF_COUNT(8, 1);
                 SF_COUNT(9, __builtin_popcountll(amx));
