@@ -62,7 +62,8 @@
 // unit} (<= 4 units per tile), per wave {start, end}
 #define SF_TRACE_WORDS(ntiles) ((size_t)(ntiles) * 15u + SF_DIAG_SLOTS + 2u * SF_DIAG_WAVES)
 
-#define SF_FLAG_NO_LOD_CULL 1u    // disable the leaf-threshold skip (A/B only; results identical)
+#define SF_FLAG_NO_LOD_CULL 1u    // disable the leaf-threshold skip (A/B only; results identical; since round 5 the
+                                  // frame-less packet traversal only -- the full-frame traversal always skips)
 #define SF_FLAG_NO_CONE_CULL 2u   // disable the per-child ray-cone cull (A/B only; results identical)
 // diagnostics (schedule studies): trace only one half unit of every 8x8 tile -- pixel rows 0-3, or
 // with SF_FLAG_DIAG_HALF_SEL rows 4-7. Other pixels are not written. Never set by the product path.

@@ -1072,7 +1072,6 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
     const bool cone_cull = (K_flags & SF_FLAG_NO_CONE_CULL) == 0u;
     const bool occl_cull = (K_flags & SF_FLAG_NO_OCCL_CULL) == 0u;
     const bool front_first = (K_flags & (SF_FLAG_NO_OCCL_CULL | SF_FLAG_NO_FRONT_FIRST)) == 0u;
-    const bool lod_cull = (K_flags & SF_FLAG_NO_LOD_CULL) == 0u;
     SF_STAMP_DECL;
 
     h.minT = FLT_MAX;
@@ -1275,7 +1274,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float tca = (pc.x * dx + pc.y * dy) + pc.z * dz;
         const float d2 = pc.w - tca * tca;
         self_test(pc, tca, d2, 0u, actv, 0u, depth_consts(K, 0u).y);
-        if (!(lod_cull && __builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u)))))
+        if (!__builtin_amdgcn_readfirstlane((int)(pc.w > depth_leaf(K, 0u))))
             C = expand(pc, L.root() + 4u, 4u, 0u, actv, tcur, kofs, readlane_f(tca, axl));
         else SF_COUNT(4, 1);
         if constexpr (SPLIT) {
@@ -1351,7 +1350,7 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
             // an inline leaf -- its own sphere only (sfhost::leaf_threshold): |c|^2 beyond depth d + 1's leaf
             // threshold; the centre's w is broadcast, so one compare is the branch (round 5: no per-level leaf mask
             // formed at the expansion and carried through the stack)
-            // (SF_FLAG_NO_LOD_CULL, an A/B switch, no longer reaches this test: the leaf skip is always on here)
+            // (the leaf skip is always on in this traversal: SF_FLAG_NO_LOD_CULL is the packet traversal's A/B switch)
             if (wave_ballot(pc.w > dk.x) != 0ull) {
                 SF_COUNT(4, 1);
                 SF_COUNT(8, 1);
