@@ -15,6 +15,7 @@
  * Built by scripts/experiments/wave_sim.py against oracle/sf_oracle.c (included).
  */
 #include <stdlib.h>
+#include <stdio.h>
 #include <float.h>
 #include "../../oracle/sf_oracle.c"
 
@@ -85,6 +86,12 @@ typedef struct {
     double part_work[8];     /* this tile's work per part (child iterations + 6 per expansion) */
     double shared_work;      /* work above depth k (every part repeats it) */
     int solo;                /* >= 0: trace only part `solo` of the subtree split (its own wave: no other part's hits) */
+    double slack;
+    float cone_k;
+    double pl[4][3];
+    float fn[4][3], fbeta, fs, fbh, fbc;
+    int npairs, pairs[4][2];   /* mode 128: the kernel's fp32 frustum (normals, beta, slack) */
+    long long fr_culled;         /* mode 32: the tile pyramid's side planes (inward unit normals, through the origin) */
 } wsim_t;
 
 static int is_anc(uint64_t a, uint64_t n)
@@ -167,11 +174,76 @@ static void expand_node(wsim_t* S, const float* M, int d, uint64_t node, uint64_
         float q = w - ca * ca; if (q < 0.0f) q = 0.0f;
         float sq = sqrtf(q);
         float X = sq * cosT - ca * sinT;
-        float Y = X * X - (R2b + w * (0x1p-18f + 0x1p-19f));
+        float Y = X * X - (R2b + w * S->cone_k);
         float a1 = ca < w - 2.0f * (R2b + dl) ? ca : w - 2.0f * (R2b + dl);
         float a2 = X < Y ? X : Y;
         float mk = a1 < a2 ? a1 : a2;
         culled[i] = mk > 0.0f;
+        if (S->mode & 4096) culled[i] = 0;   /* no cone (mode 128 alone: the frustum replaces it) */
+        if ((S->mode & 128) && !culled[i]) {   /* the planned kernel test, in fp32 */
+            /* the kernel's arithmetic (traverse_ray expand): R2bq = depth word 7, beta_h = plane.w */
+            const float R2bq = nextafterf((float)((double)R2b * (1.0 + 0x1p-16)), FLT_MAX);
+            const float Pq = sqrtf(fmaf(0x1.0001p-19f, w, R2bq));
+            const float bh = S->fbeta;
+            float dk[4];
+            for (int k = 0; k < 4; ++k)
+                dk[k] = fmaf(S->fn[k][2], C[2], fmaf(S->fn[k][1], C[1], fmaf(S->fn[k][0], C[0], bh)));
+            const float vA = fminf(dk[0], dk[1]) + fmaf(bh, w, Pq);
+            const float vB = fminf(dk[2], dk[3]) + fmaf(bh, w, Pq);
+            if (vA < 0.0f || vB < 0.0f) { culled[i] = 1; st->skip_lost[d]++; }
+            else if (getenv("DBGC") && mk > 0.0f) {
+                static int nprint = 0;
+                if (nprint++ < 12) fprintf(stderr, "cone-only d %d w %g R2b %g dk %g %g %g %g bh %g Pq %g ca %g X %g Y %g\n", d, w, R2b,
+                    dk[0], dk[1], dk[2], dk[3], bh, Pq, ca, X, Y);
+            }
+        }
+        if ((S->mode & 8192) && !culled[i]) {   /* plane pairs with the corner bound (kernel arithmetic, fp32) */
+            const float R2bq = nextafterf((float)((double)R2b * (1.0 + 0x1p-16)), FLT_MAX);
+            const float P2 = fmaf(0x1.0001p-19f, w, R2bq);
+            float dk[4], ak[4];
+            for (int k = 0; k < 4; ++k) {
+                dk[k] = fmaf(S->fn[k][2], C[2], fmaf(S->fn[k][1], C[1], fmaf(S->fn[k][0], C[0], S->fbc)));
+                dk[k] = fmaf(S->fbh, w, dk[k]);
+                ak[k] = -dk[k] > 0.0f ? -dk[k] : 0.0f;
+            }
+            int cull = 0;
+            for (int pi = 0; pi < S->npairs; ++pi) {
+                const int A = S->pairs[pi][0], B = S->pairs[pi][1];
+                const float q = fmaf(ak[A], ak[A], ak[B] * ak[B]);
+                if (q > P2) cull = 1;
+            }
+            if (cull) { culled[i] = 1; st->skip_lost[d]++; }
+        }
+        if ((S->mode & 64) && !culled[i]) {   /* the ideal cone cull: exact arithmetic, no slack */
+            double cx = C[0], cy = C[1], cz = C[2];
+            double cad = cx * ax[0] + cy * ax[1] + cz * ax[2];
+            double px = cy * ax[2] - cz * ax[1], py = cz * ax[0] - cx * ax[2], pz = cx * ax[1] - cy * ax[0];
+            double perp = sqrt(px * px + py * py + pz * pz);
+            double sT = sinT, cT = sqrt(1.0 - (double)sinT * sinT);
+            if (sinT < 1.0f) {
+                double X = perp * cT - cad * sT;   /* distance of the centre from the cone surface */
+                double R = sqrt((double)R2b + (double)w * S->slack) * (1.0 + 0x1p-12) + sqrt((double)w) * 0x1p-20;
+                if (X > R && cad > 0) { culled[i] = 1; st->skip_lost[d]++; }
+            }
+        }
+        if ((S->mode & 32) && !culled[i]) {   /* frustum: outside some side plane by more than R (1 + 2^-12) */
+            const double R = sqrt((double)R2b + (double)w * S->slack) * (1.0 + 0x1p-12) + sqrt((double)w) * 0x1p-20;
+            for (int k = 0; k < 4; ++k) {
+                double dd = S->pl[k][0] * C[0] + S->pl[k][1] * C[1] + S->pl[k][2] * C[2];
+                if (dd < -R) {
+                    culled[i] = 1; st->skip_lost[d]++;
+                    if (getenv("DBG")) for (int l = 0; l < 64; ++l) {
+                        const float* D = S->D[l];
+                        float tca = (C[0] * D[0] + C[1] * D[1]) + C[2] * D[2];
+                        float d2 = w - tca * tca;
+                        if (tca >= 0.0f && d2 <= R2b && ((A >> l) & 1))
+                            fprintf(stderr, "lane %d plane %d dd %g R %g d %d w %g d2 %g R2b %g pn %g\n", l, k, dd, R, d, w, d2, R2b,
+                                    S->pl[k][0] * D[0] + S->pl[k][1] * D[1] + S->pl[k][2] * D[2]);
+                    }
+                    break;
+                }
+            }
+        }
         leaf[i] = w > S->leaf[dc];
         front[i] = ca < kp;
         st->cone_tested[d]++;
@@ -235,6 +307,8 @@ int wsim_tiles(uint32_t W, uint32_t H, const float o[3], const float tl[3], cons
     S.child = child; S.lut = lut; S.mode = mode; S.st = st;
     S.skip_k = 0x1p-9f; S.skip_f = 4.0f;
     S.part = (mode >> 8) & 7;
+    S.cone_k = getenv("CONE_K") ? strtof(getenv("CONE_K"), NULL) : (0x1p-18f + 0x1p-19f);
+    S.slack = getenv("SLACK") ? strtod(getenv("SLACK"), NULL) : 0x1p-20;
     S.solo = getenv("SOLO") ? atoi(getenv("SOLO")) : -1;
     if (getenv("SKIP_K")) S.skip_k = strtof(getenv("SKIP_K"), NULL);
     if (getenv("SKIP_F")) S.skip_f = strtof(getenv("SKIP_F"), NULL);
@@ -283,6 +357,71 @@ int wsim_tiles(uint32_t W, uint32_t H, const float o[3], const float tl[3], cons
         float sm = sqrtf(smax) * (1.0f + 0x1p-16f) + 0x1p-16f;
         S.sinT = 1.0f; S.cosT = 0.0f;
         if (sm < 0.5f) { S.sinT = sm; S.cosT = sqrtf(1.0f - sm * sm) * (1.0f - 0x1p-16f); }
+        {   /* mode 32: pyramid of the valid lanes' extreme rays: corners of the tile's valid pixel rectangle */
+            int xs = 7, ys = 7;
+            while (xs > 0 && tx * 8 + xs >= W) xs--;
+            while (ys > 0 && ty * 8 + ys >= H) ys--;
+            const float* Cn[4] = { S.D[0], S.D[xs], S.D[ys * 8 + xs], S.D[ys * 8] };
+            for (int k = 0; k < 4; ++k) {
+                const float* a = Cn[k]; const float* b = Cn[(k + 1) & 3];
+                double n0 = (double)a[1] * b[2] - (double)a[2] * b[1], n1 = (double)a[2] * b[0] - (double)a[0] * b[2],
+                       n2 = (double)a[0] * b[1] - (double)a[1] * b[0];
+                double nn = sqrt(n0 * n0 + n1 * n1 + n2 * n2);
+                /* orient inward: the tile centre ray on the positive side */
+                const float* c = S.D[36];
+                double sg = n0 * c[0] + n1 * c[1] + n2 * c[2];
+                if (sg < 0) nn = -nn;
+                S.pl[k][0] = n0 / nn; S.pl[k][1] = n1 / nn; S.pl[k][2] = n2 / nn;
+            }
+        }
+        if (mode & (128 | 8192)) {   /* the planned kernel's per-tile frustum, fp32 */
+            const int cidx[4] = { 0, 7, 63, 56 };
+            float mneg = 0.0f, dmax = 0.0f;
+            for (int k = 0; k < 4; ++k) {
+                const float* a = S.D[cidx[k]]; const float* b = S.D[cidx[(k + 1) & 3]];
+                float n0 = a[1] * b[2] - a[2] * b[1], n1 = a[2] * b[0] - a[0] * b[2], n2 = a[0] * b[1] - a[1] * b[0];
+                const float* c = S.D[36];
+                float sg = (n0 * c[0] + n1 * c[1]) + n2 * c[2];
+                float nn = (n0 * n0 + n1 * n1) + n2 * n2;
+                float r = 1.0f / sqrtf(nn);
+                if (sg < 0.0f) r = -r;
+                S.fn[k][0] = n0 * r; S.fn[k][1] = n1 * r; S.fn[k][2] = n2 * r;
+                for (int l = 0; l < 64; ++l) {
+                    const float* D = S.D[l];
+                    float v = (S.fn[k][0] * D[0] + S.fn[k][1] * D[1]) + S.fn[k][2] * D[2];
+                    if (-v > mneg) mneg = -v;
+                }
+            }
+            for (int l = 0; l < 64; ++l) {
+                const float* D = S.D[l];
+                float e = fmaf(D[2], D[2], fmaf(D[1], D[1], fmaf(D[0], D[0], -1.0f)));
+                if (e > dmax) dmax = e;
+            }
+            S.fbeta = (mneg + 0x1p-19f) * 0x1.00002p-1f;   /* beta_h */
+            {   /* pair mode: beta' = mneg + 2^-19; t <= (1 + 2^-9)(w + 1)/2 + 2 */
+                const float bp = mneg + 0x1p-19f;
+                S.fbh = bp * 0x1.01p-1f;
+                S.fbc = S.fbh + 2.0f * bp;
+                const char* pe = getenv("PAIRS") ? getenv("PAIRS") : "01,23";
+                S.npairs = 0;
+                for (const char* q = pe; *q && S.npairs < 4; ) {
+                    S.pairs[S.npairs][0] = q[0] - '0'; S.pairs[S.npairs][1] = q[1] - '0'; S.npairs++;
+                    q += 2; if (*q == ',') q++;
+                }
+                float kap = 0.0f;
+                for (int pi = 0; pi < S.npairs; ++pi) {
+                    const float* u = S.fn[S.pairs[pi][0]]; const float* v = S.fn[S.pairs[pi][1]];
+                    float cdot = fabsf((u[0] * v[0] + u[1] * v[1]) + u[2] * v[2]);
+                    if (cdot > kap) kap = cdot;
+                }
+                const float sig = (1.0f - (kap + 0x1p-20f)) * (1.0f - 0x1p-20f);
+                if (getenv("DBGK") && t == t0) fprintf(stderr, "kappa %g\n", kap);
+                for (int k = 0; k < 4; ++k) { S.fn[k][0] *= sig; S.fn[k][1] *= sig; S.fn[k][2] *= sig; }
+                S.fbh *= sig; S.fbc *= sig;
+            }
+            S.fs = (0x1p-20f + 0x1p-22f + dmax) * (1.0f + 0x1p-16f);
+            if (getenv("DBGF")) fprintf(stderr, "tile %u mneg %g dmax %g (u %g)\n", t, mneg, dmax, 0x1p-24);
+        }
         /* root */
         S.split_k = split_k; S.split_p = split_p; S.cur_part = -1; S.shared_work = 0.0;
         for (int q = 0; q < 8; ++q) S.part_work[q] = 0.0;
