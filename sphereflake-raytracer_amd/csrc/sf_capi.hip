@@ -1417,6 +1417,9 @@ int sf_progressive(sf_ctx* c, uint32_t seed, uint64_t counter0, uint32_t packets
 int sf_synchronize(sf_ctx* c)
 {
     if (!c) return SF_EINVAL;
+    // nothing enqueued since the last check (every call that enqueues work joins first, ctx_join): no runtime
+    // call at all -- a multi-slot caller (sf_dist_synchronize) waits only for the slots that have work
+    if (!c->stats_dirty) return c->unresolved != 0 ? SF_EDEPTH : SF_OK;
     DevGuard g(c->device);
     // (after only traces that cannot change the unresolved word, the last check's value stands: no copy)
     const bool check = c->stats_dirty && c->stats_unknown;
