@@ -11,9 +11,9 @@ for rep in $(seq 1 ${REPS:-2}); do
     i=$((i+1))
     E=${v%%|*}; A=${v#*|}; [ "$A" = "$v" ] && A=""
     for st in "200 30" "20 5"; do
-      set -- $st
-      env $E timeout -k 10 150 python3 -u bench.py --no-cpu-baseline --no-extras --steps $1 --warmup $2 $A > $OUT/v$i.json 2> $OUT/v$i.err
-      python3 -c "import json; j=json.loads(open('$OUT/v$i.json').read().strip().split(chr(10))[-1]); print('[$v] steps $1', 'frame', j['frame_ms'], 'steady', j['pipeline']['steady_frame_ms'], 'lat', j['frame_latency_ms'], 'clk', j['roofline'].get('clock_mhz_live'))"
+      S=${st% *}; W=${st#* }
+      env $E timeout -k 10 150 python3 -u bench.py --no-cpu-baseline --no-extras --steps $S --warmup $W $A > $OUT/v$i.json 2> $OUT/v$i.err
+      python3 -c "import json; j=json.loads(open('$OUT/v$i.json').read().strip().split(chr(10))[-1]); print('[$v] steps $S', 'frame', j['frame_ms'], 'steady', j['pipeline']['steady_frame_ms'], 'lat', j['frame_latency_ms'], 'clk', j['roofline'].get('clock_mhz_live'))"
     done
   done
 done
