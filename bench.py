@@ -162,8 +162,9 @@ CPU_REPS = 40                        # ~1.2 s wall x 16 threads: ~20 s of CPU wo
 
 
 def ktiming_period(steps):
-    """Every k-th timed render carries the kernel-timing events: k = 10 (an event pair costs ~7 us of stream
-    time per frame, so it is sampled), or less when that would give fewer than KTIMING_MIN_SAMPLES samples."""
+    """Every k-th timed render carries the kernel-timing events: k = 10 (sampled, to keep them off the frame
+    period), or less when that would give fewer than KTIMING_MIN_SAMPLES samples. (Round 5: the driver's 20-step
+    line measured the same with 11 or 5 samples, profiles/r5/order/kt_samples_ab.txt.)"""
     return max(1, min(KTIMING_PERIOD, steps // KTIMING_MIN_SAMPLES))
 
 
