@@ -258,6 +258,40 @@ def cpu_share():
     return avail, quota
 
 
+def cpu_model(text=None):
+    """(model name, vendor) of the host CPU from /proc/cpuinfo (state the CPU model) -- the
+    first "model name" and "vendor_id" lines; None where absent (e.g. a non-x86 kernel's format)."""
+    if text is None:
+        try:
+            with open("/proc/cpuinfo") as f:
+                text = f.read()
+        except OSError:
+            return None, None
+    model = vendor = None
+    for line in text.splitlines():
+        key, _, val = line.partition(":")
+        key = key.strip()
+        if key == "model name" and model is None:
+            model = " ".join(val.split())
+        elif key == "vendor_id" and vendor is None:
+            vendor = val.strip()
+        if model is not None and vendor is not None:
+            break
+    return model, vendor
+
+
+def cpu_identity():
+    """cpu_model / vendor keys of the baseline, with the parity caveat where the host is not Intel: the oracle's
+    rsqrtps table was measured on Intel, AMD's rsqrtps returns other estimates, so the reference
+    build's frames on such a host differ from the fixtures and its baseline there is timing-only."""
+    model, vendor = cpu_model()
+    out = {"cpu_model": model, "vendor": vendor}
+    if vendor != "GenuineIntel":
+        out["note"] = ("timing-only: not an Intel host, and x86 rsqrtps estimates differ by vendor (the fixtures "
+                       "and the GPU path follow the Intel table, SURVEY.md §8(c)); parity is GPU vs committed fixtures")
+    return out
+
+
 def cpu_baseline(width, height, k, threads):
     """The reference AVX packet path (oracle/_ref/ref_bench, built from /root/reference) on host cores.
     Falls back to the oracle C restatement (per ray, 1 thread) if the reference build is absent."""
@@ -273,7 +307,7 @@ def cpu_baseline(width, height, k, threads):
                           f"pixel coverage), median; reference AVX path -O3 -mavx, {threads} threads",
                 "frame_ms": round(r["median_s"] * 1e3, 2),
                 "single_thread": {"value": round(r1["mrays_per_s"], 3), "frame_ms": round(r1["median_s"] * 1e3, 1),
-                                  "sample": "3 full frames, 1 thread"}}
+                                  "sample": "3 full frames, 1 thread"}, **cpu_identity()}
     setup = {"W": width, "H": height}
     cam = sf.config_camera(width, height, k)
     o, tl, tr, bl = cam.corners()
@@ -283,7 +317,8 @@ def cpu_baseline(width, height, k, threads):
     pyoracle.render(setup, rows=rows, threads=1)
     dt = time.perf_counter() - t0
     return {"value": round(len(rows) * width / dt / 1e6, 3), "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"every 8th row of a {width}x{height} K={k} frame, oracle C restatement, 1 thread"}
+            "sample": f"every 8th row of a {width}x{height} K={k} frame, oracle C restatement, 1 thread",
+            **cpu_identity()}
 
 
 POST_BYTES_PER_PIXEL = 36   # fused pass: position + normal in (32 B), RGBA8 out (4 B)

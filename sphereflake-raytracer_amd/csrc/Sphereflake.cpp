@@ -17,40 +17,37 @@ static void Check(int rc)
 
 void Sphereflake::Check(int rc) { SphereflakeRaytracer::Check(rc); }
 
-Sphereflake::Sphereflake(size_t width, size_t height, int device) : m_Width(width), m_Height(height)
+void Sphereflake::Open(int device, float* positions, float* normals)
 {
-    Check(sf_create(device, (uint32_t)width, (uint32_t)height, &m_Ctx));
-    // reference: m_GBuffer.positions/normals.resize(W*H) of zero vec4 (Sphereflake.cpp:48-49)
-    m_GBuffer.positions.resize(width * height);
-    m_GBuffer.normals.resize(width * height);
+    Check(sf_create(device, (uint32_t)m_Width, (uint32_t)m_Height, &m_Ctx));
+    m_Positions = positions;
+    m_Normals = normals;
     // page-lock the vectors' storage (they stay std::vector for the PBO upload, GLPixelBufferObject.h:24-29)
     // so GetGBuffer's D2H runs as DMA straight into them; not fatal when the host refuses to pin
-    const size_t bytes = width * height * sizeof(sf_vec4);
-    m_Pinned = bytes && sf_host_register(m_GBuffer.positions.data(), bytes) == SF_OK &&
-               sf_host_register(m_GBuffer.normals.data(), bytes) == SF_OK;
+    const size_t bytes = m_Width * m_Height * 16;
+    m_Pinned = bytes && sf_host_register(m_Positions, bytes) == SF_OK && sf_host_register(m_Normals, bytes) == SF_OK;
 }
 
-Sphereflake::~Sphereflake()
+void Sphereflake::Close() noexcept
 {
     m_Deinitialize = true;
     if (m_Worker.joinable()) m_Worker.join();
     const int rc = m_WorkerError.exchange(SF_OK);
     if (rc != SF_OK) std::fprintf(stderr, "sphereflake: frame-less loop failed: %s\n", sf_strerror(rc));
     sf_destroy(m_Ctx);
+    m_Ctx = nullptr;
     if (m_Pinned) {
-        sf_host_unregister(m_GBuffer.positions.data());
-        sf_host_unregister(m_GBuffer.normals.data());
+        sf_host_unregister(m_Positions);
+        sf_host_unregister(m_Normals);
+        m_Pinned = false;
     }
 }
 
-void Sphereflake::SetView(const sf_vec3& origin, const sf_vec3& topLeft, const sf_vec3& topRight, const sf_vec3& bottomLeft)
+void Sphereflake::SetViewFloats(const float origin[3], const float topLeft[3], const float topRight[3],
+                                const float bottomLeft[3])
 {
     std::lock_guard<FairMutex> lk(m_Mutex);
-    const float o[3] = { origin.x, origin.y, origin.z };
-    const float tl[3] = { topLeft.x, topLeft.y, topLeft.z };
-    const float tr[3] = { topRight.x, topRight.y, topRight.z };
-    const float bl[3] = { bottomLeft.x, bottomLeft.y, bottomLeft.z };
-    Check(sf_set_view(m_Ctx, o, tl, tr, bl));
+    Check(sf_set_view(m_Ctx, origin, topLeft, topRight, bottomLeft));
     m_ViewChange = m_SobolCounter;
 }
 
@@ -133,15 +130,14 @@ uint64_t Sphereflake::GetViewChangePacket() const
     return m_ViewChange;
 }
 
-const GBuffer& Sphereflake::GetGBuffer() const
+void Sphereflake::Refresh() const
 {
     ThrowWorkerError();
     std::lock_guard<FairMutex> lk(m_Mutex);
     if (m_Stale) {
-        Check(sf_download(m_Ctx, &m_GBuffer.positions[0].x, &m_GBuffer.normals[0].x, nullptr, nullptr));
+        Check(sf_download(m_Ctx, m_Positions, m_Normals, nullptr, nullptr));
         m_Stale = false;
     }
-    return m_GBuffer;
 }
 
 int Sphereflake::GetMaxDepthReached() const
@@ -198,11 +194,9 @@ SSAO::SSAO(Sphereflake& flake, int downScale) : m_Flake(flake)
     m_Params.downscale = (uint32_t)downScale;
 }
 
-void SSAO::SetCameraPosition(const sf_vec3& p)
+void SSAO::SetCameraPositionFloats(const float p[3])
 {
-    m_Params.camera_position[0] = p.x;
-    m_Params.camera_position[1] = p.y;
-    m_Params.camera_position[2] = p.z;
+    std::memcpy(m_Params.camera_position, p, sizeof m_Params.camera_position);
     m_CameraSet = true;
 }
 

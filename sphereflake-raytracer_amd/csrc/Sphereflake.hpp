@@ -7,7 +7,11 @@
 //
 // vec3/vec4: when glm is included first (the reference app does, with GLM_FORCE_RADIANS), define
 // SF_USE_GLM and the class uses glm::vec3 / glm::vec4 exactly like the reference. Otherwise a
-// layout-identical POD is used.
+// layout-identical POD is used. The library exports only members whose signatures and bodies do not depend on
+// that choice (the Open / Close / SetViewFloats / Refresh members take float pointers); everything that names
+// the vector types -- the constructor's resize, the destructor, SetView, GetGBuffer -- is inline here, so a
+// glm application links against the same libsphereflake_hip.so and never has its vectors touched as another
+// type (tests/test_integration_build.py links the patched reference main.cpp's object against the library).
 //
 // Differences, all deliberate:
 //   - Rendering is an explicit full frame: Render() traces every pixel once, deterministically.
@@ -82,8 +86,14 @@ private:
 
 class Sphereflake {
 public:
-    Sphereflake(size_t width, size_t height, int device = 0);
-    ~Sphereflake();
+    // reference: m_GBuffer.positions/normals.resize(W*H) of zero vec4 (Sphereflake.cpp:43-55)
+    Sphereflake(size_t width, size_t height, int device = 0) : m_Width(width), m_Height(height)
+    {
+        m_GBuffer.positions.resize(width * height);
+        m_GBuffer.normals.resize(width * height);
+        Open(device, &m_GBuffer.positions[0].x, &m_GBuffer.normals[0].x);
+    }
+    ~Sphereflake() { Close(); }
     Sphereflake(const Sphereflake&) = delete;
     Sphereflake& operator=(const Sphereflake&) = delete;
 
@@ -102,12 +112,23 @@ public:
     // it mid-packet, unsynchronised, Sphereflake.cpp:76-84).
     uint64_t GetViewChangePacket() const;
 
-    void SetView(const sf_vec3& origin, const sf_vec3& topLeft, const sf_vec3& topRight, const sf_vec3& bottomLeft);
+    void SetView(const sf_vec3& origin, const sf_vec3& topLeft, const sf_vec3& topRight, const sf_vec3& bottomLeft)
+    {
+        const float o[3] = { origin.x, origin.y, origin.z }, tl[3] = { topLeft.x, topLeft.y, topLeft.z };
+        const float tr[3] = { topRight.x, topRight.y, topRight.z }, bl[3] = { bottomLeft.x, bottomLeft.y, bottomLeft.z };
+        SetViewFloats(o, tl, tr, bl);
+    }
+    void SetViewFloats(const float origin[3], const float topLeft[3], const float topRight[3], const float bottomLeft[3]);
 
     // One deterministic full frame into the device G-buffer (new; the reference renders implicitly).
     void Render(const sf_render_params* params = nullptr);
 
-    const GBuffer& GetGBuffer() const;
+    // the device frame, downloaded into the vectors when it is newer than their contents (Refresh)
+    const GBuffer& GetGBuffer() const
+    {
+        Refresh();
+        return m_GBuffer;
+    }
     // Headless dump of the device frame (sf_save_image): SF_DUMP_NORMALS / _POSITIONS_PFM / _NORMALS_PFM,
     // or SF_DUMP_IMAGE after an SSAO::Render(). The reference only shows its frame in the GL window.
     void SaveImage(const std::string& path, int what = SF_DUMP_NORMALS) const;
@@ -124,6 +145,9 @@ public:
     size_t Height() const { return m_Height; }
 
 private:
+    void Open(int device, float* positions, float* normals);   // sf_create + page-lock the vectors' storage
+    void Close() noexcept;                                       // join the frame-less loop, sf_destroy, unpin
+    void Refresh() const;                                        // sf_download into m_Positions / m_Normals if stale
     static void Check(int rc);
     void ProgressiveLoop(uint32_t batch);
     void ThrowWorkerError() const;   // rethrows the frame-less loop's first error (held until reported once)
@@ -131,6 +155,8 @@ private:
     size_t m_Width, m_Height;
     sf_ctx* m_Ctx = nullptr;
     mutable GBuffer m_GBuffer;
+    float* m_Positions = nullptr;   // m_GBuffer's storage as the library sees it (W x H float4 each)
+    float* m_Normals = nullptr;
     mutable bool m_Stale = true;
     bool m_Pinned = false;
     mutable FairMutex m_Mutex;

@@ -27,7 +27,12 @@ public:
     // SSAO.h:15-18. Until called, the radius is 8 x the closest-hit stat read on the device.
     void SetSampleRadiusMultiplier(float m) { m_Params.sample_radius = 8.0f * m; }
     // post_final.glsl cameraPosition (main.cpp:325); defaults to the SetView origin at Render time.
-    void SetCameraPosition(const sf_vec3& p);
+    void SetCameraPosition(const sf_vec3& p)
+    {
+        const float f[3] = { p.x, p.y, p.z };
+        SetCameraPositionFloats(f);
+    }
+    void SetCameraPositionFloats(const float p[3]);   // (exported; the vec3 overload is inline, Sphereflake.hpp)
 
     void Render();                                  // SSAO, blur x, blur y, final (asynchronous)
     const std::vector<uint8_t>& GetImage() const;   // D2H of the last Render's image

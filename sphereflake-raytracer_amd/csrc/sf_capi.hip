@@ -146,6 +146,7 @@ struct sf_ctx {
     int fixup_blocks = 256;
     uint32_t waves_per_block = SF_TRACE_WAVES;   // tuning knob: env SF_TRACE_WAVES = 1 | 2 | 4
     uint32_t levels_override = 0;                // tuning knob: env SF_LEVELS (LDS levels, 0 = adaptive)
+    bool slab_shallow = false;                   // tests only: index slabs as SF_PACKED_INDEX_DIAG (env SF_DIAG_SLAB_SHALLOW)
     bool persistent = true;                      // tuning knob: env SF_PERSISTENT=0 -> one workgroup per tile group
     uint32_t flags = 0;                          // SF_FLAG_* A/B switches: env SF_FLAGS
     int cus = 256;
@@ -548,6 +549,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
         const int l = std::atoi(ev);
         c->levels_override = (l >= 2 && l <= SF_MAX_DEPTH_LIMIT) ? (uint32_t)l : 0u;
     }
+    if (const char* ev = std::getenv("SF_DIAG_SLAB_SHALLOW")) c->slab_shallow = std::atoi(ev) != 0;   // (tests only)
     DevGuard g(device);
     const size_t npx = (size_t)width * height;
     const size_t ntiles = (size_t)((width + 7) / 8) * ((height + 7) / 8);
@@ -714,6 +716,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
     if (p.packed > SF_PACKED_INDEX) return SF_EINVAL;
     if (p.packed == SF_PACKED_INDEX && sf_slab_bytes(c) != 4u) return SF_EINVAL;   // (a hit could be too deep)
     a.packed = p.packed;
+    if (a.packed == SF_PACKED_INDEX && c->slab_shallow) a.packed = SF_PACKED_INDEX_DIAG;
     if (a.packed && p.kernel == SF_KERNEL_PER_RAY) return SF_EINVAL;   // (the per-ray kernel writes the plain layout)
     a.emit_aux = p.emit_aux ? 1u : 0u;
     a.pos = pos;
@@ -911,8 +914,10 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
         // levels proven sufficient (persistent kernel) only an exact tie under the front-first child order can
         // flag a tile -- never seen on the BASELINE views --: its own wave re-traces it (tie_inline), or with
         // SF_TIE_INLINE=0 the fixup's small grid.
-        // (no fixup after the trace: nothing is counted as unresolved)
-        unresolved_safe = bounded && c->persistent && !(front_first && !tie_inline);
+        // (no fixup after the trace: nothing is counted as unresolved -- except by an index-slab trace, whose
+        // write_pixel counts a hit too deep for the format (SF_SLAB_BAD): that one must leave stats_unknown set so
+        // sf_synchronize reads the word and reports SF_EDEPTH (VERDICT/ADVICE r5))
+        unresolved_safe = bounded && c->persistent && !(front_first && !tie_inline) && a.packed < SF_PACKED_INDEX;
         if (!(bounded && c->persistent) || (front_first && !tie_inline)) {
             const size_t lds_fix = (size_t)SF_LDS_WAVE_FLOATS(SF_MAX_DEPTH_LIMIT) * 4;
             const uint32_t fb = (bounded && c->persistent) ? 8u : 4u * (uint32_t)c->fixup_blocks;
@@ -1049,6 +1054,10 @@ int sfi_unpack_slabs(sf_ctx* c, const void* stage, uint32_t bytes_per_pixel, uin
     if (join) {
         if (int rc = ctx_join(c, s)) return rc;
     }
+    // work enqueued whatever `join` says: the next sf_synchronize drains and checks (an unpack alone,
+    // without the caller's sfi_join / sf_render beside it, must not meet the idle-sync return)
+    c->stats_dirty = true;
+    c->stats_unknown = true;
     FrameArgs a = frame_args(c);
     a.pos = c->pos;
     a.nrm = c->nrm;

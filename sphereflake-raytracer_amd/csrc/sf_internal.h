@@ -186,6 +186,12 @@ struct FrameArgs {
 #define SF_PACKED_NORMAL 1u
 #define SF_PACKED_INDEX 2u
 #define SF_INDEX_SLAB_DEPTH 10
+// tests only (env SF_DIAG_SLAB_SHALLOW=1): the host launches an index-slab trace as FrameArgs.packed =
+// SF_PACKED_INDEX_DIAG, whose slab carries hits only to depth SF_DIAG_SLAB_DEPTH, so a test view's ordinary hits stand
+// in for a hit too deep for the format (SF_SLAB_BAD, counted as unresolved: sf_synchronize reports SF_EDEPTH). A packed
+// mode, not a flag or a launch argument: write_pixel already holds a.packed, and the product kernel keeps its registers
+#define SF_PACKED_INDEX_DIAG 3u
+#define SF_DIAG_SLAB_DEPTH 4
 #define SF_SLAB_MISS 0xffffffffu
 #define SF_SLAB_BAD 0xfffffffeu
 // node table of the index unpack: the frames of every node of depth <= SF_NODE_TABLE_DEPTH (3 float4 each; 28.7 MB,

@@ -1508,11 +1508,12 @@ __device__ __forceinline__ void write_pixel(const FrameArgs& a, const Tile& t, f
     shade(dx, dy, dz, h, lut, px, py, pz, nx, ny, nz);
     const size_t o = (size_t)t.orow * a.W + t.x;
     if (a.packed) {   // (uniform)
-        if (a.packed == SF_PACKED_INDEX) {
+        if (a.packed >= SF_PACKED_INDEX) {
             // 4 B: the hit's heap index; the receiver rebuilds the rest. (The host selects this format only where
             // no hit can lie deeper than SF_INDEX_SLAB_DEPTH, whose heap indices are below 2^32; a deeper one would
             // be ambiguous and is written as SF_SLAB_BAD instead.)
-            const bool bad = h.hit && h.depth > SF_INDEX_SLAB_DEPTH;
+            const int32_t lim = a.packed == SF_PACKED_INDEX ? SF_INDEX_SLAB_DEPTH : SF_DIAG_SLAB_DEPTH;   // (tests)
+            const bool bad = h.hit && h.depth > lim;
             reinterpret_cast<uint32_t*>(a.pos)[o] = !h.hit ? SF_SLAB_MISS : bad ? SF_SLAB_BAD : h.index;
             // such a pixel counts as unresolved (stats[2]): sf_synchronize then reports SF_EDEPTH instead of the gather
             // silently carrying a NaN pixel (the host's depth proof and the device must never disagree)
@@ -1636,8 +1637,8 @@ __device__ __forceinline__ bool heap_ancestor(uint32_t a, uint32_t n)
 }
 
 // Subtree part records (SF_FLAG_SUBTREE): part q of split slot s at part_rec + (4 s + q) x 192 u64, three 64-lane
-// planes. Stored and loaded with agent scope (sc1: past the writer's and the reader's caches), so that the part that
-// adds last to the tile's counter -- after every part's stores have completed (s_waitcnt vmcnt(0)) -- reads them.
+// planes. Stored and loaded with agent scope (sc1: past the writer's and the reader's caches); each part's add to the
+// tile's counter follows an agent-scope release fence and the merger (the last to add) acquires before reading them.
 __device__ __forceinline__ uint64_t* part_record(const FrameArgs& a, uint32_t slot, uint32_t q)
 {
     return a.part_rec + (size_t)(slot * 4u + q) * 192u;
@@ -1705,7 +1706,9 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(R + 128u + lane, ((uint64_t)(uint32_t)h.depth << 32) | h.index,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // release: the records are visible at agent scope before the counter add that publishes them (the
+        // memory model, not a hand-placed waitcnt, orders the stores before the add; the merger acquires below)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         // counter: parts done (low byte), parts that flagged an overflow (byte 1), a tie (byte 2)
         const uint32_t add = 1u | ((status & SF_STATUS_OVERFLOW) ? 0x100u : 0u) | ((status & SF_STATUS_TIE) ? 0x10000u : 0u);
         const uint32_t st0 = status;
@@ -1713,6 +1716,7 @@ __device__ __forceinline__ TileStats trace_tile(const FrameArgs& a, float* __res
         merger = (old & 0xffu) == 3u;   // the last part; the others are done with this tile (no write, no flag)
         status = 0u;
       if (merger) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other parts' records, published before their adds
         a.part_done[tile] = 0u;   // for the next render (uniform value and address)
         // merge: per pixel the nearest sphere over the parts. An exact tie between two parts' spheres is the
         // reference's ancestor rule where one is the other's ancestor (a node's sphere is tested before its

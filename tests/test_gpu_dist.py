@@ -201,3 +201,86 @@ def test_dist_bands_without_communicators(n):
     finally:
         for d in ranks:
             d.close()
+
+
+def _packed_index_render(s, W, H, n=2, band=8):
+    """Member 1's bands of an n-way split as a 4-B index slab (what a dist peer / group member ships)."""
+    import torch
+    rows = sf.lib().sf_slab_rows(H, band, n, 1)
+    slab = torch.zeros((rows, W), dtype=torch.int32, device="cuda")
+    s.render_to(slab.data_ptr(), 0, band_rows=band, band_count=n, band_index=1, compact=True,
+                packed=sf.SF_PACKED_INDEX)
+    return slab
+
+
+def test_index_slab_too_deep_hit_reports_edepth(monkeypatch):
+    """VERDICT/ADVICE r5 #1: a hit deeper than the index slab carries is written SF_SLAB_BAD and counted as unresolved,
+    and sf_synchronize reports SF_EDEPTH -- also after the lone-frame fast path (a context whose earlier syncs saw only
+    traces that add nothing to the unresolved word). SF_DIAG_SLAB_SHALLOW=1 (tests only) lowers the format's depth
+    limit to 4 so the c2 view's depth-5/6 hits stand in for a hit beyond depth 10 that the host proof excludes."""
+    import torch
+    monkeypatch.setenv("SF_DIAG_SLAB_SHALLOW", "1")
+    fx = load_frame("c2")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    assert fx["stats"]["max_depth"] > 4
+    # (a) the first frame of a context
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        slab = _packed_index_render(s, W, H)
+        with pytest.raises(sf.SphereflakeError) as e:
+            s.Synchronize()
+        assert e.value.code == sf.SF_EDEPTH
+        v = slab.cpu().numpy().view(np.uint32)
+        assert (v == 0xFFFFFFFE).any()   # SF_SLAB_BAD, never a plausible index
+    # (b) a later frame, after syncs that took the fast path (plain persistent traces, nothing to read back)
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for _ in range(3):
+            s.Render()
+            s.Synchronize()
+        _packed_index_render(s, W, H)
+        with pytest.raises(sf.SphereflakeError) as e:
+            s.Synchronize()
+        assert e.value.code == sf.SF_EDEPTH
+    # (c) the same on a dist slot: sf_dist_synchronize reports it (a peer rank's slot context traces exactly this)
+    with sf.SphereflakeDist(0, W, H, slots=2) as d:
+        d.SetCamera(sf.config_camera(W, H, K))
+        d.RenderBands()
+        d.RenderBands()
+        d.Synchronize()
+        ctx = d.context(1)
+        rows = sf.lib().sf_slab_rows(H, 8, 2, 1)
+        slab = torch.zeros((rows, W), dtype=torch.int32, device="cuda")
+        p = sf.render_params(band_rows=8, band_count=2, band_index=1, compact=True, packed=sf.SF_PACKED_INDEX)
+        rc = sf.lib().sf_render_to(ctx, ctypes_byref(p), slab.data_ptr(), slab.data_ptr(), None, None)
+        assert rc == sf.SF_OK
+        with pytest.raises(sf.SphereflakeError) as e:
+            d.Synchronize()
+        assert e.value.code == sf.SF_EDEPTH
+    # (d) the group path end to end: member 1 ships the slab, member 0 unpacks (the bad pixels as NaN), the sync fails
+    with sf.SphereflakeGroup([0, 0], W, H) as g:
+        g.SetCamera(sf.config_camera(W, H, K))
+        assert g.slab_bytes() == 4
+        g.Render()
+        with pytest.raises(sf.SphereflakeError) as e:
+            g.Synchronize()
+        assert e.value.code == sf.SF_EDEPTH
+
+
+def test_index_slab_at_the_format_depth_is_clean():
+    """Without the test hook the same renders synchronise cleanly (the fix leaves the default path's result alone)."""
+    fx = load_frame("c2")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        s.Render()
+        s.Synchronize()
+        slab = _packed_index_render(s, W, H)
+        s.Synchronize()
+        v = slab.cpu().numpy().view(np.uint32)
+        assert not (v == 0xFFFFFFFE).any()
+
+
+def ctypes_byref(p):
+    import ctypes
+    return ctypes.byref(p)
