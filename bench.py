@@ -67,6 +67,9 @@ def parse():
                     help="untimed frames beyond --warmup until the GPU has been under load this long (0: off)")
     ap.add_argument("--mode", choices=["dist", "frames", "rows"], default="dist")
     ap.add_argument("--slots", type=int, default=DEFAULT_SLOTS, help="frames in flight (dist mode)")
+    ap.add_argument("--batch", type=int, default=-1,
+                    help="frames per multi-frame persistent launch (sf_render_frames; 1: one launch per frame; "
+                         "-1: by the share, frames_per_launch)")
     ap.add_argument("--kernel", choices=["wave", "ray"], default="wave")
     ap.add_argument("--width", type=int, default=W)
     ap.add_argument("--height", type=int, default=H)
@@ -102,13 +105,28 @@ SHARE_GRID_FRAC = 1.5                # a share of at most this many persistent-g
 GRID_WAVES_PER_CU = 32               # the trace kernel's grid: 4 SIMDs x 8 waves per CU (LDS-limited occupancy)
 
 
-def frames_in_flight(requested, cus, width, height, band_rows, n):
+BATCH_FULL, BATCH_SHARE = 1, 1       # frames per launch (frames_per_launch); set from scripts/frames_probe.py
+GROUPS_IN_FLIGHT = 2                 # multi-frame launches in flight: slots = batch x this
+
+
+def frames_per_launch(requested, cus, width, height, band_rows, n):
+    """Frames per multi-frame persistent launch for a loop whose rank renders rank 0's bands of an n-way split."""
+    if requested >= 1:
+        return min(8, requested)
+    rows = sf.lib().sf_slab_rows(height, band_rows, n, 0) if n > 1 else height
+    tiles = -(-width // 8) * -(-rows // 8)
+    return BATCH_SHARE if tiles <= SHARE_GRID_FRAC * GRID_WAVES_PER_CU * cus else BATCH_FULL
+
+
+def frames_in_flight(requested, cus, width, height, band_rows, n, batch=1):
     """Frames in flight for a loop whose rank renders rank 0's bands of an n-way split (n = 1: whole frames).
     A share that leaves most of the persistent grid's wave slots idle is bounded by the per-frame chain
     (trace, order, host enqueue: ~55-60 us for a 1080p share over 8) over the frames that overlap, so it takes
     one frame more; frames that fill the grid are throughput-bound and a 4th frame only adds contention."""
     if requested:
-        return max(1, min(8, requested))
+        return max(batch, min(16, requested))
+    if batch > 1:
+        return batch * GROUPS_IN_FLIGHT
     rows = sf.lib().sf_slab_rows(height, band_rows, n, 0) if n > 1 else height
     tiles = -(-width // 8) * -(-rows // 8)
     return SLOTS_SHARE if tiles <= SHARE_GRID_FRAC * GRID_WAVES_PER_CU * cus else SLOTS_FULL
@@ -124,16 +142,46 @@ SETTLE_MS = 150.0                    # the shader clock ramps from ~2075 to ~237
                                      # settle lengths, profiles/r4/final: the line reports the live clock.)
 
 
-def settle(d, render, views, n_views, t_start, ms):
+class FrameIssuer:
+    """Issues the frames of a loop on a dist: `batch` 1 -- SetView + one render call (one trace launch) per frame;
+    `batch` B > 1 -- B frames of the camera path per multi-frame persistent launch (RenderBandsFrames, round 6):
+    every frame is still its own view rendered into its own slot G-buffer, B per launch. `issue(rows)` renders the
+    frames whose views are the rows of an n x 12 float32 array (made before any timed region: the camera path is
+    precomputed either way); `view_rows` turns (origin, tl, tr, bl) tuples into that array."""
+
+    def __init__(self, d, render, batch):
+        self.d, self.render, self.batch = d, render, max(1, int(batch))
+
+    @staticmethod
+    def view_rows(views):
+        return np.ascontiguousarray(np.array([[c for v in view for c in v] for view in views], np.float32).reshape(-1, 12))
+
+    def issue(self, rows):
+        d, b = self.d, self.batch
+        if b == 1:
+            for v in rows:
+                d.SetView(v[0:3], v[3:6], v[6:9], v[9:12])
+                self.render()
+            return
+        for i in range(0, len(rows), b):
+            d.RenderBandsFrames(rows[i:i + b])
+
+
+def settle(d, render, views, n_views, t_start, ms, issuer=None):
     """Untimed frames (cycling views[:n_views]) until `ms` have passed since t_start with the GPU under load;
     returns the number of extra frames."""
     k = 0
     d.Synchronize()
+    rows = FrameIssuer.view_rows(views[:n_views]) if issuer is not None else None
     while (time.perf_counter() - t_start) * 1e3 < ms:
-        for _ in range(20):
-            d.SetView(*views[k % n_views])
-            render()
-            k += 1
+        if issuer is not None:
+            issuer.issue(rows[np.arange(k, k + 20) % n_views])
+            k += 20
+        else:
+            for _ in range(20):
+                d.SetView(*views[k % n_views])
+                render()
+                k += 1
         d.Synchronize()
     return k
 
@@ -663,7 +711,8 @@ def check_golden_rows(pos, nrm, golden, rows):
 
 
 def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows, nranks, frame_of,
-              fixed=False, latency=False, first=False, gather=False, settle_ms=SETTLE_MS, long_steps=0, check=False):
+              fixed=False, latency=False, first=False, gather=False, settle_ms=SETTLE_MS, long_steps=0, check=False,
+              batch=1):
     """One timed loop of the sf_dist path: `steps` frames (frame_of(i) of the camera path at step i) after
     `warmup`, `slots` in flight, over `nranks` ranks (1: this GPU alone, every rank its own frames); each frame
     is every rank's bands into its own G-buffer (the distributed G-buffer), or with `gather` also assembled on
@@ -673,12 +722,15 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
     steady frame period (the difference of the two loops per extra frame) and the pipeline fill (what the timed
     loop pays beyond steps x the period: its first frames start with no frame in flight).
     `check`: after the timed loop, its last frame's rows (this rank's bands; 12 of them) against the oracle, and
-    after the fixed-view loop that frame's rows against the golden digests of the config (when one exists)."""
+    after the fixed-view loop that frame's rows against the golden digests of the config (when one exists).
+    `batch` > 1 (not with `gather`): the loops issue `batch` frames per multi-frame persistent launch (FrameIssuer);
+    the one-frame latency stays one launch per frame."""
     rank = ctl.rank if nranks > 1 else 0
     ids = shard.dist_ids(slots) if nranks > 1 and gather else None
     d = sf.SphereflakeDist(dev.index, width, height, rank=rank, nranks=nranks, slots=slots, ids=ids,
                            band_rows=band_rows)
     render = d.Render if gather else d.RenderBands
+    issuer = FrameIssuer(d, render, 1 if gather else batch)
     view_at = path_views(width, height, k, frame_of)
     views = [view_at(i) for i in range(warmup + steps)]
     out = {"checks": {}}
@@ -698,15 +750,14 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
     for s in range(slots):
         d.kernel_timing(s, True, period=kp)
     t_w = time.perf_counter()
-    for i in range(warmup):
-        d.SetView(*views[i])
-        render()
-    out["settle_frames"] = settle(d, render, views, max(1, warmup), t_w, settle_ms)
+    issuer.issue(FrameIssuer.view_rows(views[:warmup]))
+    out["settle_frames"] = settle(d, render, views, max(1, warmup), t_w, settle_ms, issuer)
     for s in range(slots):
         d.kernel_timing(s, True, period=kp)
     d.reset_stats()
 
     def timed(n, view_of):
+        rows = FrameIssuer.view_rows([view_of(i) for i in range(n)])   # (the camera path, made before the timing)
         torch.cuda.synchronize(dev)
         ctl.barrier()
         torch.cuda.synchronize(dev)
@@ -716,11 +767,14 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
         enq = [] if ENQ_TRACE else None
         try:
             t0 = time.perf_counter()
-            for i in range(n):
-                d.SetView(*view_of(i))
-                render()
-                if enq is not None:
-                    enq.append(time.perf_counter())
+            if enq is not None or issuer.batch == 1:
+                for i in range(n):
+                    d.SetView(*view_of(i))
+                    render()
+                    if enq is not None:
+                        enq.append(time.perf_counter())
+            else:
+                issuer.issue(rows)
             # the device synchronize waits for every stream of the process, the slots' own included; the dist's
             # Synchronize (its stats copy and error check) follows the timed region
             torch.cuda.synchronize(dev)
@@ -756,7 +810,7 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
         del pos, nrm
     if long_steps > steps:
         # (a short settle first: the readouts above left the GPU idle for a few ms)
-        settle(d, render, views, max(1, warmup), time.perf_counter(), LONG_SETTLE_MS)
+        settle(d, render, views, max(1, warmup), time.perf_counter(), LONG_SETTLE_MS, issuer)
         kpl = slot_period(long_steps, slots)
         for s in range(slots):   # the live clock of this loop too (the chip's clock moves between loops)
             d.kernel_timing(s, True, period=kpl)
@@ -782,10 +836,9 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
         cfg_view = frame_camera(width, height, k, 0).corners()
         d.SetView(*cfg_view)
         t_w = time.perf_counter()
-        for i in range(warmup):
-            render()
+        issuer.issue(FrameIssuer.view_rows([cfg_view] * warmup))
         # (the host work since the timed loop let the clock drop: settle again)
-        settle(d, render, [cfg_view], 1, t_w, settle_ms)
+        settle(d, render, [cfg_view], 1, t_w, settle_ms, issuer)
         out["t_fixed"] = timed(steps, lambda i: cfg_view) / steps
         golden = golden_frame(width, height, k) if check else None
         if golden is not None and (rank == 0 or not gather):
@@ -921,17 +974,19 @@ def main():
 
     ranks = rank_devices(ctl, gpu)
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    slots = frames_in_flight(args.slots, cus, width, height, args.band_rows, n if args.mode == "dist" else 1)
+    nshare = n if args.mode == "dist" else 1
+    batch = frames_per_launch(args.batch, cus, width, height, args.band_rows, nshare)
+    slots = frames_in_flight(args.slots, cus, width, height, args.band_rows, nshare, batch)
     if args.mode == "dist":
         # the frame split over the ranks, each rank's bands into its own HBM (the distributed G-buffer)
         r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, n,
                       lambda i: i, fixed=True, latency=True, first=True, settle_ms=args.settle_ms,
-                      long_steps=long_steps, check=check)
+                      long_steps=long_steps, check=check, batch=batch)
         rays_step = width * height
     else:   # frames: every rank its own frames (frame i * N + rank), one GPU each, slots in flight
         r = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup, slots, args.band_rows, 1,
                       lambda i: i * n + rank, fixed=True, latency=True, first=True, settle_ms=args.settle_ms,
-                      long_steps=long_steps, check=check)
+                      long_steps=long_steps, check=check, batch=batch)
         rays_step = width * height * n
     d = r["dist"]
     t_step = r["t_step"]
@@ -942,9 +997,10 @@ def main():
     # weak-scaling companion of a multi-GPU run: every rank renders its own frames (no gather)
     indep = None
     if args.mode == "dist" and n > 1:
+        bi = frames_per_launch(args.batch, cus, width, height, args.band_rows, 1)
         ri = dist_loop(ctl, torch, dev, width, height, args.K, args.steps, args.warmup,
-                       frames_in_flight(args.slots, cus, width, height, args.band_rows, 1), args.band_rows, 1,
-                       lambda i: i * n + rank, settle_ms=args.settle_ms)
+                       frames_in_flight(args.slots, cus, width, height, args.band_rows, 1, bi), args.band_rows, 1,
+                       lambda i: i * n + rank, settle_ms=args.settle_ms, batch=bi)
         ri["dist"].close()
         indep = {"value": round(n * width * height / ri["t_step"] / 1e6, 2), "frame_ms": round(ri["t_step"] * 1e3, 4),
                  "scaling": "weak", "note": "every rank renders its own full frames (frame i * N + rank), no gather"}
@@ -952,11 +1008,12 @@ def main():
     # BASELINE configs[3] (3840x2160, K = 0.22, depth 9) on the same path, all ranks
     c4 = None
     if not args.no_extras and (width, height, round(args.K, 4)) == (W, H, K):
+        b4 = frames_per_launch(args.batch, cus, 3840, 2160, args.band_rows, nshare)
         r4 = dist_loop(ctl, torch, dev, 3840, 2160, 0.22, 60, 15,
-                       frames_in_flight(args.slots, cus, 3840, 2160, args.band_rows, n if args.mode == "dist" else 1),
+                       frames_in_flight(args.slots, cus, 3840, 2160, args.band_rows, nshare, b4),
                        args.band_rows,
                        n if args.mode == "dist" else 1, (lambda i: i) if args.mode == "dist" else (lambda i: i * n + rank),
-                       settle_ms=args.settle_ms)
+                       settle_ms=args.settle_ms, batch=b4)
         rays0_4 = (sf.lib().sf_slab_rows(2160, args.band_rows, n, 0) if args.mode == "dist" else 2160) * 3840
         a4 = BYTES_PER_RAY * rays0_4 / r4["t_step"] / 1e9
         c4 = {"config": "BASELINE configs[3]: 3840x2160, K=0.22", "max_depth": r4["stats"].max_depth,
@@ -1040,7 +1097,7 @@ def main():
                                    f"depth {st.max_depth})" + (f", BASELINE {cfg_name}" if cfg_name else "")
                                    + f", moving camera, {args.kernel} kernel",
                        "width": width, "height": height, "K": args.K, "max_depth": st.max_depth, "camera": "moving",
-                       "slots": slots, "parallelism": par},
+                       "slots": slots, "frames_per_launch": batch, "parallelism": par},
             "frame_ms": round(t_step * 1e3, 4),
             "frame_latency_ms": round(r["latency_ms"], 4),
             "first_render_ms": round(r["first_render_ms"], 4),

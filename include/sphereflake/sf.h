@@ -131,6 +131,20 @@ int sf_render(sf_ctx* ctx, const sf_render_params* params);
 int sf_render_to(sf_ctx* ctx, const sf_render_params* params, float* pos4, float* nrm4,
                  float* min_t, uint32_t* hit_index);
 
+/* Several frames in ONE persistent launch (round 6): frame k is ctxs[k]'s current view, rendered into ctxs[k]'s
+   G-buffer and stats exactly as sf_render(ctxs[k], params) would (bit for bit), but one resident grid takes the
+   work units of all n frames from one set of tile queues -- a wave whose frame runs dry goes on with the next
+   frame's units, and the heaviest tiles of every frame start first -- instead of n launches each ending on its
+   own heaviest tiles. For frames of a camera path rendered ahead (the reference's workers trace continuously,
+   Sphereflake.cpp:67-74; bench.py's frames in flight). n <= SF_RENDER_FRAMES_MAX contexts on one device, of
+   one frame size, each with a view. Launched on params->stream or ctxs[0]'s stream, ordered after every
+   context's earlier work; every context's later calls are ordered after it. params: as sf_render, but whole
+   frames or bands at frame positions only (compact / packed / per-ray kernel / max_depth: SF_EINVAL). Where the
+   batch cannot take one launch (levels not proven for some view, diagnostics on, the subtree-split or
+   compaction kernels), the frames are rendered one launch each, with the same results. */
+#define SF_RENDER_FRAMES_MAX 8
+int sf_render_frames(sf_ctx* const* ctxs, uint32_t n, const sf_render_params* params);
+
 /* Rows of the slab a (band_rows, band_count, band_index) shard owns (compact layout). */
 uint32_t sf_slab_rows(uint32_t height, uint32_t band_rows, uint32_t band_count, uint32_t band_index);
 
@@ -387,6 +401,12 @@ int sf_dist_render(sf_dist* dist);                    /* one frame, asynchronous
 /* One frame as a distributed G-buffer: this rank's bands into its slot's G-buffer at frame positions (reference
    layout), no gather -- every rank holds its own rows in its own HBM. Asynchronous; no collective. */
 int sf_dist_render_bands(sf_dist* dist);
+
+/* The next n frames of a camera path (views[k][0..11] = origin, top-left, top-right, bottom-left) as this rank's
+   bands, frame k into slot (frames + k) % slots's G-buffer (n <= slots, n <= SF_RENDER_FRAMES_MAX), in ONE
+   multi-frame persistent launch (sf_render_frames): sf_dist_render_bands for n frames without a launch each.
+   The views are set on the slots (sf_dist_set_view is not needed). Asynchronous. */
+int sf_dist_render_bands_frames(sf_dist* dist, uint32_t n, const float (*views)[12]);
 int sf_dist_synchronize(sf_dist* dist);               /* every slot of this rank done */
 int sf_dist_download(sf_dist* dist, float* pos4, float* nrm4);   /* rank 0: D2H of the last frame (synchronises) */
 int sf_dist_get_stats(sf_dist* dist, sf_stats* out);  /* over slots, and over ranks when made with ids

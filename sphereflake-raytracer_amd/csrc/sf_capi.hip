@@ -23,6 +23,7 @@ extern "C" __global__ void sf_trace_wave1(FrameArgs a, uint32_t* overflow_list, 
 extern "C" __global__ void sf_trace_wave2(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
 extern "C" __global__ void sf_trace_wave4(FrameArgs a, uint32_t* overflow_list, uint32_t* overflow_count);
 extern "C" __global__ void sf_trace_queue1(FrameArgs a);
+extern "C" __global__ void sf_trace_frames1(FrameBatch b);
 extern "C" __global__ void sf_trace_queue1s(FrameArgs a);
 extern "C" __global__ void sf_trace_queue2(FrameArgs a);
 extern "C" __global__ void sf_trace_queue4(FrameArgs a);
@@ -677,6 +678,65 @@ static FrameArgs frame_args(const sf_ctx* c)
     return a;
 }
 
+// The next render's tile order from the tile costs the render just enqueued on `s` recorded (sf_order_scan /
+// sf_order_bucket_scan + sf_order_scatter_plan); `waves`: resident waves of its persistent grid.
+static int order_rebuild(sf_ctx* c, hipStream_t s, uint32_t ntiles, uint32_t waves, uint32_t split_buckets)
+{
+    const uint32_t nc = (ntiles + 63u) / 64u;
+    const uint32_t spare = waves > ntiles ? waves - ntiles : 0u;
+    // few chunks: the scan's workgroup also scatters (one launch: ~3 us less host time and one
+    // dispatch less on the frame's stream); more: one wave per chunk in a launch of its own
+    const bool fuse = nc <= SF_ORDER_FUSE_CHUNKS;
+    const uint32_t cap = c->part_rec ? SF_SPLIT_CAP : 0xffffffffu;
+    if (fuse) {
+        hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, c->chunk_cnt, nc, ntiles, split_buckets,
+                           c->split_parts, spare, waves, c->prio_buckets, c->chunk_off, c->order_meta,
+                           (const uint32_t*)c->tile_cost, c->tile_order, cap);
+        SF_HIP(c, hipGetLastError());
+    } else {   // (round 5: one-wave workgroups only -- see sf_order_bucket_scan)
+        hipLaunchKernelGGL(sf_order_bucket_scan, dim3(SF_ORDER_BUCKETS), dim3(64), 0, s, (const uint32_t*)c->chunk_cnt,
+                           nc, c->chunk_off, c->order_tot);
+        SF_HIP(c, hipGetLastError());
+        hipLaunchKernelGGL(sf_order_scatter_plan, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost, ntiles,
+                           c->chunk_cnt, (const uint32_t*)c->chunk_off, (const uint32_t*)c->order_tot, split_buckets,
+                           c->split_parts, spare, waves, c->prio_buckets, cap, c->order_meta, c->tile_order);
+        SF_HIP(c, hipGetLastError());
+    }
+    c->order_n = ntiles;
+    return SF_OK;
+}
+
+// LDS traversal levels for the context's view, and whether they are proven sufficient (no tile can overflow).
+// Geometric bound: every sphere lies inside the root's bounding sphere (radius 2 around the root centre), so a
+// depth-d node can pass the LOD test (t < T_d, Sphereflake.h:146) only if |root centre| - 2 < T_d. The deepest such
+// d + 1 levels suffice; a bound that is off only costs a re-trace of the affected tiles (sf_fixup_wave), never results.
+static uint32_t frame_levels(const sf_ctx* c, bool* bounded_out)
+{
+    uint32_t levels = kDefaultLevels;
+    const float rc = std::sqrt(c->root[12] * c->root[12] + c->root[13] * c->root[13] + c->root[14] * c->root[14]);
+    const float gap = (rc - 2.0f) * (1.0f - 1e-3f);
+    bool bounded = false;
+    if (gap > 0.0f) {
+        uint32_t dmax = 0;
+        while (dmax + 1u < SF_DEPTH_TABLE && c->host_consts.dt.lod[dmax + 1u] > gap) ++dmax;
+        levels = dmax + 1u;
+        bounded = levels <= SF_MAX_DEPTH_LIMIT;
+    }
+    const int32_t seen = *(volatile int32_t*)c->h_depth;   // max depth of a finished render
+    if (seen >= 0 && (uint32_t)seen + 1u < levels) {
+        levels = (uint32_t)seen + 1u;
+        bounded = false;
+    }
+    if (levels < 4u) levels = 4u;
+    if (levels > SF_MAX_DEPTH_LIMIT) levels = SF_MAX_DEPTH_LIMIT;
+    if (c->levels_override) {
+        levels = c->levels_override;
+        bounded = false;
+    }
+    *bounded_out = bounded;
+    return levels;
+}
+
 static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm, float* min_t, uint32_t* hidx)
 {
     if (!c) return SF_EINVAL;
@@ -740,31 +800,8 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
         SF_HIP(c, hipGetLastError());
     } else {
         const bool autod = p.max_depth == 0;
-        uint32_t levels = kDefaultLevels;
-        // Geometric bound: every sphere lies inside the root's bounding sphere (radius 2 around the
-        // root centre), so a depth-d node can pass the LOD test (t < T_d, Sphereflake.h:146) only if
-        // |root centre| - 2 < T_d. The deepest such d + 1 levels suffice; a bound that is off only
-        // costs a re-trace of the affected tiles (sf_fixup_wave), never results.
-        const float rc = std::sqrt(c->root[12] * c->root[12] + c->root[13] * c->root[13] + c->root[14] * c->root[14]);
-        const float gap = (rc - 2.0f) * (1.0f - 1e-3f);
         bool bounded = false;   // levels proven sufficient: no tile can overflow
-        if (gap > 0.0f) {
-            uint32_t dmax = 0;
-            while (dmax + 1u < SF_DEPTH_TABLE && c->host_consts.dt.lod[dmax + 1u] > gap) ++dmax;
-            levels = dmax + 1u;
-            bounded = levels <= SF_MAX_DEPTH_LIMIT;
-        }
-        const int32_t seen = *(volatile int32_t*)c->h_depth;   // max depth of a finished render
-        if (seen >= 0 && (uint32_t)seen + 1u < levels) {
-            levels = (uint32_t)seen + 1u;
-            bounded = false;
-        }
-        if (levels < 4u) levels = 4u;
-        if (levels > SF_MAX_DEPTH_LIMIT) levels = SF_MAX_DEPTH_LIMIT;
-        if (c->levels_override) {
-            levels = c->levels_override;
-            bounded = false;
-        }
+        uint32_t levels = frame_levels(c, &bounded);
         if (!autod) bounded = bounded && p.max_depth >= levels;
         a.max_depth = autod ? levels : p.max_depth;
         const size_t lds = (size_t)SF_LDS_WAVE_FLOATS(a.max_depth) * 4;
@@ -879,29 +916,7 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
                 c->ev_count = c->ev_count < (uint32_t)sf_ctx::kTimed ? c->ev_count + 1u : c->ev_count;
             }
             if (rebuild) {   // the next render's tile order, from this render's tile costs
-                const uint32_t nc = (ntiles + 63u) / 64u;
-                const uint32_t waves = nblk * wpb;   // resident waves of the persistent grid
-                const uint32_t spare = waves > ntiles ? waves - ntiles : 0u;
-                // few chunks: the scan's workgroup also scatters (one launch: ~3 us less host time and one
-                // dispatch less on the frame's stream); more: one wave per chunk in a launch of its own
-                const bool fuse = nc <= SF_ORDER_FUSE_CHUNKS;
-                const uint32_t cap = c->part_rec ? SF_SPLIT_CAP : 0xffffffffu;
-                if (fuse) {
-                    hipLaunchKernelGGL(sf_order_scan, dim3(1), dim3(1024), 0, s, c->chunk_cnt, nc, ntiles,
-                                       split_buckets, c->split_parts, spare, waves, c->prio_buckets, c->chunk_off,
-                                       c->order_meta, (const uint32_t*)c->tile_cost, c->tile_order, cap);
-                    SF_HIP(c, hipGetLastError());
-                } else {   // (round 5: one-wave workgroups only -- see sf_order_bucket_scan)
-                    hipLaunchKernelGGL(sf_order_bucket_scan, dim3(SF_ORDER_BUCKETS), dim3(64), 0, s,
-                                       (const uint32_t*)c->chunk_cnt, nc, c->chunk_off, c->order_tot);
-                    SF_HIP(c, hipGetLastError());
-                    hipLaunchKernelGGL(sf_order_scatter_plan, dim3(nc), dim3(64), 0, s, (const uint32_t*)c->tile_cost,
-                                       ntiles, c->chunk_cnt, (const uint32_t*)c->chunk_off,
-                                       (const uint32_t*)c->order_tot, split_buckets, c->split_parts, spare, waves,
-                                       c->prio_buckets, cap, c->order_meta, c->tile_order);
-                    SF_HIP(c, hipGetLastError());
-                }
-                c->order_n = ntiles;
+                if (int rc = order_rebuild(c, s, ntiles, nblk * wpb, split_buckets)) return rc;
             }
         } else {
             const dim3 grid((ntiles + wpb - 1) / wpb);
@@ -949,6 +964,157 @@ int sf_render_to(sf_ctx* c, const sf_render_params* p, float* pos4, float* nrm4,
 {
     if (p && p->packed && !nrm4) nrm4 = pos4;   // (packed slabs write pos4 only)
     return launch(c, p, pos4, nrm4, min_t, hidx);
+}
+
+// Multi-frame persistent trace (sf.h; kernel sf_trace_frames1). One launch where every frame's own launch() would be
+// a bounded persistent one-wave trace (levels proven for its view, ties re-traced inline, no fixup launch), else one
+// launch() per frame. The frames share the first context's tile queues, its unit order (rebuilt from frame 0's costs
+// on its schedule) and its kernel timing; each frame writes its own context's G-buffer, aux channels and stats.
+int sf_render_frames(sf_ctx* const* cs, uint32_t n, const sf_render_params* pp)
+{
+    static_assert(SF_RENDER_FRAMES_MAX <= (int)SF_BATCH_MAX, "the batch travels in the kernel argument segment");
+    static_assert(sizeof(FrameBatch) <= 4096, "kernel argument segment");
+    if (!cs || n == 0 || n > (uint32_t)SF_RENDER_FRAMES_MAX) return SF_EINVAL;
+    sf_render_params p;
+    std::memset(&p, 0, sizeof p);
+    if (pp) p = *pp;
+    if (p.compact || p.packed || p.kernel == SF_KERNEL_PER_RAY || p.max_depth) return SF_EINVAL;
+    sf_ctx* const c0 = cs[0];
+    for (uint32_t k = 0; k < n; ++k) {
+        if (!cs[k]) return SF_EINVAL;
+        if (!cs[k]->has_view) return SF_ENOVIEW;
+        if (cs[k]->device != c0->device || cs[k]->W != c0->W || cs[k]->H != c0->H) return SF_EINVAL;
+        for (uint32_t j = 0; j < k; ++j)
+            if (cs[j] == cs[k]) return SF_EINVAL;   // (two frames into one G-buffer in one launch would race)
+    }
+    const uint32_t tiles_y = (c0->H + 7) / 8;
+    const uint32_t band_rows = p.band_rows ? p.band_rows : tiles_y * 8;
+    const uint32_t band_count = p.band_count ? p.band_count : 1;
+    if (band_rows % 8 != 0 || p.band_index >= band_count || p.kernel > SF_KERNEL_PER_RAY) return SF_EINVAL;
+    // one launch only where each frame alone would take the bounded one-wave persistent trace with nothing after it
+    uint32_t levels = 0;
+    bool one = n > 1;
+    for (uint32_t k = 0; k < n && one; ++k) {
+        const sf_ctx* c = cs[k];
+        bool bounded = false;
+        const uint32_t l = frame_levels(c, &bounded);
+        const bool front_first = (c->flags & (SF_FLAG_NO_OCCL_CULL | SF_FLAG_NO_FRONT_FIRST)) == 0u;
+        one = bounded && c->persistent && c->waves_per_block == 1u && !c->compact && !c->part_rec && !c->tile_trace &&
+              !(front_first && !c->tie_inline) && c->flags == c0->flags && c->variant == c0->variant &&
+              !(c->flags & SF_FLAG_DIAG_HALF);
+        levels = l > levels ? l : levels;
+    }
+    if (!one) {   // one launch per frame: the same frames (launch() orders each context's own calls)
+        for (uint32_t k = 0; k < n; ++k)
+            if (int rc = launch(cs[k], &p, cs[k]->pos, cs[k]->nrm, cs[k]->min_t, cs[k]->hit_index)) return rc;
+        return SF_OK;
+    }
+    const uint32_t tpb = band_rows / 8;
+    const uint32_t bands = (tiles_y + tpb - 1) / tpb;
+    uint32_t tile_rows = 0, rows = 0;
+    for (uint32_t b = p.band_index; b < bands; b += band_count) {
+        const uint32_t t0 = b * tpb, t1 = t0 + tpb < tiles_y ? t0 + tpb : tiles_y;
+        tile_rows += t1 - t0;
+        const uint32_t y0 = b * band_rows, y1 = y0 + band_rows < c0->H ? y0 + band_rows : c0->H;
+        rows += y1 - y0;
+    }
+    hipStream_t s = p.stream ? (hipStream_t)p.stream : c0->stream;
+    DevGuard g(c0->device);
+    if (tile_rows == 0) return SF_OK;
+    bool unknown_before[SF_BATCH_MAX];
+    for (uint32_t k = 0; k < n; ++k) {
+        unknown_before[k] = cs[k]->stats_unknown;
+        if (int rc = ctx_join(cs[k], s)) return rc;
+    }
+    const size_t lds = (size_t)SF_LDS_WAVE_FLOATS(levels) * 4;
+    const int key = (int)(64 + levels) | (1 << 21);   // (c0's occupancy cache, told apart from launch()'s keys)
+    if (c0->occ_key != key) {
+        int nb = 0;
+        SF_HIP(c0, hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sf_trace_frames1, 64, lds));
+        c0->occ_blocks = nb < 1 ? 1 : nb;
+        c0->occ_key = key;
+    }
+    uint32_t nblk = (uint32_t)c0->occ_blocks * (uint32_t)c0->cus;
+    const uint32_t ntiles = ((c0->W + 7) / 8) * tile_rows;
+    // c0's order policy, as launch() decides it for one of these frames
+    const bool small = ntiles <= 2u * nblk;
+    const bool tiny = 2u * ntiles <= nblk && band_count == 1u;
+    const bool large = !small && band_count == 1u;
+    const bool use_order = c0->order_mode > 0 || (c0->order_mode < 0 && (tiny || large));
+    const uint32_t split_buckets = (large && !c0->split_env) ? 0u : c0->split_buckets;
+    const uint32_t units_max = (use_order && split_buckets != 0u) ? c0->split_parts * ntiles : ntiles;
+    if ((uint64_t)n * units_max >= 0x80000000ull) return SF_EINVAL;   // (positions below bit 31: the re-trace word)
+    if (nblk > n * units_max) nblk = n * units_max;
+    if (c0->max_blocks && nblk > c0->max_blocks) nblk = c0->max_blocks;
+    uint32_t xcds = c0->queues;
+    while (xcds > 1u && xcds > nblk) xcds >>= 1;
+    uint32_t queues = xcds;
+    if (c0->queues_per_xcd > 1u && nblk >= 64u * xcds * c0->queues_per_xcd) queues = xcds * c0->queues_per_xcd;
+    const uint32_t every = c0->order_every ? c0->order_every : (small ? 3u : large ? 64u : 1u);
+    const bool rebuild = use_order && (c0->order_n != ntiles || c0->order_phase + 1u >= every);
+    if (use_order) c0->order_phase = rebuild ? 0u : c0->order_phase + 1u;
+    const bool record = use_order && (c0->order_record_env >= 0 ? c0->order_record_env != 0 : !large);
+    const bool front_first = (c0->flags & (SF_FLAG_NO_OCCL_CULL | SF_FLAG_NO_FRONT_FIRST)) == 0u;
+    FrameBatch b;
+    std::memset(&b, 0, sizeof b);
+    b.nframes = n;
+    b.units = ntiles;
+    b.heavy = nblk / n;   // every frame's heaviest units among the waves' static first units
+    for (uint32_t k = 0; k < n; ++k) {
+        sf_ctx* c = cs[k];
+        FrameArgs a = frame_args(c);
+        a.tile_rows = tile_rows;
+        a.tiles_per_band = tpb;
+        a.tpb_magic = 0xffffffffu / tpb;
+        a.band_count = band_count;
+        a.band_index = p.band_index;
+        a.emit_aux = p.emit_aux ? 1u : 0u;
+        a.pos = c->pos;
+        a.nrm = c->nrm;
+        a.min_t = c->min_t;
+        a.hit_index = c->hit_index;
+        a.max_depth = levels;
+        if (front_first) a.flags |= SF_FLAG_TIE_INLINE;
+        a.counters = c0->ovf_counters;   // the launch's queues: c0's, at c0's parity
+        a.overflow_list = c0->ovf_list;
+        a.parity = c0->parity;
+        a.xcds = xcds;
+        a.queues = queues;
+        if (use_order) {
+            a.tile_order = c0->order_n == ntiles ? c0->tile_order : nullptr;
+            a.order_meta = c0->order_meta;
+            a.part_cost = c0->part_cost;
+            a.part_done = c0->part_done;
+            if (k == 0u) {   // only frame 0 records tile costs (the order and its histogram are per tile)
+                a.tile_cost = (rebuild || record) ? c0->tile_cost : nullptr;
+                a.chunk_cnt = rebuild ? c0->chunk_cnt : nullptr;
+            }
+        }
+        b.f[k] = a;
+    }
+    const bool timed = c0->timing && c0->ev_phase == 0;
+    if (c0->timing) c0->ev_phase = (c0->ev_phase + 1u) % c0->ev_period;
+    if (timed) {
+        SF_HIP(c0, hipEventRecord(c0->ev[c0->ev_next][0], s));
+        b.f[0].clock_probe = c0->clock_buf + (size_t)c0->ev_next * SF_CLOCK_WAVES * 4u;
+    }
+    hipLaunchKernelGGL(sf_trace_frames1, dim3(nblk), dim3(64), lds, s, b);
+    SF_HIP(c0, hipGetLastError());
+    if (timed) {
+        SF_HIP(c0, hipEventRecord(c0->ev[c0->ev_next][1], s));
+        c0->ev_next = (c0->ev_next + 1u) % sf_ctx::kTimed;
+        c0->ev_count = c0->ev_count < (uint32_t)sf_ctx::kTimed ? c0->ev_count + 1u : c0->ev_count;
+    }
+    if (rebuild)
+        if (int rc = order_rebuild(c0, s, ntiles, nblk, split_buckets)) return rc;
+    c0->parity ^= 1u;
+    for (uint32_t k = 0; k < n; ++k) {
+        sf_ctx* c = cs[k];
+        c->rays += (int64_t)rows * c->W;
+        c->stats_unknown = unknown_before[k];   // (bounded, unpacked: the launch adds nothing to the unresolved word)
+        if (s != c->stream) SF_HIP(c, hipEventRecord(c->join_ev, s));   // (StreamMark)
+    }
+    return SF_OK;
 }
 
 // Depth bound of every hit under the context's view (-1: none provable). Every sphere lies inside the root's

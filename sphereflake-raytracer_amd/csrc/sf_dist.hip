@@ -312,6 +312,29 @@ extern "C" int sf_dist_render_bands(sf_dist* d)
     return SF_OK;
 }
 
+// The next n frames of a camera path (views[k] = {origin, top-left, top-right, bottom-left}) as this rank's bands,
+// each into its own slot's G-buffer (slots (frames + k) % slots, n <= slots), in ONE multi-frame persistent launch
+// (sf_render_frames) on the first frame's slot stream -- the distributed G-buffer of sf_dist_render_bands without a
+// launch per frame.
+extern "C" int sf_dist_render_bands_frames(sf_dist* d, uint32_t n, const float (*views)[12])
+{
+    if (!d || !views || n == 0 || n > (uint32_t)SF_RENDER_FRAMES_MAX || n > d->slot.size()) return SF_EINVAL;
+    sf_ctx* cs[SF_RENDER_FRAMES_MAX];
+    for (uint32_t k = 0; k < n; ++k) {
+        cs[k] = d->slot[(d->frames + k) % d->slot.size()].ctx;
+        const float* v = views[k];
+        if (int rc = sf_set_view(cs[k], v, v + 3, v + 6, v + 9)) return rc;
+    }
+    sf_render_params p;
+    std::memset(&p, 0, sizeof p);
+    p.band_rows = d->band_rows;
+    p.band_count = (uint32_t)d->nranks;
+    p.band_index = (uint32_t)d->rank;
+    if (int rc = sf_render_frames(cs, n, &p)) return rc;
+    d->frames += n;
+    return SF_OK;
+}
+
 extern "C" int sf_dist_synchronize(sf_dist* d)
 {
     if (!d) return SF_EINVAL;

@@ -177,6 +177,18 @@ struct FrameArgs {
 };
 #define SF_CLOCK_WAVES 8u             // live shader clock samples per timed render (one per XCD group)
 
+// Multi-frame persistent trace (round 6, sf_render_frames): the frames of one launch, passed by value in the kernel
+// argument segment (copied by the runtime at the launch, so the host may build the next batch at once; 4 KB at most:
+// 11 FrameArgs). Frame f is one slot context's view into that context's G-buffer and stats. All frames share one
+// set of tile queues and one unit order (`units` per frame); the first `heavy` units of every frame's order are
+// interleaved across the frames at the head of the launch's sequence (the heaviest tiles of every frame start first),
+// the rest follow frame by frame.
+#define SF_BATCH_MAX 8u
+struct FrameBatch {
+    uint32_t nframes, units, heavy, pad;
+    FrameArgs f[SF_BATCH_MAX];
+};
+
 // Band slab formats of the multi-GPU gather (FrameArgs.packed / sf_render_params.packed):
 //   SF_PACKED_NORMAL  16 B per pixel: float4 (nx, ny, nz, minT); the receiver forms pos = dir * minT
 //   SF_PACKED_INDEX    4 B per pixel: the hit's heap index (SF_SLAB_MISS: none); the receiver rebuilds the

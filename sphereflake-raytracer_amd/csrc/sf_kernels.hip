@@ -1847,6 +1847,45 @@ __device__ __forceinline__ void publish_stats(const FrameArgs& a, int32_t maxd, 
     }
 }
 
+// publish_stats for a call inside a wave-uniform loop (the multi-frame trace publishes a frame's stats when the
+// wave leaves the frame): no lane-0 region -- each atomic runs with EXEC forced to lane 0 inside its asm block, as
+// wave_atomic_max does (signed max / min: the words start at -1 and at the key of FLT_MAX).
+__device__ __forceinline__ void wave_atomic_smax(int32_t* p, int32_t v)
+{
+    p = reinterpret_cast<int32_t*>(uniform_ptr(reinterpret_cast<uint32_t*>(p)));
+    uint64_t saved;
+    const uint32_t zero = 0u;
+    __asm__ volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "global_atomic_smax %1, %2, %3\n\t"
+        "s_mov_b64 exec, %0\n\t"
+        : "=&s"(saved)
+        : "v"(zero), "v"(v), "s"(p)
+        : "memory");
+}
+__device__ __forceinline__ void wave_atomic_smin(int32_t* p, int32_t v)
+{
+    p = reinterpret_cast<int32_t*>(uniform_ptr(reinterpret_cast<uint32_t*>(p)));
+    uint64_t saved;
+    const uint32_t zero = 0u;
+    __asm__ volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "global_atomic_smin %1, %2, %3\n\t"
+        "s_mov_b64 exec, %0\n\t"
+        : "=&s"(saved)
+        : "v"(zero), "v"(v), "s"(p)
+        : "memory");
+}
+__device__ __forceinline__ void publish_stats_in_loop(const FrameArgs& a, int32_t maxd, float closest)
+{
+    const int32_t key = __builtin_amdgcn_readfirstlane(sf_float_key(wave_min(closest)));
+    maxd = __builtin_amdgcn_readfirstlane(maxd);
+    if (maxd >= 0) wave_atomic_smax(a.stats + 0, maxd);
+    if (key != sf_float_key(FLT_MAX)) wave_atomic_smin(a.stats + 1, key);
+}
+
 }  // namespace
 
 // One wave (one 8x8 tile) per workgroup: LDS is the occupancy limit, so the finest granularity packs best.
@@ -2065,6 +2104,172 @@ extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(
 extern "C" __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_queue2p(FrameArgs a)
 {
     trace_queue_body<2, true>(a);
+}
+
+// Multi-frame persistent trace (round 6, sf_render_frames): ONE resident grid takes the work units of
+// up to SF_BATCH_MAX frames -- each a slot context's own view, G-buffer and stats -- from one set of tile queues. A
+// wave whose frame runs dry goes on with the next frame's units, so there is no per-frame launch, no hardware queue
+// per frame and no frame boundary where waves wait for a successor grid; and the launch's sequence starts with the
+// `heavy` heaviest units of EVERY frame of the batch, interleaved (the static first unit of wave w is position w), so
+// no frame's heaviest tiles start late and leave a serial tail (the reference's workers likewise trace continuously,
+// Sphereflake.cpp:67-74,112-213). Position G of the sequence:
+// (units: the shared order's unit count, read on the device like trace_queue_body's; heavy: at most units)
+//   G < nframes x heavy:  frame G % nframes, order position G / nframes (the interleaved heads)
+//   else (q = G - nframes x heavy): frame q / (units - heavy), order position heavy + q % (units - heavy)
+// Per frame everything is as in trace_queue_body<1>: the frame's FrameArgs re-read from the kernel argument segment
+// per unit (scalar loads), its root staged in the wave's LDS when the wave's frame changes, its stats published when
+// the wave leaves the frame. The frames share the unit order (the camera moves little between frames), the queues
+// and their parity (the host gives every frame the first context's); only one frame may record tile costs.
+// The batch in the kernel argument segment, through an address the compiler may not reason about: every read is a
+// scalar load where it is used, so no batch word stays live in an SGPR across the tile loop (the loop's state is a few
+// words: the wave's next position, its frame, its queue, its stats).
+__device__ __forceinline__ const __attribute__((address_space(4))) FrameBatch* kernarg_batch()
+{
+    typedef const __attribute__((address_space(4))) FrameBatch* KernargBatch;
+    KernargBatch pa = (KernargBatch)__builtin_amdgcn_kernarg_segment_ptr();
+    __asm__ volatile("" : "+s"(pa));
+    return pa;
+}
+
+__device__ __forceinline__ void load_frame(FrameArgs& at, uint32_t f)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) FrameArgs* KernargArgs;
+    KernargArgs pf = &((const __attribute__((address_space(4))) FrameBatch*)__builtin_amdgcn_kernarg_segment_ptr())->f[f];
+    __asm__ volatile("" : "+s"(pf));   // (opaque: the fields are loaded where trace_tile uses them, as in trace_queue_body)
+    __builtin_memcpy(&at, (const FrameArgs*)pf, sizeof(FrameArgs));
+#else
+    (void)at;
+    (void)f;
+#endif
+}
+
+template <int WAVES = 1>   // (one wave per workgroup; a template like trace_queue_body, for the shared `lds` declaration)
+__device__ __forceinline__ void trace_frames_body()
+{
+    extern __shared__ float lds[];
+    const uint64_t w_start = __builtin_amdgcn_s_memrealtime();
+    {
+        const auto pb = kernarg_batch();
+        if (blockIdx.x == 0 && threadIdx.x < SF_QUEUES)   // the next launch's queues and overflow count
+            pb->f[0].counters[SF_QUEUE_WORD(pb->f[0].parity ^ 1u, threadIdx.x)] = 0u;
+        if (blockIdx.x == 0 && threadIdx.x == 0) pb->f[0].counters[pb->f[0].parity ^ 1u] = 0u;
+        if (pb->f[0].clock_probe && blockIdx.x < SF_CLOCK_WAVES) {   // measurement: the live clock (trace_queue_body)
+            uint64_t* cp = pb->f[0].clock_probe + 4u * blockIdx.x;
+            cp[0] = __builtin_amdgcn_s_memtime();
+            cp[1] = w_start;
+        }
+    }
+    float* const L = lds;
+    const float4 bcol = build_column(kernarg_batch()->f[0].consts);   // (the slot contexts' constant blocks are equal)
+    uint32_t k;
+    {
+        const auto pb = kernarg_batch();
+        const uint32_t nq = pb->f[0].queues, nx = pb->f[0].xcds;
+        k = blockIdx.x & (nx - 1u);
+        if (nq > nx) {
+            const uint32_t lx = __builtin_ctz(nx);
+            k += nx * ((blockIdx.x >> lx) & ((nq >> lx) - 1u));
+        }
+        k = __builtin_amdgcn_readfirstlane(k);
+    }
+    int32_t maxd = -1;
+    float closest = FLT_MAX;      // per lane, of frame cur
+    uint32_t cur = 0xffffffffu;   // the frame whose root is staged and whose stats accumulate (uniform)
+    uint32_t first = __builtin_amdgcn_readfirstlane(blockIdx.x);
+    for (;;) {
+        const uint32_t G = first;
+        const bool again = (G >> 31) != 0u;
+        uint32_t f = cur, pos = 0u;
+        if (!again) {
+            const auto pb = kernarg_batch();
+            const uint32_t nframes = pb->nframes;
+            // units per frame: the shared order's (order_meta[0]: split tiles count as their parts), else the tiles
+            uint32_t units = pb->units;
+            if (pb->f[0].tile_order) {
+#if defined(__HIP_DEVICE_COMPILE__)
+                typedef const __attribute__((address_space(4))) uint32_t* ConstU32;
+                units = ((ConstU32)(const void*)pb->f[0].order_meta)[0];
+#else
+                units = pb->f[0].order_meta[0];
+#endif
+            }
+            const uint32_t heavy = pb->heavy < units ? pb->heavy : units;
+            if (G >= nframes * units) break;
+            const uint32_t hh = nframes * heavy;
+            if (G < hh) {
+                f = G % nframes;
+                pos = G / nframes;
+            } else {
+                const uint32_t q = G - hh, rest = units - heavy;
+                f = q / rest;
+                pos = heavy + q % rest;
+            }
+            f = __builtin_amdgcn_readfirstlane(f);
+            pos = __builtin_amdgcn_readfirstlane(pos);
+        }
+        if (f != cur) {
+            if (cur != 0xffffffffu) {   // leaving frame cur: its stats
+                FrameArgs pc;
+                load_frame(pc, cur);
+                publish_stats_in_loop(pc, maxd, closest);
+                maxd = -1;
+                closest = FLT_MAX;
+            }
+            FrameArgs ar;
+            load_frame(ar, f);
+            stage_root(L, ar.root);
+            cur = f;
+        }
+        FrameArgs at;
+        load_frame(at, f);
+        uint32_t t = pos, part = 0u;
+        if (again) {
+            t = G & SF_UNIT_TILE_MASK;
+            part = (G >> SF_UNIT_PRIO_SHIFT) & 7u;
+        } else if (at.tile_order) {
+#if defined(__HIP_DEVICE_COMPILE__)
+            typedef const __attribute__((address_space(4))) uint32_t* ConstU32;
+            const uint32_t u = ((ConstU32)(const void*)at.tile_order)[pos];
+#else
+            const uint32_t u = at.tile_order[pos];
+#endif
+            t = u & SF_UNIT_TILE_MASK;
+            part = u >> SF_UNIT_PART_SHIFT;
+            const uint32_t pr = (u >> SF_UNIT_PRIO_SHIFT) & 3u;
+            if (pr == 2u && !(at.flags & SF_FLAG_PRIO_FLAT)) __builtin_amdgcn_s_setprio(3);
+            else if (pr != 0u) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+        auto ticket = [&](bool retrace) {
+            first = retrace ? (0x80000000u | (part << SF_UNIT_PRIO_SHIFT) | t)
+                            : gridDim.x + wave_fetch_add(at.counters + SF_QUEUE_WORD(at.parity, k), 1u) * at.queues + k;
+        };
+        const TileStats st = trace_tile<false, false, decltype(ticket)>(at, L, bcol, t, at.max_depth, at.overflow_list,
+                                                                      at.counters + at.parity, part, ticket,
+                                                                      again ? (at.flags | SF_FLAG_NO_FRONT_FIRST |
+                                                                               SF_FLAG_REDO_PASS)
+                                                                            : at.flags);
+        maxd = st.maxd > maxd ? st.maxd : maxd;
+        closest = fminf(closest, st.closest);
+    }
+    if (cur != 0xffffffffu) {
+        FrameArgs e;
+        load_frame(e, cur);
+        publish_stats(e, maxd, closest, 0u);
+    }
+    const auto pb = kernarg_batch();
+    if (pb->f[0].clock_probe && blockIdx.x < SF_CLOCK_WAVES) {
+        uint64_t* cp = pb->f[0].clock_probe + 4u * blockIdx.x;
+        cp[2] = __builtin_amdgcn_s_memtime();
+        cp[3] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SF_WAVES_PER_EU, 8))) void sf_trace_frames1(FrameBatch b)
+{
+    (void)b;   // (read through the kernel argument segment, per unit: trace_frames_body)
+    trace_frames_body<1>();
 }
 
 // Tile order for the next render: tiles sorted by this render's cost, heaviest first (LPT list
@@ -2478,30 +2683,24 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         w = ((size_t)m * stage_rows + sr) * a.W + x;
         return x < a.W && y < a.H;
     };
-    // the next item's slab word is loaded while this one is rebuilt (its HBM latency off the chain)
-    uint32_t x, y;
-    size_t w;
-    bool ok = blockIdx.x < items && locate(blockIdx.x, x, y, w);
-    uint32_t idx_next = ok ? stage[w] : SF_SLAB_MISS;
-    for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
-        const uint32_t idx = idx_next;
-        const bool cur = ok;
-        const uint32_t cx_ = x, cy_ = y;
-        ok = it + gridDim.x < items && locate(it + gridDim.x, x, y, w);
-        if (ok) idx_next = stage[w];
-        if (!cur) continue;
-        const uint32_t px_ = cx_, py_ = cy_;
-        float dx, dy, dz;
-        ray_dir(a, (float)px_, (float)py_, dx, dy, dz, S.lut);   // (independent of idx: in flight with its load)
-        const size_t o = (size_t)py_ * a.W + px_;
-        if (idx >= SF_SLAB_BAD) {   // a miss: (0, 0, 0, 1) twice; SF_SLAB_BAD (never made by a correct split): NaN
-            const float v = idx == SF_SLAB_MISS ? 0.0f : __builtin_nanf("");
-            reinterpret_cast<float4*>(a.pos)[o] = make_float4(v, v, v, 1.0f);
-            reinterpret_cast<float4*>(a.nrm)[o] = make_float4(v, v, v, 1.0f);
-            continue;
-        }
-        // the depth from the index (the first heap index of depth k is (9^k - 1) / 8), then only the child digits
-        // below the table's depth, bottom-up: the deepest lands in the highest nibble, depth td + 1's in the lowest
+    // Round 6: a two-deep pipeline. While item it is rebuilt, item it + G (G = the grid) already has its node-table
+    // frame in flight (its slab word came one item earlier), and item it + 2G's slab word is loaded: the chain slab
+    // word -> table frame -> frame levels no longer waits on memory twice per item (round 5 prefetched the slab word
+    // only: ~half of the wave cycles waited at full occupancy).
+    struct Item {
+        bool ok;
+        uint32_t x, y, idx, d, td, path;
+        float4 c0, c1, c2;   // the node-table frame of the sphere's ancestor at depth td (hits only)
+    };
+    // the depth from the index (the first heap index of depth k is (9^k - 1) / 8), then only the child digits below
+    // the table's depth, bottom-up (the deepest in the highest nibble, depth td + 1's in the lowest), and the table
+    // frame's loads issued
+    // (the loads are unconditional -- a miss or a lane past the frame reads the root's entry -- so that no branch
+    // around them makes the compiler wait for every load in flight at the join: round 5's pipelined form lost its
+    // overlap to exactly that vmcnt(0))
+    auto prepare = [&](Item& m) {
+        const bool hit = m.ok && m.idx < SF_SLAB_BAD;
+        const uint32_t idx = hit ? m.idx : 0u;
         uint32_t d = 0u;
 #pragma unroll
         for (uint32_t k = 1u, f = 1u; k <= 10u; ++k, f = 9u * f + 1u) d += idx >= f ? 1u : 0u;
@@ -2513,45 +2712,81 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             path = (path << 4) | (anc - 1u - 9u * q);
             anc = q;
         }
-        float xf[12], nx[12];
-        {
-            const float4 c0 = table[3u * anc], c1 = table[3u * anc + 1u], c2 = table[3u * anc + 2u];
-            xf[0] = c0.x; xf[1] = c0.y; xf[2] = c0.z; xf[3] = c0.w;
-            xf[4] = c1.x; xf[5] = c1.y; xf[6] = c1.z; xf[7] = c1.w;
-            xf[8] = c2.x; xf[9] = c2.y; xf[10] = c2.z; xf[11] = c2.w;
-        }
-        // the frames down to the parent, then only the sphere's centre: child_frame's translation column (the same
-        // operations on the same operands)
-        for (uint32_t j = td; j + 1u < d; ++j) {
-            child_frame(S.child, S.scale, j, path & 15u, xf, nx);
-            path >>= 4;
+        m.d = d;
+        m.td = td;
+        m.path = path;
+        m.c0 = table[3u * anc];
+        m.c1 = table[3u * anc + 1u];
+        m.c2 = table[3u * anc + 2u];
+    };
+    const uint32_t G = gridDim.x;
+    Item cur, nxt;
+    size_t w;
+    cur.ok = blockIdx.x < items && locate(blockIdx.x, cur.x, cur.y, w);
+    cur.idx = cur.ok ? stage[w] : SF_SLAB_MISS;
+    nxt.ok = blockIdx.x + G < items && locate(blockIdx.x + G, nxt.x, nxt.y, w);
+    uint32_t idx_next = nxt.ok ? stage[w] : SF_SLAB_MISS;
+    prepare(cur);
+    for (uint32_t it = blockIdx.x; it < items; it += G) {
+        // item it + G: its table frame in flight; item it + 2G: its slab word
+        nxt.idx = idx_next;
+        prepare(nxt);
+        uint32_t x2 = 0u, y2 = 0u;
+        const bool ok2 = it + 2u * G < items && locate(it + 2u * G, x2, y2, w);
+        const uint32_t word = stage[ok2 ? w : 0u];   // (unconditional, see prepare)
+        idx_next = ok2 ? word : SF_SLAB_MISS;
+        if (cur.ok) {
+            float dx, dy, dz;
+            ray_dir(a, (float)cur.x, (float)cur.y, dx, dy, dz, S.lut);
+            const size_t o = (size_t)cur.y * a.W + cur.x;
+            if (cur.idx >= SF_SLAB_BAD) {   // a miss: (0, 0, 0, 1) twice; SF_SLAB_BAD (never made by a correct split): NaN
+                const float v = cur.idx == SF_SLAB_MISS ? 0.0f : __builtin_nanf("");
+                reinterpret_cast<float4*>(a.pos)[o] = make_float4(v, v, v, 1.0f);
+                reinterpret_cast<float4*>(a.nrm)[o] = make_float4(v, v, v, 1.0f);
+            } else {
+                const uint32_t d = cur.d;
+                uint32_t path = cur.path;
+                float xf[12] = { cur.c0.x, cur.c0.y, cur.c0.z, cur.c0.w, cur.c1.x, cur.c1.y,
+                                 cur.c1.z, cur.c1.w, cur.c2.x, cur.c2.y, cur.c2.z, cur.c2.w };
+                float nx[12];
+                // the frames down to the parent, then only the sphere's centre: child_frame's translation column (the
+                // same operations on the same operands)
+                for (uint32_t j = cur.td; j + 1u < d; ++j) {
+                    child_frame(S.child, S.scale, j, path & 15u, xf, nx);
+                    path >>= 4;
 #pragma unroll
-            for (int q = 0; q < 12; ++q) xf[q] = nx[q];
+                    for (int q = 0; q < 12; ++q) xf[q] = nx[q];
+                }
+                float cx = xf[9], cy = xf[10], cz = xf[11];
+                if (d > cur.td) {
+                    const uint32_t ci = path & 15u;
+                    const float sc = S.scale[d - 1u];
+                    const float* B = S.child[ci] + 12;
+                    const float b0 = B[0] * sc, b1 = B[1] * sc, b2 = B[2] * sc, b3 = B[3];
+                    cx = ((xf[0] * b0 + xf[3] * b1) + xf[6] * b2) + xf[9] * b3;
+                    cy = ((xf[1] * b0 + xf[4] * b1) + xf[7] * b2) + xf[10] * b3;
+                    cz = ((xf[2] * b0 + xf[5] * b1) + xf[8] * b2) + xf[11] * b3;
+                }
+                const float tca = (cx * dx + cy * dy) + cz * dz;
+                const float d2 = ((cx * cx + cy * cy) + cz * cz) - tca * tca;
+                HitState h;
+                h.minT = near_root(tca, d2, S.r2_self[d]);
+                h.cx = cx;
+                h.cy = cy;
+                h.cz = cz;
+                h.index = cur.idx;
+                h.depth = (int32_t)d;
+                h.hit = true;
+                float px, py, pz, qx, qy, qz;
+                shade(dx, dy, dz, h, S.lut, px, py, pz, qx, qy, qz);
+                reinterpret_cast<float4*>(a.pos)[o] = make_float4(px, py, pz, 1.0f);
+                reinterpret_cast<float4*>(a.nrm)[o] = make_float4(qx, qy, qz, 1.0f);
+            }
         }
-        float cx = xf[9], cy = xf[10], cz = xf[11];
-        if (d > td) {
-            const uint32_t ci = path & 15u;
-            const float sc = S.scale[d - 1u];
-            const float* B = S.child[ci] + 12;
-            const float b0 = B[0] * sc, b1 = B[1] * sc, b2 = B[2] * sc, b3 = B[3];
-            cx = ((xf[0] * b0 + xf[3] * b1) + xf[6] * b2) + xf[9] * b3;
-            cy = ((xf[1] * b0 + xf[4] * b1) + xf[7] * b2) + xf[10] * b3;
-            cz = ((xf[2] * b0 + xf[5] * b1) + xf[8] * b2) + xf[11] * b3;
-        }
-        const float tca = (cx * dx + cy * dy) + cz * dz;
-        const float d2 = ((cx * cx + cy * cy) + cz * cz) - tca * tca;
-        HitState h;
-        h.minT = near_root(tca, d2, S.r2_self[d]);
-        h.cx = cx;
-        h.cy = cy;
-        h.cz = cz;
-        h.index = idx;
-        h.depth = (int32_t)d;
-        h.hit = true;
-        float px, py, pz, qx, qy, qz;
-        shade(dx, dy, dz, h, S.lut, px, py, pz, qx, qy, qz);
-        reinterpret_cast<float4*>(a.pos)[o] = make_float4(px, py, pz, 1.0f);
-        reinterpret_cast<float4*>(a.nrm)[o] = make_float4(qx, qy, qz, 1.0f);
+        cur = nxt;
+        nxt.ok = ok2;
+        nxt.x = x2;
+        nxt.y = y2;
     }
 }
 

@@ -86,6 +86,8 @@ SIGNATURES = {
     "sf_render": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_render_params)]),
     "sf_render_to": (ctypes.c_int, [_CTX, ctypes.POINTER(sf_render_params), ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_void_p]),
+    "sf_render_frames": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                        ctypes.POINTER(sf_render_params)]),
     "sf_slab_rows": (ctypes.c_uint32, [ctypes.c_uint32] * 4),
     "sf_unpack_bands": (ctypes.c_int, [_CTX, ctypes.c_void_p] + [ctypes.c_uint32] * 5 + [ctypes.c_void_p]),
     "sf_unpack_slabs": (ctypes.c_int, [_CTX, ctypes.c_void_p] + [ctypes.c_uint32] * 6 + [ctypes.c_void_p]),
@@ -159,6 +161,7 @@ SIGNATURES = {
     "sf_dist_set_view": (ctypes.c_int, [ctypes.c_void_p, _F, _F, _F, _F]),
     "sf_dist_render": (ctypes.c_int, [ctypes.c_void_p]),
     "sf_dist_render_bands": (ctypes.c_int, [ctypes.c_void_p]),
+    "sf_dist_render_bands_frames": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, _F]),
     "sf_dist_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "sf_dist_download": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "sf_dist_get_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(sf_stats)]),
@@ -390,6 +393,30 @@ class _FifoLock:
         with self._c:
             self._serving += 1
             self._c.notify_all()
+
+
+def _views12(views) -> np.ndarray:
+    """[(origin, top-left, top-right, bottom-left), ...] (or an n x 12 float32 array) -> a contiguous float32 n x 12
+    array."""
+    if isinstance(views, np.ndarray) and views.dtype == np.float32 and views.ndim == 2 and views.shape[1] == 12 \
+            and views.flags.c_contiguous:
+        return views
+    return np.ascontiguousarray(np.array([[c for v in view for c in v] for view in views], np.float32).reshape(-1, 12))
+
+
+def render_frames(flakes, **kw):
+    """Each flake's current view into its own G-buffer, in ONE multi-frame persistent launch (sf_render_frames):
+    bit for bit what flake.Render(**kw) does for each (whole frames or bands at frame positions)."""
+    import contextlib
+    p = render_params(**kw)
+    arr = (ctypes.c_void_p * len(flakes))(*[f.ctx for f in flakes])
+    with contextlib.ExitStack() as held:   # (every context's lock once, as each Render would take its own; a
+        seen = set()                        # context given twice is the C ABI's SF_EINVAL, not a deadlock here)
+        for f in flakes:
+            if id(f) not in seen:
+                seen.add(id(f))
+                held.enter_context(f._mutex)
+        _check(lib().sf_render_frames(arr, len(flakes), ctypes.byref(p)), "sf_render_frames", flakes[0].ctx)
 
 
 class Sphereflake:
@@ -685,6 +712,13 @@ class Sphereflake:
     def ResetClosestSphereDistance(self):
         _check(lib().sf_reset_closest(self._ctx), "ResetClosestSphereDistance")
 
+    def reset_stats(self):
+        """All three reference counters at once (ResetMaxDepthReached, ResetClosestSphereDistance,
+        ResetRaysPerSecond)."""
+        self.ResetMaxDepthReached()
+        self.ResetClosestSphereDistance()
+        self.ResetRaysPerSecond()
+
     # frame-less progressive mode (Sphereflake.cpp:67-74, 86-214) -------------
     def Progressive(self, seed: int, packets: int, counter0: int | None = None, stream=None):
         """Trace `packets` random 8-ray packets of one reference worker stream (seed, Sobol counter)."""
@@ -903,6 +937,12 @@ class SphereflakeDist:
     def RenderBands(self):
         """One frame as a distributed G-buffer: this rank's bands into its own slot G-buffer, no gather."""
         self._check(lib().sf_dist_render_bands(self._d), "sf_dist_render_bands")
+
+    def RenderBandsFrames(self, views):
+        """The next len(views) frames (each (origin, top-left, top-right, bottom-left)) as RenderBands would render
+        them one by one, in ONE multi-frame persistent launch (sf_dist_render_bands_frames; len(views) <= slots)."""
+        v = _views12(views)
+        self._check(lib().sf_dist_render_bands_frames(self._d, len(views), _fp(v)), "sf_dist_render_bands_frames")
 
     def download_slot(self, slot: int):
         """The G-buffer of one slot's context on this rank (synchronises)."""

@@ -64,10 +64,15 @@ def test_issue_fractions_on_the_frame_period():
                                         (640, 360, 1, 4), (1280, 720, 1, 3), (3840, 2160, 8, 3), (3840, 2160, 1, 3)])
 def test_frames_in_flight_by_share(w, h, n, want):
     """4 frames in flight where rank 0's share of 8x8 tiles is at most 1.5 persistent grids (256 CUs x 32 waves),
-    else 3; an explicit --slots wins (clamped to 1..8)."""
+    else 3; an explicit --slots wins (clamped to batch..16). With multi-frame launches of B frames (round 6), B x
+    GROUPS_IN_FLIGHT slots, and never fewer slots than one launch's frames."""
     assert bench.frames_in_flight(0, 256, w, h, 8, n) == want
     assert bench.frames_in_flight(5, 256, w, h, 8, n) == 5
-    assert bench.frames_in_flight(99, 256, w, h, 8, n) == 8
+    assert bench.frames_in_flight(99, 256, w, h, 8, n) == 16
+    assert bench.frames_in_flight(0, 256, w, h, 8, n, batch=4) == 4 * bench.GROUPS_IN_FLIGHT
+    assert bench.frames_in_flight(2, 256, w, h, 8, n, batch=4) == 4
+    assert bench.frames_per_launch(3, 256, w, h, 8, n) == 3
+    assert bench.frames_per_launch(0, 256, w, h, 8, n) in (bench.BATCH_FULL, bench.BATCH_SHARE)
 
 
 def test_cpu_model_and_vendor_parsed():
