@@ -105,7 +105,8 @@ SHARE_GRID_FRAC = 1.5                # a share of at most this many persistent-g
 GRID_WAVES_PER_CU = 32               # the trace kernel's grid: 4 SIMDs x 8 waves per CU (LDS-limited occupancy)
 
 
-BATCH_FULL, BATCH_SHARE = 1, 1       # frames per launch (frames_per_launch); set from scripts/frames_probe.py
+BATCH_FULL, BATCH_SHARE = 1, 1       # frames per launch (frames_per_launch): one launch per frame -- multi-frame launches
+                                     # measured slower at 1080p and for a 1/8 share (profiles/r6/frames/README.md)
 GROUPS_IN_FLIGHT = 2                 # multi-frame launches in flight: slots = batch x this
 
 

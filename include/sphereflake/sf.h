@@ -381,7 +381,7 @@ int sf_group_slab_bytes(const sf_group* group);
    rank's stats alone). Every rank must issue the same calls in the same order (set_view, render, get_stats) with
    the same views. */
 #define SF_DIST_ID_BYTES 128   /* ncclUniqueId */
-#define SF_DIST_MAX_SLOTS 8
+#define SF_DIST_MAX_SLOTS 16
 typedef struct sf_dist sf_dist;
 /* Rank 0 makes one id per slot and hands them to every rank (any channel: MPI, a torch.distributed broadcast). */
 int sf_dist_unique_id(uint8_t id[SF_DIST_ID_BYTES]);

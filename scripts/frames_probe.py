@@ -43,7 +43,11 @@ def main():
     cfgs = [tuple(int(x) for x in c.split(":")) for c in args.configs.split(",")]
     dists = {c: sf.SphereflakeDist(0, W, H, rank=0, nranks=args.share, slots=c[0]) for c in cfgs}
 
-    def loop(d, B, n, start):
+    def loop(d, B, n, start):   # (B = -1: one frame per launch through RenderBandsFrames, for SF_FRAMES_ONE=1)
+        if B == -1:
+            for i in range(n):
+                d.RenderBandsFrames(np.ascontiguousarray(views[[(start + i) % 40]]))
+            return
         if B == 1:
             for i in range(n):
                 v = views[(start + i) % 40]

@@ -148,6 +148,9 @@ struct sf_ctx {
     uint32_t waves_per_block = SF_TRACE_WAVES;   // tuning knob: env SF_TRACE_WAVES = 1 | 2 | 4
     uint32_t levels_override = 0;                // tuning knob: env SF_LEVELS (LDS levels, 0 = adaptive)
     bool slab_shallow = false;                   // tests only: index slabs as SF_PACKED_INDEX_DIAG (env SF_DIAG_SLAB_SHALLOW)
+    int frames_heavy = -1;                       // A/B: sf_render_frames' interleaved head units per frame (env
+                                                 // SF_FRAMES_HEAVY; -1: the grid's waves / frames)
+    bool frames_one = false;                     // A/B: sf_render_frames takes its kernel for one frame too (env SF_FRAMES_ONE)
     bool persistent = true;                      // tuning knob: env SF_PERSISTENT=0 -> one workgroup per tile group
     uint32_t flags = 0;                          // SF_FLAG_* A/B switches: env SF_FLAGS
     int cus = 256;
@@ -551,6 +554,8 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
         c->levels_override = (l >= 2 && l <= SF_MAX_DEPTH_LIMIT) ? (uint32_t)l : 0u;
     }
     if (const char* ev = std::getenv("SF_DIAG_SLAB_SHALLOW")) c->slab_shallow = std::atoi(ev) != 0;   // (tests only)
+    if (const char* ev = std::getenv("SF_FRAMES_HEAVY")) c->frames_heavy = std::atoi(ev);
+    if (const char* ev = std::getenv("SF_FRAMES_ONE")) c->frames_one = std::atoi(ev) != 0;
     DevGuard g(device);
     const size_t npx = (size_t)width * height;
     const size_t ntiles = (size_t)((width + 7) / 8) * ((height + 7) / 8);
@@ -993,7 +998,7 @@ int sf_render_frames(sf_ctx* const* cs, uint32_t n, const sf_render_params* pp)
     if (band_rows % 8 != 0 || p.band_index >= band_count || p.kernel > SF_KERNEL_PER_RAY) return SF_EINVAL;
     // one launch only where each frame alone would take the bounded one-wave persistent trace with nothing after it
     uint32_t levels = 0;
-    bool one = n > 1;
+    bool one = n > 1 || c0->frames_one;
     for (uint32_t k = 0; k < n && one; ++k) {
         const sf_ctx* c = cs[k];
         bool bounded = false;
@@ -1043,7 +1048,7 @@ int sf_render_frames(sf_ctx* const* cs, uint32_t n, const sf_render_params* pp)
     const bool use_order = c0->order_mode > 0 || (c0->order_mode < 0 && (tiny || large));
     const uint32_t split_buckets = (large && !c0->split_env) ? 0u : c0->split_buckets;
     const uint32_t units_max = (use_order && split_buckets != 0u) ? c0->split_parts * ntiles : ntiles;
-    if ((uint64_t)n * units_max >= 0x80000000ull) return SF_EINVAL;   // (positions below bit 31: the re-trace word)
+    if ((uint64_t)n * units_max >= 0x20000000ull) return SF_EINVAL;   // (positions below 2^29: FrameBatch.magic)
     if (nblk > n * units_max) nblk = n * units_max;
     if (c0->max_blocks && nblk > c0->max_blocks) nblk = c0->max_blocks;
     uint32_t xcds = c0->queues;
@@ -1058,8 +1063,10 @@ int sf_render_frames(sf_ctx* const* cs, uint32_t n, const sf_render_params* pp)
     FrameBatch b;
     std::memset(&b, 0, sizeof b);
     b.nframes = n;
+    b.magic = (uint32_t)((0x100000000ull + n - 1u) / n);
     b.units = ntiles;
-    b.heavy = nblk / n;   // every frame's heaviest units among the waves' static first units
+    b.heavy = c0->frames_heavy >= 0 ? (uint32_t)c0->frames_heavy : nblk / n;   // every frame's heaviest units among
+                                                                                // the waves' static first units
     for (uint32_t k = 0; k < n; ++k) {
         sf_ctx* c = cs[k];
         FrameArgs a = frame_args(c);

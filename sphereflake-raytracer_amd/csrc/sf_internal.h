@@ -185,7 +185,8 @@ struct FrameArgs {
 // the rest follow frame by frame.
 #define SF_BATCH_MAX 8u
 struct FrameBatch {
-    uint32_t nframes, units, heavy, pad;
+    uint32_t nframes, units, heavy;
+    uint32_t magic;                   // ceil(2^32 / nframes): G / nframes = mulhi(G, magic) for G < 2^29
     FrameArgs f[SF_BATCH_MAX];
 };
 

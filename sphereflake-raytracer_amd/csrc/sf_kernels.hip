@@ -472,6 +472,25 @@ __device__ __forceinline__ void stage_root(float* __restrict__ Lbase, const floa
     }
 }
 
+// The same staging without a branch on the lane (the multi-frame trace re-stages the root inside its persistent loop,
+// where a lane-dependent region made the compiler allocate the whole loop's registers worse: 62 -> 30 SGPR spills):
+// lane l writes word l & 15 -- the lanes above 15 repeat a lower lane's store, same address and value.
+__device__ __forceinline__ void stage_root_all_lanes(float* __restrict__ Lbase, const float* root)
+{
+    const uint32_t l = threadIdx.x & 15u;
+    const float rcc = (root[9] * root[9] + root[10] * root[10]) + root[11] * root[11];
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        float rk = 0.f;
+        if (k < 3) rk = root[9 + k];
+        else if (k == 3) rk = rcc;
+        else if ((k & 3) != 3) rk = root[3 * ((k >> 2) - 1) + (k & 3)];
+        v = (l == (uint32_t)k) ? rk : v;
+    }
+    Lbase[l] = v;   // TraverseLds::root()
+}
+
 // PW: packet width of the semantics (0 per ray, 8 (AVX) or 4 (SSE) frame-less packets); PIPE: the latency
 // variant of the per-ray child loop (small frames, whose heaviest tiles' serial DFS is the frame)
 // Lane -> (child bi, column bc) of the cooperative child build: lanes 0..26 the axis columns of child lane % 9
@@ -1878,12 +1897,16 @@ __device__ __forceinline__ void wave_atomic_smin(int32_t* p, int32_t v)
         : "v"(zero), "v"(v), "s"(p)
         : "memory");
 }
+// Read before the atomic, as publish_stats does: thousands of waves leave a frame together, and atomics on one
+// address serialise (~10 ns each) -- issued unconditionally they made a 4-frame launch take twice as long.
 __device__ __forceinline__ void publish_stats_in_loop(const FrameArgs& a, int32_t maxd, float closest)
 {
     const int32_t key = __builtin_amdgcn_readfirstlane(sf_float_key(wave_min(closest)));
     maxd = __builtin_amdgcn_readfirstlane(maxd);
-    if (maxd >= 0) wave_atomic_smax(a.stats + 0, maxd);
-    if (key != sf_float_key(FLT_MAX)) wave_atomic_smin(a.stats + 1, key);
+    const int32_t cur_d = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&a.stats[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const int32_t cur_k = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&a.stats[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (maxd > cur_d) wave_atomic_smax(a.stats + 0, maxd);
+    if (key < cur_k) wave_atomic_smin(a.stats + 1, key);
 }
 
 }  // namespace
@@ -2175,7 +2198,8 @@ __device__ __forceinline__ void trace_frames_body()
     }
     int32_t maxd = -1;
     float closest = FLT_MAX;      // per lane, of frame cur
-    uint32_t cur = 0xffffffffu;   // the frame whose root is staged and whose stats accumulate (uniform)
+    uint32_t cur = 0xffffffffu;   // the frame whose stats accumulate (uniform)
+    uint32_t staged = 0xffffffffu;   // the frame whose root is staged in LDS (uniform)
     uint32_t first = __builtin_amdgcn_readfirstlane(blockIdx.x);
     for (;;) {
         const uint32_t G = first;
@@ -2196,14 +2220,21 @@ __device__ __forceinline__ void trace_frames_body()
             }
             const uint32_t heavy = pb->heavy < units ? pb->heavy : units;
             if (G >= nframes * units) break;
+            // (no integer division per unit: a division by a uniform value is a ~35-instruction scalar sequence, and
+            // four of them per unit measured +18 % SALU against trace_queue_body)
             const uint32_t hh = nframes * heavy;
             if (G < hh) {
-                f = G % nframes;
-                pos = G / nframes;
+                pos = __builtin_amdgcn_readfirstlane(__umulhi(G, pb->magic));   // G / nframes (exact for G < 2^29)
+                f = G - pos * nframes;
             } else {
-                const uint32_t q = G - hh, rest = units - heavy;
-                f = q / rest;
-                pos = heavy + q % rest;
+                uint32_t q = G - hh;
+                const uint32_t rest = units - heavy;
+                f = 0u;
+                while (q >= rest) {   // (<= SF_BATCH_MAX - 1 trips)
+                    q -= rest;
+                    ++f;
+                }
+                pos = heavy + q;
             }
             f = __builtin_amdgcn_readfirstlane(f);
             pos = __builtin_amdgcn_readfirstlane(pos);
@@ -2216,13 +2247,14 @@ __device__ __forceinline__ void trace_frames_body()
                 maxd = -1;
                 closest = FLT_MAX;
             }
-            FrameArgs ar;
-            load_frame(ar, f);
-            stage_root(L, ar.root);
             cur = f;
         }
         FrameArgs at;
         load_frame(at, f);
+        if (f != staged) {   // (the frame's root transform into the wave's LDS image)
+            stage_root_all_lanes(L, at.root);
+            staged = f;
+        }
         uint32_t t = pos, part = 0u;
         if (again) {
             t = G & SF_UNIT_TILE_MASK;
@@ -2683,24 +2715,30 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         w = ((size_t)m * stage_rows + sr) * a.W + x;
         return x < a.W && y < a.H;
     };
-    // Round 6: a two-deep pipeline. While item it is rebuilt, item it + G (G = the grid) already has its node-table
-    // frame in flight (its slab word came one item earlier), and item it + 2G's slab word is loaded: the chain slab
-    // word -> table frame -> frame levels no longer waits on memory twice per item (round 5 prefetched the slab word
-    // only: ~half of the wave cycles waited at full occupancy).
-    struct Item {
-        bool ok;
-        uint32_t x, y, idx, d, td, path;
-        float4 c0, c1, c2;   // the node-table frame of the sphere's ancestor at depth td (hits only)
-    };
-    // the depth from the index (the first heap index of depth k is (9^k - 1) / 8), then only the child digits below
-    // the table's depth, bottom-up (the deepest in the highest nibble, depth td + 1's in the lowest), and the table
-    // frame's loads issued
-    // (the loads are unconditional -- a miss or a lane past the frame reads the root's entry -- so that no branch
-    // around them makes the compiler wait for every load in flight at the join: round 5's pipelined form lost its
-    // overlap to exactly that vmcnt(0))
-    auto prepare = [&](Item& m) {
-        const bool hit = m.ok && m.idx < SF_SLAB_BAD;
-        const uint32_t idx = hit ? m.idx : 0u;
+    // the next item's slab word is loaded while this one is rebuilt (its HBM latency off the chain)
+    uint32_t x, y;
+    size_t w;
+    bool ok = blockIdx.x < items && locate(blockIdx.x, x, y, w);
+    uint32_t idx_next = ok ? stage[w] : SF_SLAB_MISS;
+    for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const uint32_t idx = idx_next;
+        const bool cur = ok;
+        const uint32_t cx_ = x, cy_ = y;
+        ok = it + gridDim.x < items && locate(it + gridDim.x, x, y, w);
+        if (ok) idx_next = stage[w];
+        if (!cur) continue;
+        const uint32_t px_ = cx_, py_ = cy_;
+        float dx, dy, dz;
+        ray_dir(a, (float)px_, (float)py_, dx, dy, dz, S.lut);   // (independent of idx: in flight with its load)
+        const size_t o = (size_t)py_ * a.W + px_;
+        if (idx >= SF_SLAB_BAD) {   // a miss: (0, 0, 0, 1) twice; SF_SLAB_BAD (never made by a correct split): NaN
+            const float v = idx == SF_SLAB_MISS ? 0.0f : __builtin_nanf("");
+            reinterpret_cast<float4*>(a.pos)[o] = make_float4(v, v, v, 1.0f);
+            reinterpret_cast<float4*>(a.nrm)[o] = make_float4(v, v, v, 1.0f);
+            continue;
+        }
+        // the depth from the index (the first heap index of depth k is (9^k - 1) / 8), then only the child digits
+        // below the table's depth, bottom-up: the deepest lands in the highest nibble, depth td + 1's in the lowest
         uint32_t d = 0u;
 #pragma unroll
         for (uint32_t k = 1u, f = 1u; k <= 10u; ++k, f = 9u * f + 1u) d += idx >= f ? 1u : 0u;
@@ -2712,81 +2750,45 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             path = (path << 4) | (anc - 1u - 9u * q);
             anc = q;
         }
-        m.d = d;
-        m.td = td;
-        m.path = path;
-        m.c0 = table[3u * anc];
-        m.c1 = table[3u * anc + 1u];
-        m.c2 = table[3u * anc + 2u];
-    };
-    const uint32_t G = gridDim.x;
-    Item cur, nxt;
-    size_t w;
-    cur.ok = blockIdx.x < items && locate(blockIdx.x, cur.x, cur.y, w);
-    cur.idx = cur.ok ? stage[w] : SF_SLAB_MISS;
-    nxt.ok = blockIdx.x + G < items && locate(blockIdx.x + G, nxt.x, nxt.y, w);
-    uint32_t idx_next = nxt.ok ? stage[w] : SF_SLAB_MISS;
-    prepare(cur);
-    for (uint32_t it = blockIdx.x; it < items; it += G) {
-        // item it + G: its table frame in flight; item it + 2G: its slab word
-        nxt.idx = idx_next;
-        prepare(nxt);
-        uint32_t x2 = 0u, y2 = 0u;
-        const bool ok2 = it + 2u * G < items && locate(it + 2u * G, x2, y2, w);
-        const uint32_t word = stage[ok2 ? w : 0u];   // (unconditional, see prepare)
-        idx_next = ok2 ? word : SF_SLAB_MISS;
-        if (cur.ok) {
-            float dx, dy, dz;
-            ray_dir(a, (float)cur.x, (float)cur.y, dx, dy, dz, S.lut);
-            const size_t o = (size_t)cur.y * a.W + cur.x;
-            if (cur.idx >= SF_SLAB_BAD) {   // a miss: (0, 0, 0, 1) twice; SF_SLAB_BAD (never made by a correct split): NaN
-                const float v = cur.idx == SF_SLAB_MISS ? 0.0f : __builtin_nanf("");
-                reinterpret_cast<float4*>(a.pos)[o] = make_float4(v, v, v, 1.0f);
-                reinterpret_cast<float4*>(a.nrm)[o] = make_float4(v, v, v, 1.0f);
-            } else {
-                const uint32_t d = cur.d;
-                uint32_t path = cur.path;
-                float xf[12] = { cur.c0.x, cur.c0.y, cur.c0.z, cur.c0.w, cur.c1.x, cur.c1.y,
-                                 cur.c1.z, cur.c1.w, cur.c2.x, cur.c2.y, cur.c2.z, cur.c2.w };
-                float nx[12];
-                // the frames down to the parent, then only the sphere's centre: child_frame's translation column (the
-                // same operations on the same operands)
-                for (uint32_t j = cur.td; j + 1u < d; ++j) {
-                    child_frame(S.child, S.scale, j, path & 15u, xf, nx);
-                    path >>= 4;
-#pragma unroll
-                    for (int q = 0; q < 12; ++q) xf[q] = nx[q];
-                }
-                float cx = xf[9], cy = xf[10], cz = xf[11];
-                if (d > cur.td) {
-                    const uint32_t ci = path & 15u;
-                    const float sc = S.scale[d - 1u];
-                    const float* B = S.child[ci] + 12;
-                    const float b0 = B[0] * sc, b1 = B[1] * sc, b2 = B[2] * sc, b3 = B[3];
-                    cx = ((xf[0] * b0 + xf[3] * b1) + xf[6] * b2) + xf[9] * b3;
-                    cy = ((xf[1] * b0 + xf[4] * b1) + xf[7] * b2) + xf[10] * b3;
-                    cz = ((xf[2] * b0 + xf[5] * b1) + xf[8] * b2) + xf[11] * b3;
-                }
-                const float tca = (cx * dx + cy * dy) + cz * dz;
-                const float d2 = ((cx * cx + cy * cy) + cz * cz) - tca * tca;
-                HitState h;
-                h.minT = near_root(tca, d2, S.r2_self[d]);
-                h.cx = cx;
-                h.cy = cy;
-                h.cz = cz;
-                h.index = cur.idx;
-                h.depth = (int32_t)d;
-                h.hit = true;
-                float px, py, pz, qx, qy, qz;
-                shade(dx, dy, dz, h, S.lut, px, py, pz, qx, qy, qz);
-                reinterpret_cast<float4*>(a.pos)[o] = make_float4(px, py, pz, 1.0f);
-                reinterpret_cast<float4*>(a.nrm)[o] = make_float4(qx, qy, qz, 1.0f);
-            }
+        float xf[12], nx[12];
+        {
+            const float4 c0 = table[3u * anc], c1 = table[3u * anc + 1u], c2 = table[3u * anc + 2u];
+            xf[0] = c0.x; xf[1] = c0.y; xf[2] = c0.z; xf[3] = c0.w;
+            xf[4] = c1.x; xf[5] = c1.y; xf[6] = c1.z; xf[7] = c1.w;
+            xf[8] = c2.x; xf[9] = c2.y; xf[10] = c2.z; xf[11] = c2.w;
         }
-        cur = nxt;
-        nxt.ok = ok2;
-        nxt.x = x2;
-        nxt.y = y2;
+        // the frames down to the parent, then only the sphere's centre: child_frame's translation column (the same
+        // operations on the same operands)
+        for (uint32_t j = td; j + 1u < d; ++j) {
+            child_frame(S.child, S.scale, j, path & 15u, xf, nx);
+            path >>= 4;
+#pragma unroll
+            for (int q = 0; q < 12; ++q) xf[q] = nx[q];
+        }
+        float cx = xf[9], cy = xf[10], cz = xf[11];
+        if (d > td) {
+            const uint32_t ci = path & 15u;
+            const float sc = S.scale[d - 1u];
+            const float* B = S.child[ci] + 12;
+            const float b0 = B[0] * sc, b1 = B[1] * sc, b2 = B[2] * sc, b3 = B[3];
+            cx = ((xf[0] * b0 + xf[3] * b1) + xf[6] * b2) + xf[9] * b3;
+            cy = ((xf[1] * b0 + xf[4] * b1) + xf[7] * b2) + xf[10] * b3;
+            cz = ((xf[2] * b0 + xf[5] * b1) + xf[8] * b2) + xf[11] * b3;
+        }
+        const float tca = (cx * dx + cy * dy) + cz * dz;
+        const float d2 = ((cx * cx + cy * cy) + cz * cz) - tca * tca;
+        HitState h;
+        h.minT = near_root(tca, d2, S.r2_self[d]);
+        h.cx = cx;
+        h.cy = cy;
+        h.cz = cz;
+        h.index = idx;
+        h.depth = (int32_t)d;
+        h.hit = true;
+        float px, py, pz, qx, qy, qz;
+        shade(dx, dy, dz, h, S.lut, px, py, pz, qx, qy, qz);
+        reinterpret_cast<float4*>(a.pos)[o] = make_float4(px, py, pz, 1.0f);
+        reinterpret_cast<float4*>(a.nrm)[o] = make_float4(qx, qy, qz, 1.0f);
     }
 }
 
