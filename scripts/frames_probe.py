@@ -61,14 +61,18 @@ def main():
                 d.RenderBandsFrames(np.ascontiguousarray(views[idx]))
                 i += b
 
+    host = {}
+
     def timed(d, B, n, start):
         torch.cuda.synchronize(dev)
         gc.disable()
         t0 = time.perf_counter()
         loop(d, B, n, start)
+        th = time.perf_counter() - t0
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
         gc.enable()
+        host.setdefault(id(d), []).append(th / n * 1e3)
         return dt
 
     # warm up every configuration (clock ramp, first-render order)
@@ -90,7 +94,7 @@ def main():
         print(f"{W}x{H} K={K} share 1/{args.share} slots={c[0]} batch={c[1]}: {args.short} steps "
               f"{s:.4f} ms/frame [{' '.join(f'{x:.4f}' for x in res[c]['short'])}], {args.long} steps {l_:.4f} "
               f"[{' '.join(f'{x:.4f}' for x in res[c]['long'])}], steady {steady:.4f}, "
-              f"fill {(s - steady) * args.short:.4f} ms", flush=True)
+              f"fill {(s - steady) * args.short:.4f} ms, host enqueue {min(host[id(dists[c])]):.4f} ms/frame", flush=True)
     for d in dists.values():
         d.Synchronize()
         d.close()

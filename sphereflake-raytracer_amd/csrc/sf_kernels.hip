@@ -2196,9 +2196,12 @@ __device__ __forceinline__ void trace_frames_body()
         }
         k = __builtin_amdgcn_readfirstlane(k);
     }
-    int32_t maxd = -1;
-    float closest = FLT_MAX;      // per lane, of frame cur
-    uint32_t cur = 0xffffffffu;   // the frame whose stats accumulate (uniform)
+    // per-frame stats in the lanes of two VGPRs -- lane f: frame f's max depth and closest-hit key so far -- published
+    // once per frame when the wave ends: publishing at every frame switch (two agent-scope loads, maybe atomics) put a
+    // ~2-us latency on the switch, which a wave of a banded share meets at nearly every unit
+    uint32_t stat_d = 0xffffffffu;                  // (int -1)
+    uint32_t stat_k = (uint32_t)sf_float_key(FLT_MAX);
+    uint32_t cur = 0xffffffffu;   // the frame of the last unit (uniform)
     uint32_t staged = 0xffffffffu;   // the frame whose root is staged in LDS (uniform)
     uint32_t first = __builtin_amdgcn_readfirstlane(blockIdx.x);
     for (;;) {
@@ -2239,16 +2242,7 @@ __device__ __forceinline__ void trace_frames_body()
             f = __builtin_amdgcn_readfirstlane(f);
             pos = __builtin_amdgcn_readfirstlane(pos);
         }
-        if (f != cur) {
-            if (cur != 0xffffffffu) {   // leaving frame cur: its stats
-                FrameArgs pc;
-                load_frame(pc, cur);
-                publish_stats_in_loop(pc, maxd, closest);
-                maxd = -1;
-                closest = FLT_MAX;
-            }
-            cur = f;
-        }
+        cur = f;
         FrameArgs at;
         load_frame(at, f);
         if (f != staged) {   // (the frame's root transform into the wave's LDS image)
@@ -2282,13 +2276,25 @@ __device__ __forceinline__ void trace_frames_body()
                                                                       again ? (at.flags | SF_FLAG_NO_FRONT_FIRST |
                                                                                SF_FLAG_REDO_PASS)
                                                                             : at.flags);
-        maxd = st.maxd > maxd ? st.maxd : maxd;
-        closest = fminf(closest, st.closest);
+        {   // frame cur's stats: the unit's max depth and closest hit into lane cur of the accumulators
+            const int32_t ud = __builtin_amdgcn_readfirstlane(st.maxd);
+            const int32_t uk = __builtin_amdgcn_readfirstlane(sf_float_key(wave_min(st.closest)));
+            const int32_t od = (int32_t)__builtin_amdgcn_readlane(stat_d, cur);
+            const int32_t ok = (int32_t)__builtin_amdgcn_readlane(stat_k, cur);
+            stat_d = writelane_s((uint32_t)(ud > od ? ud : od), cur, stat_d);
+            stat_k = writelane_s((uint32_t)(uk < ok ? uk : ok), cur, stat_k);
+        }
     }
-    if (cur != 0xffffffffu) {
-        FrameArgs e;
-        load_frame(e, cur);
-        publish_stats(e, maxd, closest, 0u);
+    {   // every frame's stats once (read before the atomics: thousands of waves end together, publish_stats)
+        const uint32_t nframes = kernarg_batch()->nframes;
+        for (uint32_t fr = 0u; fr < nframes; ++fr) {
+            const int32_t dd = (int32_t)__builtin_amdgcn_readlane(stat_d, fr);
+            const int32_t kk = (int32_t)__builtin_amdgcn_readlane(stat_k, fr);
+            if (dd < 0 && kk == sf_float_key(FLT_MAX)) continue;   // (no unit of that frame)
+            FrameArgs e;
+            load_frame(e, fr);
+            publish_stats_in_loop(e, dd, sf_key_float(kk));
+        }
     }
     const auto pb = kernarg_batch();
     if (pb->f[0].clock_probe && blockIdx.x < SF_CLOCK_WAVES) {
