@@ -112,7 +112,8 @@ int sf_set_view(sf_ctx* ctx, const float origin[3], const float top_left[3],
                 const float top_right[3], const float bottom_left[3]);
 
 /* Override the host-computed setup constants (root transform and 9 unit child frames,
-   glm column-major 4x4). For parity tests against fixture dumps. */
+   glm column-major 4x4). For parity tests against fixture dumps. The child frames must be affine
+   (row 3 exactly 0, 0, 0, 1, as Sphereflake.cpp:216-249 makes them): SF_EINVAL otherwise. */
 int sf_set_setup(sf_ctx* ctx, const float child[9][16], const float root[16]);
 
 /* Read back the setup constants currently in use. */

@@ -3,7 +3,12 @@
 (band_count N, band_index 0), traced at `slots` frames in flight on the bench's moving camera path, for split
 rules (SF_SPLIT_BUCKETS: auto = into idle wave slots only; model = the makespan model of sf_order_scan).
 Prints ms per frame of the share, the N x speed-up over the whole frame and the host's enqueue time per frame
-(the loop before the final synchronize). Usage: share_probe.py [W H K]"""
+(the loop before the final synchronize). Usage: share_probe.py [W H K]
+
+Frames in flight: PROBE_SLOTS=policy (the default) gives every N the bench's own policy (bench.frames_in_flight:
+3 for a whole 1080p frame, 4 for a share that leaves most of the grid idle), so the N = 1 basis of every ratio is
+the bench's best single-GPU period (round 5 quoted 1080p ratios against N = 1 at 4 in flight, a slower
+basis); PROBE_SLOTS=1,3 runs every N at each of the given counts, as before. Each line names its N = 1 basis."""
 import os
 import sys
 import time
@@ -14,7 +19,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "sphereflake-raytracer_amd"))
 sys.path.insert(0, REPO)
 import sphereflake_amd as sf  # noqa: E402
-from bench import frame_camera  # noqa: E402
+from bench import frame_camera, frames_in_flight  # noqa: E402
 
 W, H, K = (int(sys.argv[1]), int(sys.argv[2]), float(sys.argv[3])) if len(sys.argv) > 3 else (1920, 1080, 0.25)
 STEPS, WARM = int(os.environ.get("PROBE_STEPS", 120)), int(os.environ.get("PROBE_WARM", 30))
@@ -51,17 +56,23 @@ def run(n, slots, split):
 
 
 ENQ = []
-SLOTS = [int(v) for v in os.environ.get("PROBE_SLOTS", "1,3").split(",")]
-SPLITS = os.environ.get("PROBE_SPLITS", "auto,model").split(",")
+SLOTS_ENV = os.environ.get("PROBE_SLOTS", "policy")
+SLOTS = [0] if SLOTS_ENV == "policy" else [int(v) for v in SLOTS_ENV.split(",")]
+SPLITS = os.environ.get("PROBE_SPLITS", "auto").split(",")
 NS = [int(v) for v in os.environ.get("PROBE_N", "1,2,4,8").split(",")]
+CUS = int(os.environ.get("PROBE_CUS", 256))   # (MI355X: 256 CUs; the bench reads it from the device)
 for slots in SLOTS:
     for split in SPLITS:
         base = None
         row = []
         for n in NS:
             ENQ.clear()
-            ms = np.median([run(n, slots, split) for _ in range(2)])
-            base = ms if n == 1 else base
+            sl = slots or frames_in_flight(0, CUS, W, H, 8, n)
+            ms = np.median([run(n, sl, split) for _ in range(2)])
+            if n == 1:
+                base = ms
+                basis = f"N=1 basis {ms:.4f} ms at {sl} in flight"
             sp = f"{base / ms:.2f}x, " if base else ""
-            row.append(f"N={n} {ms:.4f} ms ({sp}host {min(ENQ):.4f})")
-        print(f"{W}x{H} K={K} slots={slots} split={split}: " + "  ".join(row), flush=True)
+            row.append(f"N={n} {ms:.4f} ms ({sp}{sl} in flight, host {min(ENQ):.4f})")
+        print(f"{W}x{H} K={K} slots={SLOTS_ENV if not slots else slots} split={split} [{basis}]: " + "  ".join(row),
+              flush=True)

@@ -631,6 +631,11 @@ int sf_set_view(sf_ctx* c, const float origin[3], const float tl[3], const float
 int sf_set_setup(sf_ctx* c, const float child[9][16], const float root[16])
 {
     if (!c || !child || !root) return SF_EINVAL;
+    // the kernels fuse the 4th term of every child product (SF_AFFINE_FMA, sf_kernels.hip): exact only for affine unit
+    // child frames, row 3 = (0, 0, 0, 1) -- what the reference's ComputeChildTransformations makes
+    for (int i = 0; i < 9; ++i)
+        for (int col = 0; col < 4; ++col)
+            if (child[i][4 * col + 3] != (col == 3 ? 1.0f : 0.0f)) return SF_EINVAL;
     DevGuard g(c->device);
     std::memcpy(c->child, child, sizeof c->child);
     std::memcpy(c->root, root, sizeof c->root);

@@ -120,6 +120,11 @@ __device__ __forceinline__ float near_root(float tca, float d2, float R2)
 // with it, so a node's frame is the same float values whichever computes it.
 // (child: the 9 unit child frames, scale: the per-depth child translation scales -- from the constant block, or an
 // LDS image of them in the slab unpack)
+// SF_AFFINE_FMA (round 6): the unit child frames are affine -- row 3 of column c is exactly 0 (c < 3) or 1 (c = 3), as
+// glm's translate/rotate make them (Sphereflake.cpp:216-249; sf_set_setup refuses any other) -- so the 4th product
+// P[9 + r] * b3 is exact (+-0 or P[9 + r] itself) and s + P[9 + r] * b3 rounds once either way: fma(P[9 + r], b3, s)
+// is the same float bit for bit (also for -0, inf and NaN), one VALU instead of two. The traversal's cooperative child
+// build (expand) and the slab unpack's centre use the same form.
 __device__ __forceinline__ void child_frame(const float (*child)[16], const float* scale, uint32_t p, uint32_t i,
                                             const float* P, float* out)
 {
@@ -133,7 +138,7 @@ __device__ __forceinline__ void child_frame(const float (*child)[16], const floa
         const float b3 = B[3];
 #pragma unroll
         for (int r = 0; r < 3; ++r)
-            out[3 * c + r] = ((P[r] * b0 + P[3 + r] * b1) + P[6 + r] * b2) + P[9 + r] * b3;
+            out[3 * c + r] = __builtin_fmaf(P[9 + r], b3, (P[r] * b0 + P[3 + r] * b1) + P[6 + r] * b2);   // (SF_AFFINE_FMA)
     }
 }
 __device__ __forceinline__ void child_frame(const DeviceConsts* __restrict__ K, uint32_t p, uint32_t i,
@@ -688,9 +693,9 @@ __device__ __forceinline__ void traverse(const DeviceConsts* __restrict__ K, con
         // column 3 lanes multiply b0..b2 by s, the others by 1 (exact)
         const float sm = bc == 3u ? dtn.z : 1.0f;
         const float b0 = b[0] * sm, b1 = b[1] * sm, b2 = b[2] * sm;
-        const float x = ((p0.x * b0 + p1.x * b1) + p2.x * b2) + pc.x * b[3];
-        const float y = ((p0.y * b0 + p1.y * b1) + p2.y * b2) + pc.y * b[3];
-        const float z = ((p0.z * b0 + p1.z * b1) + p2.z * b2) + pc.z * b[3];
+        const float x = __builtin_fmaf(pc.x, b[3], (p0.x * b0 + p1.x * b1) + p2.x * b2);
+        const float y = __builtin_fmaf(pc.y, b[3], (p0.y * b0 + p1.y * b1) + p2.y * b2);
+        const float z = __builtin_fmaf(pc.z, b[3], (p0.z * b0 + p1.z * b1) + p2.z * b2);
         const float w = (x * x + y * y) + z * z;   // Dot(centre, centre) on the centre lanes (bc = 3)
         // table(levels-1) is never read: entering a child of the deepest provisioned level overflows
         // first. Not allocated, not stored (uniform branch).
@@ -1224,9 +1229,9 @@ __device__ __forceinline__ void traverse_ray(const DeviceConsts* __restrict__ K,
         const float4 dtc = depth_consts_at(K, ko);
         const float sm = bc == 3u ? dtn.z : 1.0f;
         const float b0 = b[0] * sm, b1 = b[1] * sm, b2 = b[2] * sm;
-        const float x = ((p0.x * b0 + p1.x * b1) + p2.x * b2) + pc.x * b[3];
-        const float y = ((p0.y * b0 + p1.y * b1) + p2.y * b2) + pc.y * b[3];
-        const float z = ((p0.z * b0 + p1.z * b1) + p2.z * b2) + pc.z * b[3];
+        const float x = __builtin_fmaf(pc.x, b[3], (p0.x * b0 + p1.x * b1) + p2.x * b2);
+        const float y = __builtin_fmaf(pc.y, b[3], (p0.y * b0 + p1.y * b1) + p2.y * b2);
+        const float z = __builtin_fmaf(pc.z, b[3], (p0.z * b0 + p1.z * b1) + p2.z * b2);
         const float w = (x * x + y * y) + z * z;
         const float R2b = dtc.x;
         // cone cull of child bi (centre lanes 32..40), in squares (see traverse). The test is this kernel's own
@@ -2680,126 +2685,207 @@ extern "C" __global__ __launch_bounds__(256) void sf_node_table(FrameArgs a, flo
 // child_frame for the levels below, then the node's self test (Sphereflake.h:174-224: tca, d2, the near root with
 // r_d^2) gives minT, and shade's position dir * minT and normal Normalize(position - centre). Coalesced 4-B reads
 // along a slab row, 2 x 16-B writes per pixel.
-// Round 5: a grid of resident workgroups, each first copying into LDS the constants every pixel reads at a lane-
-// dependent index -- the rsqrtps table (ray_dir, shade), the 9 unit child frames, the depth scales and self radii^2 --
-// then taking 256-pixel segments (member, slab row, x / 256) in turn. Read through the constant block they were ~15
-// dependent global loads per pixel (PMC, 4K: 57 % of the wave cycles waiting on memory against VALU issue ~0.5).
+// A grid of resident workgroups, each first copying into LDS the constants every pixel reads at a lane-dependent
+// index -- the rsqrtps table (ray_dir, shade), the 9 unit child frames, the depth scales and self radii^2, the first
+// heap index of each depth -- then taking 256-pixel segments (member, slab row, x / 256) G = gridDim.x apart.
+// Round 6:
+//  * two items deep: while item i is rebuilt, item i + G's node-table frame and item i + 2G's slab word are already
+//    loading, and no memory operation sits under a branch. gfx9 counts loads and stores on one in-order counter
+//    (vmcnt), so a load consumed after a store waits for that store too, and at a join of paths that issued different
+//    memory operations the compiler waits for all of them: round 5's loop (a branch around each item's stores, the
+//    miss branch) waited for its own stores before every item (`s_waitcnt vmcnt(0)` at the loop head). Here a lane
+//    past the frame's width redoes the row's last pixel and an item past a member's slab redoes item 0 -- the same
+//    inputs, so the same bits stored twice -- and a miss is rebuilt as the root with its outputs selected after;
+//  * the depth of an index from its leading-zero count and one threshold compare (was ten compares), the correctly
+//    rounded square root and x86 rsqrtps in their fast forms with a wave-uniform fallback to the general ones (never
+//    taken on the views the tests and the bench render), the frame constants read once per launch.
+#define SF_DEPTH_MSB_BITS 0x92491249u   // bit k set iff some depth's first heap index (9^d - 1) / 8 has its MSB at k
+
 struct UnpackLds {
     uint32_t lut[2048];
     float child[9][16];
     float scale[SF_DEPTH_TABLE];
     float r2_self[SF_DEPTH_TABLE];
+    uint32_t first[12];   // first[c] = (9^(c+1) - 1) / 8: the first heap index of depth c + 1 (first[11]: none)
 };
 
+// rsqrtps_x86 for a positive, normal, finite x: the table entry of (exponent parity, mantissa >> 13) less the
+// exponent's half -- ((E - E0) / 2) << 23 with E0 = 127 or 128 of E's parity is (E + (E & 1) - 128) << 22
+__device__ __forceinline__ float rsqrtps_pos(float x, const uint32_t* __restrict__ lut)
+{
+    const uint32_t b = __float_as_uint(x);
+    const uint32_t E = b >> 23;
+    return __uint_as_float(lut[(b >> 13) & 0x7ffu] - ((E + (E & 1u) - 128u) << 22));
+}
+
+// normalize3 (SIMD::Normalize) with rsqrtps_pos, falling back to rsqrtps_x86 for the whole wave when a live lane's
+// length is zero, denormal, negative, infinite or NaN
+__device__ __forceinline__ void normalize3_fast(float& x, float& y, float& z, const uint32_t* __restrict__ lut, bool live)
+{
+    const float len = (x * x + y * y) + z * z;
+    float nr;
+    if (wave_ballot(live && !(__float_as_uint(len) - 0x00800000u < 0x7f000000u)) != 0ull) nr = rsqrtps_x86(len, lut);
+    else nr = rsqrtps_pos(len, lut);
+    const float muls = (len * nr) * nr;
+    const float s = (0.5f * nr) * (3.0f - muls);
+    x = x * s;
+    y = y * s;
+    z = z * s;
+}
+
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void sf_slab_unpack4(
-    FrameArgs a, const uint32_t* __restrict__ stage,
-                                                                   const float4* __restrict__ table,
-                                                                   uint32_t table_depth, uint32_t stage_rows,
-                                                                   uint32_t band_rows, uint32_t n, uint32_t first,
-                                                                   uint32_t members)
+    FrameArgs a, const uint32_t* __restrict__ stage, const float4* __restrict__ table, uint32_t table_depth,
+    uint32_t stage_rows, uint32_t band_rows, uint32_t n, uint32_t first, uint32_t members)
 {
     __shared__ UnpackLds S;
+    const DeviceConsts* __restrict__ K = a.consts;
     {
-        const DeviceConsts* __restrict__ K = a.consts;
         for (uint32_t i = threadIdx.x; i < 2048u; i += 256u) S.lut[i] = K->lut[i];
         if (threadIdx.x < 144u) S.child[threadIdx.x >> 4][threadIdx.x & 15u] = K->child[threadIdx.x >> 4][threadIdx.x & 15u];
         if (threadIdx.x < SF_DEPTH_TABLE) {
             S.scale[threadIdx.x] = K->dt.scale[threadIdx.x];
             S.r2_self[threadIdx.x] = K->dt.r2_self[threadIdx.x];
         }
+        if (threadIdx.x < 12u) {
+            uint32_t f = 1u;
+            for (uint32_t k = 0; k < threadIdx.x; ++k) f = 9u * f + 1u;
+            S.first[threadIdx.x] = threadIdx.x < 11u ? f : 0xffffffffu;
+        }
     }
+    // ray_dir's constants (uniform, read once; ray_dir reads them per call)
+    const float rw = K->rw, rh = K->rh;
+    const bool fast = K->fast_div != 0u;
     __syncthreads();
     const uint32_t segs = (a.W + 255u) >> 8;
     const uint32_t items = members * stage_rows * segs;   // (< 2^32: 16384^2 frames give 2^22)
-    // item -> this lane's pixel (x, frame row y) and slab word; false past the frame (rows past a member's slab)
-    auto locate = [&](uint32_t it, uint32_t& x, uint32_t& y, size_t& w) {
-        const uint32_t seg = it % segs, rest = it / segs;   // (uniform)
+    const uint32_t G = gridDim.x;
+    const uint32_t lane_x = threadIdx.x;
+    // item -> its frame row y, its slab row's first word and its segment's first x (uniform, in SGPRs: located once
+    // per item); the lane's pixel is x = min(xb + lane, W - 1) -- past the width, the row's last pixel again
+    struct Loc { uint32_t y, row, xb; };
+    auto locate = [&](uint32_t it) -> Loc {
+        const uint32_t seg = it % segs, rest = it / segs;
         const uint32_t sr = rest % stage_rows, m = rest / stage_rows;
-        x = (seg << 8) + threadIdx.x;
         const uint32_t k = first + m, i = sr / band_rows, r = sr % band_rows;
-        y = (i * n + k) * band_rows + r;
-        w = ((size_t)m * stage_rows + sr) * a.W + x;
-        return x < a.W && y < a.H;
+        return Loc{ (i * n + k) * band_rows + r, (m * stage_rows + sr) * a.W, seg << 8 };
     };
-    // the next item's slab word is loaded while this one is rebuilt (its HBM latency off the chain)
-    uint32_t x, y;
-    size_t w;
-    bool ok = blockIdx.x < items && locate(blockIdx.x, x, y, w);
-    uint32_t idx_next = ok ? stage[w] : SF_SLAB_MISS;
-    for (uint32_t it = blockIdx.x; it < items; it += gridDim.x) {
-        const uint32_t idx = idx_next;
-        const bool cur = ok;
-        const uint32_t cx_ = x, cy_ = y;
-        ok = it + gridDim.x < items && locate(it + gridDim.x, x, y, w);
-        if (ok) idx_next = stage[w];
-        if (!cur) continue;
-        const uint32_t px_ = cx_, py_ = cy_;
-        float dx, dy, dz;
-        ray_dir(a, (float)px_, (float)py_, dx, dy, dz, S.lut);   // (independent of idx: in flight with its load)
-        const size_t o = (size_t)py_ * a.W + px_;
-        if (idx >= SF_SLAB_BAD) {   // a miss: (0, 0, 0, 1) twice; SF_SLAB_BAD (never made by a correct split): NaN
-            const float v = idx == SF_SLAB_MISS ? 0.0f : __builtin_nanf("");
-            reinterpret_cast<float4*>(a.pos)[o] = make_float4(v, v, v, 1.0f);
-            reinterpret_cast<float4*>(a.nrm)[o] = make_float4(v, v, v, 1.0f);
-            continue;
-        }
-        // the depth from the index (the first heap index of depth k is (9^k - 1) / 8), then only the child digits
-        // below the table's depth, bottom-up: the deepest lands in the highest nibble, depth td + 1's in the lowest
-        uint32_t d = 0u;
-#pragma unroll
-        for (uint32_t k = 1u, f = 1u; k <= 10u; ++k, f = 9u * f + 1u) d += idx >= f ? 1u : 0u;
-        d += idx >= 3922632451u ? 1u : 0u;   // (depth 11: (9^11 - 1) / 8)
+    // item 0 has the lowest frame row of the launch: without it no item has a row
+    const Loc l0 = locate(0u);
+    if (l0.y >= a.H) return;
+    // the item it rebuilds: it itself, or item 0 past the items or past a member's slab
+    auto item = [&](uint32_t it) -> Loc {
+        const Loc l = locate(it < items ? it : 0u);
+        return it < items && l.y < a.H ? l : l0;
+    };
+    auto lane_px = [&](const Loc& l) -> uint32_t { return min(l.xb + lane_x, a.W - 1u); };
+    // one item in flight: its location, slab word, and once prepared its depth, table depth, the child digits below
+    // the table's depth (the deepest in the highest nibble, depth td + 1's in the lowest) and its ancestor's table frame
+    struct Slot {
+        Loc l;
+        uint32_t idx, d, td, path;
+        float4 f0, f1, f2;
+    };
+    auto prepare = [&](Slot& q) {
+        const uint32_t e = q.idx < SF_SLAB_BAD ? q.idx : 0u;   // (a miss: the root, its outputs replaced)
+        const uint32_t c = __builtin_popcount(SF_DEPTH_MSB_BITS & (0x7fffffffu >> __builtin_clz(e | 1u)));
+        const uint32_t d = c + (e >= S.first[c] ? 1u : 0u);
         const uint32_t td = d < table_depth ? d : table_depth;
-        uint32_t anc = idx, path = 0u;
+        uint32_t anc = e, p = 0u;
         for (uint32_t j = d; j > td; --j) {
-            const uint32_t q = (anc - 1u) / 9u;
-            path = (path << 4) | (anc - 1u - 9u * q);
-            anc = q;
+            const uint32_t qq = (anc - 1u) / 9u;
+            p = (p << 4) | (anc - 1u - 9u * qq);
+            anc = qq;
         }
-        float xf[12], nx[12];
-        {
-            const float4 c0 = table[3u * anc], c1 = table[3u * anc + 1u], c2 = table[3u * anc + 2u];
-            xf[0] = c0.x; xf[1] = c0.y; xf[2] = c0.z; xf[3] = c0.w;
-            xf[4] = c1.x; xf[5] = c1.y; xf[6] = c1.z; xf[7] = c1.w;
-            xf[8] = c2.x; xf[9] = c2.y; xf[10] = c2.z; xf[11] = c2.w;
+        q.d = d;
+        q.td = td;
+        q.path = p;
+        q.f0 = table[3u * anc];
+        q.f1 = table[3u * anc + 1u];
+        q.f2 = table[3u * anc + 2u];
+    };
+    // item it in slot P (its frame loaded), item it + G in slot Q (its slab word loaded): Q's frame loads and item
+    // it + 2G's slab word (into P, once P's item is written) go out first, then P's pixel is rebuilt and stored
+    auto step = [&](Slot& P, Slot& Q, uint32_t it) {
+        prepare(Q);
+        const Loc l2 = item(it + 2u * G);
+        const uint32_t idx2 = stage[l2.row + lane_px(l2)];
+
+        const uint32_t px_ = lane_px(P.l), py_ = P.l.y;
+        float dx, dy, dz;
+        {   // ray_dir with the constants read above
+            const float fx = (float)px_, fy = (float)py_;
+            float u, v;
+            if (fast) {
+                const float qu = fx * rw, qv = fy * rh;
+                u = __builtin_fmaf(__builtin_fmaf(-qu, a.fw, fx), rw, qu);
+                v = __builtin_fmaf(__builtin_fmaf(-qv, a.fh, fy), rh, qv);
+            } else {
+                u = fx / a.fw;
+                v = fy / a.fh;
+            }
+            dx = ((a.tl[0] + a.dh[0] * u) + a.dv[0] * v) - a.o[0];
+            dy = ((a.tl[1] + a.dh[1] * u) + a.dv[1] * v) - a.o[1];
+            dz = ((a.tl[2] + a.dh[2] * u) + a.dv[2] * v) - a.o[2];
+            normalize3_fast(dx, dy, dz, S.lut, true);
         }
+        const bool hit = P.idx < SF_SLAB_BAD;
+        float xf[12] = { P.f0.x, P.f0.y, P.f0.z, P.f0.w, P.f1.x, P.f1.y, P.f1.z, P.f1.w, P.f2.x, P.f2.y, P.f2.z, P.f2.w };
+        uint32_t path = P.path;
         // the frames down to the parent, then only the sphere's centre: child_frame's translation column (the same
         // operations on the same operands)
-        for (uint32_t j = td; j + 1u < d; ++j) {
-            child_frame(S.child, S.scale, j, path & 15u, xf, nx);
+        for (uint32_t j = P.td; j + 1u < P.d; ++j) {
+            float nf[12];
+            child_frame(S.child, S.scale, j, path & 15u, xf, nf);
             path >>= 4;
 #pragma unroll
-            for (int q = 0; q < 12; ++q) xf[q] = nx[q];
+            for (int q = 0; q < 12; ++q) xf[q] = nf[q];
         }
-        float cx = xf[9], cy = xf[10], cz = xf[11];
-        if (d > td) {
-            const uint32_t ci = path & 15u;
-            const float sc = S.scale[d - 1u];
-            const float* B = S.child[ci] + 12;
+        float cx, cy, cz;
+        {
+            const float sc = S.scale[P.d > 0u ? P.d - 1u : 0u];
+            const float* B = S.child[path & 15u] + 12;   // (path & 15 <= 8; 0 where the table holds the sphere)
             const float b0 = B[0] * sc, b1 = B[1] * sc, b2 = B[2] * sc, b3 = B[3];
-            cx = ((xf[0] * b0 + xf[3] * b1) + xf[6] * b2) + xf[9] * b3;
-            cy = ((xf[1] * b0 + xf[4] * b1) + xf[7] * b2) + xf[10] * b3;
-            cz = ((xf[2] * b0 + xf[5] * b1) + xf[8] * b2) + xf[11] * b3;
+            const float ex = __builtin_fmaf(xf[9], b3, (xf[0] * b0 + xf[3] * b1) + xf[6] * b2);   // (SF_AFFINE_FMA)
+            const float ey = __builtin_fmaf(xf[10], b3, (xf[1] * b0 + xf[4] * b1) + xf[7] * b2);
+            const float ez = __builtin_fmaf(xf[11], b3, (xf[2] * b0 + xf[5] * b1) + xf[8] * b2);
+            const bool below = P.d > P.td;
+            cx = below ? ex : xf[9];
+            cy = below ? ey : xf[10];
+            cz = below ? ez : xf[11];
         }
         const float tca = (cx * dx + cy * dy) + cz * dz;
         const float d2 = ((cx * cx + cy * cy) + cz * cz) - tca * tca;
-        HitState h;
-        h.minT = near_root(tca, d2, S.r2_self[d]);
-        h.cx = cx;
-        h.cy = cy;
-        h.cz = cz;
-        h.index = idx;
-        h.depth = (int32_t)d;
-        h.hit = true;
-        float px, py, pz, qx, qy, qz;
-        shade(dx, dy, dz, h, S.lut, px, py, pz, qx, qy, qz);
-        reinterpret_cast<float4*>(a.pos)[o] = make_float4(px, py, pz, 1.0f);
-        reinterpret_cast<float4*>(a.nrm)[o] = make_float4(qx, qy, qz, 1.0f);
+        const float R2 = S.r2_self[P.d];
+        const float xs = R2 - d2;
+        float t;   // (a hit's own self test passed: xs >= 0)
+        if (wave_ballot(hit && !(xs >= 0x1p-96f)) != 0ull) t = near_root(tca, d2, R2);
+        else t = near_root_big(tca, xs);
+        // shade (Sphereflake.h:218-224)
+        const float px = dx * t, py = dy * t, pz = dz * t;
+        float qx = px - cx, qy = py - cy, qz = pz - cz;
+        normalize3_fast(qx, qy, qz, S.lut, hit);
+        const float mv = P.idx == SF_SLAB_MISS ? 0.0f : __builtin_nanf("");   // (SF_SLAB_BAD: never made by a correct split)
+        const size_t o = (size_t)py_ * a.W + px_;
+        reinterpret_cast<float4*>(a.pos)[o] = hit ? make_float4(px, py, pz, 1.0f) : make_float4(mv, mv, mv, 1.0f);
+        reinterpret_cast<float4*>(a.nrm)[o] = hit ? make_float4(qx, qy, qz, 1.0f) : make_float4(mv, mv, mv, 1.0f);
+        P.l = l2;
+        P.idx = idx2;
+    };
+
+    Slot A, B;
+    A.l = item(blockIdx.x);
+    A.idx = stage[A.l.row + lane_px(A.l)];
+    B.l = item(blockIdx.x + G);
+    B.idx = stage[B.l.row + lane_px(B.l)];
+    prepare(A);
+    // unrolled twice, so the two slots swap roles without register moves
+    for (uint32_t it = blockIdx.x; it < items; it += 2u * G) {
+        step(A, B, it);
+        if (it + G >= items) break;
+        step(B, A, it + G);
     }
 }
 
-// Re-traces flagged tiles with SF_MAX_LEVELS levels. Grid-stride over the list; reads this
-// render's counter and zeroes the other one (the next render's), so no memset is needed.
 extern "C" __global__ __launch_bounds__(64) void sf_fixup_wave(FrameArgs a, const uint32_t* overflow_list,
                                                                uint32_t* counters, uint32_t parity)
 {
