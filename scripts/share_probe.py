@@ -23,6 +23,7 @@ from bench import frame_camera, frames_in_flight  # noqa: E402
 
 W, H, K = (int(sys.argv[1]), int(sys.argv[2]), float(sys.argv[3])) if len(sys.argv) > 3 else (1920, 1080, 0.25)
 STEPS, WARM = int(os.environ.get("PROBE_STEPS", 120)), int(os.environ.get("PROBE_WARM", 30))
+SETTLE_MS = float(os.environ.get("PROBE_SETTLE_MS", 150))
 if os.environ.get("PROBE_TORCH"):   # A/B: the HIP runtime as a torch process has it (bench.py)
     import torch
     torch.cuda.set_device(0)
@@ -40,8 +41,14 @@ def run(n, slots, split):
             c.Render(band_rows=8, band_count=n, band_index=0)
         for i in range(WARM):
             frame(i)
-        for c in cs:
-            c.Synchronize()
+        # settle the shader clock as bench.py does (--settle-ms): frames under load for SETTLE_MS before the timed
+        # loop -- a 1080p loop of 150 frames (11 ms) otherwise runs inside the ~60-ms clock ramp
+        t_settle = time.perf_counter()
+        while (time.perf_counter() - t_settle) * 1e3 < SETTLE_MS:
+            for i in range(WARM):
+                frame(i)
+            for c in cs:
+                c.Synchronize()
         t = time.perf_counter()
         for i in range(STEPS):
             frame(WARM + i)

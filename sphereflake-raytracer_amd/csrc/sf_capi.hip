@@ -265,6 +265,7 @@ struct sf_ctx {
     int order_record_env = -1;         // env SF_ORDER_RECORD=0|1: tile costs recorded only by the render a rebuild
                                        // reads / by every render (default: only on frames over twice the grid)
     bool split_env = false;            // SF_SPLIT_BUCKETS given
+    int halves = -1;                   // env SF_HALVES: row-major units as tile halves (SF_FLAG_HALVES); -1 = by policy
     // The frame-less prefetch stream at the device's greatest priority (env SF_PF_PRIO=0: normal): HIP deals streams
     // over GPU_MAX_HW_QUEUES (4) hardware queues, and in a process that made other streams first (the bench) the
     // prefetch stream shared the context stream's queue, serialising the next batch's draws behind this batch's
@@ -534,6 +535,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
         c->split_buckets = std::strcmp(ev, "model") == 0 ? SF_SPLIT_MODEL
                          : std::strcmp(ev, "auto") == 0 ? SF_SPLIT_AUTO : (uint32_t)std::atoi(ev);
     if (std::getenv("SF_SPLIT_BUCKETS")) c->split_env = true;
+    if (const char* ev = std::getenv("SF_HALVES")) c->halves = std::atoi(ev);
     bool subtree = false;
     if (const char* ev = std::getenv("SF_SPLIT_PARTS")) {
         subtree = std::strcmp(ev, "subtree") == 0;
@@ -861,8 +863,12 @@ static int launch(sf_ctx* c, const sf_render_params* pp, float* pos, float* nrm,
             const bool large = !small && band_count == 1u;
             const bool use_order = c->order_mode > 0 || (c->order_mode < 0 && (tiny || large));
             const uint32_t split_buckets = (large && !c->split_env) ? 0u : c->split_buckets;
+            // row-major halves (SF_FLAG_HALVES): every tile as two units of its pixel rows 0-3 / 4-7
+            const bool halves = !use_order && c->halves > 0;
+            if (halves) a.flags |= SF_FLAG_HALVES;
             // work units: tiles, or up to `split_parts` per tile when the schedule may split tiles
-            const uint32_t units_max = (use_order && split_buckets != 0u) ? c->split_parts * ntiles : ntiles;
+            const uint32_t units_max = (use_order && split_buckets != 0u) ? c->split_parts * ntiles
+                                                                          : halves ? 2u * ntiles : ntiles;
             const uint32_t need = (units_max + wpb - 1) / wpb;
             if (nblk > need) nblk = need;
             if (c->max_blocks && nblk > c->max_blocks) nblk = c->max_blocks;

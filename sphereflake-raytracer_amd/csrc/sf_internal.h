@@ -98,6 +98,9 @@
 // part number mod 4; the part that finishes last merges the 4 per-pixel results (nearest, the reference's tie rule)
 // and writes the tile (trace_tile). Quarter units (pixel parts) otherwise.
 #define SF_FLAG_SUBTREE 0x2000u
+// row-major units are tile halves (pixel rows 0-3 / 4-7 of tile u / 2): a frame of fewer tiles than wave slots -- a
+// member's share -- then ends on half its heaviest tile's traversal (round 6, A/B: SF_HALVES)
+#define SF_FLAG_HALVES 0x4000u
 
 struct DepthTables {
     float r2_bound[SF_DEPTH_TABLE];   // (2 r_d)^2  bounding sphere (Sphereflake.h:108-110)

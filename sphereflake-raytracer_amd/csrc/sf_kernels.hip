@@ -1981,6 +1981,8 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
 #else
         nunits = a.order_meta[0];
 #endif
+    } else if (a.flags & SF_FLAG_HALVES) {
+        nunits = 2u * ntiles;
     }
     stage_root(L, a.root);
     const float4 bcol = build_column(a.consts);
@@ -2051,6 +2053,9 @@ __device__ __forceinline__ void trace_queue_body(const FrameArgs& a)
             if (pr == 2u && !(at.flags & SF_FLAG_PRIO_FLAT)) __builtin_amdgcn_s_setprio(3);
             else if (pr != 0u) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(0);
+        } else if (at.flags & SF_FLAG_HALVES) {   // (row-major halves: unit g = half g & 1 of tile g / 2)
+            t = g >> 1;
+            part = SF_PART_HALF0 + (g & 1u);
         }
         const uint64_t u_start = (at.flags & SF_FLAG_DIAG_UNITS) ? __builtin_amdgcn_s_memrealtime() : 0ull;
         // the next unit's ticket, taken when this tile's traversal ends (see trace_tile)

@@ -835,3 +835,22 @@ def test_active_ray_compaction_kernel_bit_exact(name, monkeypatch):
                 assert bad_rows(fx["row_digest_aux"], aux_digests(mint, idx)) == [], (name, k)
         st = s.stats()
     assert st.max_depth == fx["stats"]["max_depth"] and st.overflow_tiles == 0
+
+
+@pytest.mark.parametrize("name", ["t3", "t5"])
+def test_row_major_halves_bit_exact(name, monkeypatch):
+    """SF_HALVES=1 (SF_FLAG_HALVES, round-6 A/B): row-major frames traced as tile halves (pixel rows 0-3 / 4-7, two
+    waves per tile) equal the golden frames bit for bit, twice in a row (the queues' second parity)."""
+    monkeypatch.setenv("SF_HALVES", "1")
+    monkeypatch.setenv("SF_ORDER", "0")
+    fx = load_frame(name)
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    exp = load_npz(name)
+    with sf.Sphereflake(W, H) as s:
+        s.SetCamera(sf.config_camera(W, H, K))
+        for _ in range(2):
+            s.Render(emit_aux=True)
+            pos, nrm, mint, idx = s.download(aux=True)
+            for k, got in (("pos4", pos), ("nrm4", nrm), ("minT", mint), ("index", idx)):
+                assert np.array_equal(np.ascontiguousarray(got).view(np.uint8),
+                                      np.ascontiguousarray(exp[k]).view(np.uint8)), (k, name)
