@@ -71,6 +71,7 @@ CUS = int(os.environ.get("PROBE_CUS", 256))   # (MI355X: 256 CUs; the bench read
 for slots in SLOTS:
     for split in SPLITS:
         base = None
+        basis = "no N=1 run"
         row = []
         for n in NS:
             ENQ.clear()
