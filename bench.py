@@ -43,7 +43,16 @@ import subprocess
 import sys
 import time
 
-import numpy as np
+# Hardware queues per process (the HIP runtime's GPU_MAX_HW_QUEUES, default 4). Every frame in flight has a stream of
+# its own (plus the order, prefetch and receive streams); with 4 queues, streams share them and one slot's kernel waits
+# in order behind another's. Round 6: a 1080p member's share over 8 GPUs at 8 frames in flight 0.0146 ms with 4
+# queues, 0.0121 with 16; the whole frame at 3 in flight unchanged (profiles/r6/multi/queues.txt). Raised to 16 before
+# the HIP runtime starts (its first call); a larger value already in the environment is kept.
+HW_QUEUES = int(os.environ.get("SF_HW_QUEUES", "16") or 0)   # (SF_HW_QUEUES=0: leave the runtime's setting, A/B)
+if HW_QUEUES > 0 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < HW_QUEUES:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
+
+import numpy as np  # noqa: E402
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "sphereflake-raytracer_amd"))
@@ -102,6 +111,10 @@ SLOTS_FULL, SLOTS_SHARE = 3, 4       # 1080p: 3 in flight 0.0751 ms steady, 4 0.
                                      # 6 0.020 (the process's 4 hardware queues); over 4: 0.0247 / 0.0235; over 2:
                                      # 0.0452 / 0.0459 (profiles/r4/slots/)
 SHARE_GRID_FRAC = 1.5                # a share of at most this many persistent-grid waves' worth of tiles takes 4
+SLOTS_TINY, TINY_GRID_FRAC = 8, 0.75  # round 6, with 16 hardware queues (HW_QUEUES): a share of at most 3/4 of the grid's
+                                     # waves (every tile a wave of its own, the frame bound by its heaviest tiles' traversal)
+                                     # takes 8 -- 1080p over 8 GPUs 0.0143-0.0146 -> 0.0121 ms; over 4, 4 stays best (0.0193
+                                     # vs 0.0198-0.0199 at 6-8), whole frames 3 (profiles/r6/multi/queues.txt)
 GRID_WAVES_PER_CU = 32               # the trace kernel's grid: 4 SIMDs x 8 waves per CU (LDS-limited occupancy)
 
 
@@ -130,6 +143,9 @@ def frames_in_flight(requested, cus, width, height, band_rows, n, batch=1):
         return batch * GROUPS_IN_FLIGHT
     rows = sf.lib().sf_slab_rows(height, band_rows, n, 0) if n > 1 else height
     tiles = -(-width // 8) * -(-rows // 8)
+    if n > 1 and tiles <= TINY_GRID_FRAC * GRID_WAVES_PER_CU * cus \
+            and int(os.environ.get("GPU_MAX_HW_QUEUES", 4)) >= SLOTS_TINY:
+        return SLOTS_TINY   # (band shares only: a whole 640x360 frame measured 0.0186-0.0189 ms at 8 vs 0.0172 at 4)
     return SLOTS_SHARE if tiles <= SHARE_GRID_FRAC * GRID_WAVES_PER_CU * cus else SLOTS_FULL
 
 
@@ -1098,7 +1114,8 @@ def main():
                                    f"depth {st.max_depth})" + (f", BASELINE {cfg_name}" if cfg_name else "")
                                    + f", moving camera, {args.kernel} kernel",
                        "width": width, "height": height, "K": args.K, "max_depth": st.max_depth, "camera": "moving",
-                       "slots": slots, "frames_per_launch": batch, "parallelism": par},
+                       "slots": slots, "frames_per_launch": batch,
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4), "parallelism": par},
             "frame_ms": round(t_step * 1e3, 4),
             "frame_latency_ms": round(r["latency_ms"], 4),
             "first_render_ms": round(r["first_render_ms"], 4),

@@ -13,6 +13,9 @@ import os
 import sys
 import time
 
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:   # (bench.HW_QUEUES, before the HIP runtime starts)
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
 import numpy as np
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
