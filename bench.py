@@ -729,7 +729,7 @@ def check_golden_rows(pos, nrm, golden, rows):
 
 def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows, nranks, frame_of,
               fixed=False, latency=False, first=False, gather=False, settle_ms=SETTLE_MS, long_steps=0, check=False,
-              batch=1):
+              batch=1, timing=True):
     """One timed loop of the sf_dist path: `steps` frames (frame_of(i) of the camera path at step i) after
     `warmup`, `slots` in flight, over `nranks` ranks (1: this GPU alone, every rank its own frames); each frame
     is every rank's bands into its own G-buffer (the distributed G-buffer), or with `gather` also assembled on
@@ -764,12 +764,12 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
     # started after it ran at 2200-2240 MHz instead of ~2375 (0.085 vs 0.0785 ms per frame, profiles/r4/clock/).
     # Switched on again after the settle, it only restarts the sample ring (host state, no GPU call).
     kp = slot_period(steps, slots)
-    for s in range(slots):
+    for s in range(slots if timing else 0):
         d.kernel_timing(s, True, period=kp)
     t_w = time.perf_counter()
     issuer.issue(FrameIssuer.view_rows(views[:warmup]))
     out["settle_frames"] = settle(d, render, views, max(1, warmup), t_w, settle_ms, issuer)
-    for s in range(slots):
+    for s in range(slots if timing else 0):
         d.kernel_timing(s, True, period=kp)
     d.reset_stats()
 
@@ -807,7 +807,7 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
 
     out["t_step"] = timed(steps, lambda i: views[warmup + i]) / steps
     tk, clk = [], []
-    for s in range(slots):
+    for s in range(slots if timing else 0):
         tk += list(d.kernel_timing(s, n=64))
         clk += list(d.kernel_clocks(s, n=64))
         d.kernel_timing(s, False)
@@ -829,11 +829,11 @@ def dist_loop(ctl, torch, dev, width, height, k, steps, warmup, slots, band_rows
         # (a short settle first: the readouts above left the GPU idle for a few ms)
         settle(d, render, views, max(1, warmup), time.perf_counter(), LONG_SETTLE_MS, issuer)
         kpl = slot_period(long_steps, slots)
-        for s in range(slots):   # the live clock of this loop too (the chip's clock moves between loops)
+        for s in range(slots if timing else 0):   # the live clock of this loop too (the chip's clock moves between loops)
             d.kernel_timing(s, True, period=kpl)
         t_long = timed(long_steps, lambda i: view_at(warmup + steps + i))
         clk_l = []
-        for s in range(slots):
+        for s in range(slots if timing else 0):
             clk_l += list(d.kernel_clocks(s, n=64))
             d.kernel_timing(s, False)
         period = (t_long - out["t_step"] * steps) / (long_steps - steps)
@@ -1043,6 +1043,28 @@ def main():
                            "clock_mhz_live": round(r4["clock_mhz"], 1) if r4["clock_mhz"] else None}}
         r4["dist"].close()
 
+    # Multi-GPU scaling projected on this one GPU (N = 1 runs only): rank 0's bands of an N-way split -- the member
+    # with the most rows -- traced at the bench's own frames-in-flight policy, N = 2 / 4 / 8, each with its steady
+    # period from a second loop; the speedup is against this run's own N = 1 steady period. Labelled a projection: the
+    # N-GPU run itself is `bench.py --gpus N` (value = the distributed frame).
+    shares = None
+    SHARES_TIMING = os.environ.get("SF_BENCH_SHARES_TIMING", "0") == "1"   # (A/B: the kernel-timing events on)
+    if n == 1 and args.mode == "dist" and not args.no_extras and "pipeline" in r:
+        base = r["pipeline"]["steady_frame_ms"]
+        shares = {"basis_steady_ms": base, "note": (
+            "ONE GPU tracing rank 0's interleaved band share of an N-way split (the member with the most rows), at the "
+            "bench's frames-in-flight policy, 60 timed steps + a 600-step loop for the steady period (kernel-timing events off); speedup = this "
+            "run's N = 1 steady period / the share's; projected_mrays = W x H / the share's steady period. A "
+            "projection of the distributed G-buffer at N GPUs, not an N-GPU run")}
+        for nn in (2, 4, 8):
+            sl = frames_in_flight(args.slots, cus, width, height, args.band_rows, nn, 1)
+            rs = dist_loop(ctl, torch, dev, width, height, args.K, 60, 15, sl, args.band_rows, nn, lambda i: i,
+                           settle_ms=args.settle_ms, long_steps=600, timing=SHARES_TIMING)
+            rs["dist"].close()
+            sp = rs.get("pipeline", {}).get("steady_frame_ms") or rs["t_step"] * 1e3
+            shares[f"n{nn}"] = {"slots": sl, "ms_per_step": round(rs["t_step"] * 1e3, 5), "steady_ms": round(sp, 5),
+                                "speedup": round(base / sp, 3), "projected_mrays": round(width * height / sp / 1e3, 1)}
+
     post = d2h = prog = None
     if rank == 0 and n == 1 and not args.no_extras:
         # the consumers of the G-buffer on a plain context: SSAO post-process, D2H into the
@@ -1147,6 +1169,8 @@ def main():
                 out["config"]["parallelism"] += f" [rehearsal: {n} ranks on {ndev} GPU(s), no RCCL gather]"
         if c4 is not None:
             out["configs"] = {"c4": c4}
+        if shares is not None:
+            out["member_shares"] = shares
         if post is not None:
             out["post"], out["d2h"], out["frameless"] = post, d2h, prog
         if not args.no_cpu_baseline and n == 1:

@@ -854,3 +854,21 @@ def test_row_major_halves_bit_exact(name, monkeypatch):
             for k, got in (("pos4", pos), ("nrm4", nrm), ("minT", mint), ("index", idx)):
                 assert np.array_equal(np.ascontiguousarray(got).view(np.uint8),
                                       np.ascontiguousarray(exp[k]).view(np.uint8)), (k, name)
+
+
+def test_set_setup_refuses_non_affine_child_frames():
+    """The kernels fuse the 4th term of every child product (SF_AFFINE_FMA: exact only when row 3 of every unit child
+    frame is 0, 0, 0, 1, as the reference's ComputeChildTransformations makes them), so sf_set_setup refuses any other
+    child frames with SF_EINVAL and keeps the setup it had; the affine setup read back is accepted unchanged."""
+    with sf.Sphereflake(64, 32) as s:
+        child, root = s.GetSetup()
+        assert np.all(child.reshape(9, 4, 4)[:, :3, 3] == 0.0) and np.all(child.reshape(9, 4, 4)[:, 3, 3] == 1.0)
+        s.SetSetup(child, root)
+        for col, val in ((0, 1e-30), (3, 1.0 + 2.0 ** -23), (1, -0.0 + 0.5)):
+            bad = child.copy().reshape(9, 16)
+            bad[4, 4 * col + 3] = val
+            with pytest.raises(sf.SphereflakeError) as e:
+                s.SetSetup(bad, root)
+            assert e.value.code == sf.SF_EINVAL
+        c2, r2 = s.GetSetup()
+        assert np.array_equal(c2.view(np.uint32), child.view(np.uint32)) and np.array_equal(r2.view(np.uint32), root.view(np.uint32))
