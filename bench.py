@@ -119,7 +119,11 @@ GRID_WAVES_PER_CU = 32               # the trace kernel's grid: 4 SIMDs x 8 wave
 
 
 BATCH_FULL, BATCH_SHARE = 1, 1       # frames per launch (frames_per_launch): one launch per frame -- multi-frame launches
-                                     # measured slower at 1080p and for a 1/8 share (profiles/r6/frames/README.md)
+                                     # measured slower at 1080p and for a 1/4 share (profiles/r6/frames/README.md)
+BATCH_TINY = 1                       # (round 6: launches of 8 frames for a 1080p share over 8 GPUs, two in flight on 16
+                                     # queues, reach 0.0100-0.0103 ms per frame in most loops but 0.019-0.025 in others --
+                                     # alternating reps in one process, every rep in another -- against a stable 0.0110-0.0123
+                                     # for one launch per frame at 8 in flight: not the default, profiles/r6/frames/README.md)
 GROUPS_IN_FLIGHT = 2                 # multi-frame launches in flight: slots = batch x this
 
 
@@ -129,6 +133,9 @@ def frames_per_launch(requested, cus, width, height, band_rows, n):
         return min(8, requested)
     rows = sf.lib().sf_slab_rows(height, band_rows, n, 0) if n > 1 else height
     tiles = -(-width // 8) * -(-rows // 8)
+    if BATCH_TINY > 1 and n > 1 and tiles <= TINY_GRID_FRAC * GRID_WAVES_PER_CU * cus \
+            and int(os.environ.get("GPU_MAX_HW_QUEUES", 4)) >= BATCH_TINY * GROUPS_IN_FLIGHT:
+        return BATCH_TINY
     return BATCH_SHARE if tiles <= SHARE_GRID_FRAC * GRID_WAVES_PER_CU * cus else BATCH_FULL
 
 
@@ -1053,17 +1060,19 @@ def main():
         base = r["pipeline"]["steady_frame_ms"]
         shares = {"basis_steady_ms": base, "note": (
             "ONE GPU tracing rank 0's interleaved band share of an N-way split (the member with the most rows), at the "
-            "bench's frames-in-flight policy, 60 timed steps + a 600-step loop for the steady period (kernel-timing events off); speedup = this "
+            "bench's frames-in-flight and frames-per-launch policy, 64 timed steps + a 600-step loop for the steady period (kernel-timing events off); speedup = this "
             "run's N = 1 steady period / the share's; projected_mrays = W x H / the share's steady period. A "
             "projection of the distributed G-buffer at N GPUs, not an N-GPU run")}
         for nn in (2, 4, 8):
-            sl = frames_in_flight(args.slots, cus, width, height, args.band_rows, nn, 1)
-            rs = dist_loop(ctl, torch, dev, width, height, args.K, 60, 15, sl, args.band_rows, nn, lambda i: i,
-                           settle_ms=args.settle_ms, long_steps=600, timing=SHARES_TIMING)
+            bb = frames_per_launch(args.batch, cus, width, height, args.band_rows, nn)
+            sl = frames_in_flight(args.slots, cus, width, height, args.band_rows, nn, bb)
+            rs = dist_loop(ctl, torch, dev, width, height, args.K, 64, 16, sl, args.band_rows, nn, lambda i: i,
+                           settle_ms=args.settle_ms, long_steps=600, timing=SHARES_TIMING, batch=bb)
             rs["dist"].close()
             sp = rs.get("pipeline", {}).get("steady_frame_ms") or rs["t_step"] * 1e3
-            shares[f"n{nn}"] = {"slots": sl, "ms_per_step": round(rs["t_step"] * 1e3, 5), "steady_ms": round(sp, 5),
-                                "speedup": round(base / sp, 3), "projected_mrays": round(width * height / sp / 1e3, 1)}
+            shares[f"n{nn}"] = {"slots": sl, "frames_per_launch": bb, "ms_per_step": round(rs["t_step"] * 1e3, 5),
+                                "steady_ms": round(sp, 5), "speedup": round(base / sp, 3),
+                                "projected_mrays": round(width * height / sp / 1e3, 1)}
 
     post = d2h = prog = None
     if rank == 0 and n == 1 and not args.no_extras:

@@ -78,7 +78,9 @@ def test_frames_in_flight_by_share(w, h, n, want, monkeypatch):
     assert bench.frames_in_flight(0, 256, w, h, 8, n, batch=4) == 4 * bench.GROUPS_IN_FLIGHT
     assert bench.frames_in_flight(2, 256, w, h, 8, n, batch=4) == 4
     assert bench.frames_per_launch(3, 256, w, h, 8, n) == 3
-    assert bench.frames_per_launch(0, 256, w, h, 8, n) in (bench.BATCH_FULL, bench.BATCH_SHARE)
+    # one frame per launch (the multi-frame launch is opt-in: --batch)
+    assert bench.frames_per_launch(0, 256, w, h, 8, n) == (bench.BATCH_TINY if want == 8 else 1) == 1
+    assert bench.frames_in_flight(0, 256, w, h, 8, n, batch=8) == 16
 
 
 def test_cpu_model_and_vendor_parsed():

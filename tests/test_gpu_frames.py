@@ -201,7 +201,7 @@ def test_frames_rejects_bad_batches():
             f.close()
 
 
-@pytest.mark.parametrize("slots,n,nranks,rank", [(4, 4, 1, 0), (8, 4, 1, 0), (6, 3, 3, 2)])
+@pytest.mark.parametrize("slots,n,nranks,rank", [(4, 4, 1, 0), (8, 4, 1, 0), (6, 3, 3, 2), (16, 8, 8, 0), (16, 8, 8, 7)])
 def test_dist_render_bands_frames(slots, n, nranks, rank):
     """sf_dist_render_bands_frames: the next n frames of a camera path on slots (frames + k) % slots in one launch,
     three batches in a row -- each slot's G-buffer equals RenderBands of the same frame (a dist of its own)."""
