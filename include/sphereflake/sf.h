@@ -396,7 +396,8 @@ int sf_dist_slots(const sf_dist* dist);
 sf_ctx* sf_dist_context(sf_dist* dist, int slot);     /* slot's context; on rank 0 it holds that slot's frames */
 int sf_dist_last_slot(const sf_dist* dist);           /* slot of the last frame issued (SF_ESTATE before any) */
 int sf_dist_set_view(sf_dist* dist, const float origin[3], const float top_left[3], const float top_right[3],
-                     const float bottom_left[3]);     /* the view of the next frames */
+                     const float bottom_left[3]);     /* the view of the next frames (kept by the dist and set on
+                                                         a slot's context when a frame is rendered on it) */
 int sf_dist_render(sf_dist* dist);                    /* one frame, asynchronous (this rank's share + gather;
                                                          SF_ESTATE for nranks > 1 without communicators) */
 /* One frame as a distributed G-buffer: this rank's bands into its slot's G-buffer at frame positions (reference

@@ -49,10 +49,15 @@ struct sf_dist {
         hipStream_t recv = nullptr;  // rank 0 with peers: receive + unpack stream
         hipEvent_t start = nullptr;  // rank 0: the frame's start on the context stream (G-buffer free to rewrite)
         hipEvent_t done = nullptr;   // rank 0: the frame's unpack done (on `recv`)
+        uint64_t view_gen = 0;       // the dist view (generation) this slot's context holds; 0 = none / its own
     };
     std::vector<Slot> slot;
     uint32_t slab_rows = 0, stage_rows = 0;
     uint64_t frames = 0;             // frames issued
+    // the view of the next frames (sf_dist_set_view), applied to a slot's context only when a frame is rendered on it
+    // (round 6: setting it on every slot at every frame was `slots` host-side root transforms per frame)
+    float view[12] = {};
+    uint64_t view_gen = 0;
     int last_hip = 0;
     int last_nccl = 0;
     int64_t* red = nullptr;          // device scratch of sf_dist_get_stats (4 x int64)
@@ -199,11 +204,25 @@ extern "C" int sf_dist_last_slot(const sf_dist* d)
 extern "C" int sf_dist_set_view(sf_dist* d, const float origin[3], const float top_left[3], const float top_right[3],
                                 const float bottom_left[3])
 {
-    if (!d) return SF_EINVAL;
-    for (auto& s : d->slot)
-        if (int rc = sf_set_view(s.ctx, origin, top_left, top_right, bottom_left)) return rc;
+    if (!d || !origin || !top_left || !top_right || !bottom_left) return SF_EINVAL;
+    std::memcpy(d->view, origin, 12);
+    std::memcpy(d->view + 3, top_left, 12);
+    std::memcpy(d->view + 6, top_right, 12);
+    std::memcpy(d->view + 9, bottom_left, 12);
+    ++d->view_gen;
     return SF_OK;
 }
+
+namespace {
+// The dist view into slot s's context, if it does not hold it yet (before a frame is rendered on it)
+int apply_view(sf_dist* d, sf_dist::Slot& s)
+{
+    if (d->view_gen == 0 || s.view_gen == d->view_gen) return SF_OK;   // (no dist view yet: the context's own)
+    if (int rc = sf_set_view(s.ctx, d->view, d->view + 3, d->view + 6, d->view + 9)) return rc;
+    s.view_gen = d->view_gen;
+    return SF_OK;
+}
+}   // namespace
 
 extern "C" int sf_dist_render(sf_dist* d)
 {
@@ -211,6 +230,7 @@ extern "C" int sf_dist_render(sf_dist* d)
     const uint32_t n = (uint32_t)d->nranks, W = d->W;
     auto& s = d->slot[d->frames % d->slot.size()];
     if (n > 1 && !s.comm) return SF_ESTATE;   // made without ids: bands only (sf_dist_render_bands)
+    if (int rc = apply_view(d, s)) return rc;
     hipStream_t st = (hipStream_t)sf_context_stream(s.ctx);
     // the slab format follows from the view, the same on every rank (every rank sets the same views)
     const uint32_t bytes = sf_slab_bytes(s.ctx);
@@ -293,7 +313,10 @@ extern "C" int sf_dist_comm_info(const sf_dist* d, int slot, int* count, int* ra
 extern "C" int sf_dist_slab_bytes(const sf_dist* d)
 {
     if (!d) return SF_EINVAL;
-    return (int)sf_slab_bytes(d->slot[0].ctx);
+    sf_dist* m = const_cast<sf_dist*>(d);   // (only the lazily applied view changes: the next frame's slot gets it now)
+    auto& s = m->slot[m->frames % m->slot.size()];
+    if (int rc = apply_view(m, s)) return rc;
+    return (int)sf_slab_bytes(s.ctx);
 }
 
 // This rank's bands of the next frame into its slot's G-buffer at frame positions (reference layout): the frame
@@ -302,6 +325,7 @@ extern "C" int sf_dist_render_bands(sf_dist* d)
 {
     if (!d) return SF_EINVAL;
     auto& s = d->slot[d->frames % d->slot.size()];
+    if (int rc = apply_view(d, s)) return rc;
     sf_render_params p;
     std::memset(&p, 0, sizeof p);
     p.band_rows = d->band_rows;
@@ -321,9 +345,11 @@ extern "C" int sf_dist_render_bands_frames(sf_dist* d, uint32_t n, const float (
     if (!d || !views || n == 0 || n > (uint32_t)SF_RENDER_FRAMES_MAX || n > d->slot.size()) return SF_EINVAL;
     sf_ctx* cs[SF_RENDER_FRAMES_MAX];
     for (uint32_t k = 0; k < n; ++k) {
-        cs[k] = d->slot[(d->frames + k) % d->slot.size()].ctx;
+        auto& s = d->slot[(d->frames + k) % d->slot.size()];
+        cs[k] = s.ctx;
         const float* v = views[k];
         if (int rc = sf_set_view(cs[k], v, v + 3, v + 6, v + 9)) return rc;
+        s.view_gen = 0;   // (its own view now, not the dist view)
     }
     sf_render_params p;
     std::memset(&p, 0, sizeof p);

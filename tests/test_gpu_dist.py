@@ -168,6 +168,39 @@ def test_dist_render_bands_one_rank_is_the_frame():
             assert frame_digest(pos, nrm) == fx["frame_digest"], slot
 
 
+def test_dist_view_applied_per_slot_at_render():
+    """sf_dist_set_view keeps the view in the dist and sets it on a slot's context only when a frame is rendered
+    there (not on every slot per frame): a slot that last rendered a frame of its own (sf_dist_render_bands_frames)
+    gets the dist view back at its next RenderBands, and slab_bytes of the next frame sees the dist view."""
+    fx = load_frame("c2")
+    W, H, K = fx["W"], fx["H"], float.fromhex(fx["K"])
+    a, b, c = path_views(W, H, K, 3)
+    with sf.SphereflakeDist(0, W, H, slots=2) as d, sf.Sphereflake(W, H) as ref:
+        want = {}
+        for name, v in (("a", a), ("b", b), ("c", c)):
+            ref.SetView(*v)
+            ref.Render()
+            rp, rn, _, _ = ref.download()
+            want[name] = frame_digest(rp, rn)
+        d.SetView(*a)
+        assert d.slab_bytes() == 4
+        d.RenderBands()                       # (frame 0) slot 0: a
+        d.RenderBandsFrames([b, c])           # (frames 1, 2) slot 1: b, slot 0: c
+        d.Synchronize()
+        assert frame_digest(*d.download_slot(1)) == want["b"]
+        assert frame_digest(*d.download_slot(0)) == want["c"]
+        d.RenderBands()                       # (frame 3) slot 1: the dist view a again, not b
+        d.RenderBands()                       # (frame 4) slot 0: a, not c
+        d.Synchronize()
+        for slot in (0, 1):
+            assert frame_digest(*d.download_slot(slot)) == want["a"], slot
+        d.SetView(*b)
+        d.RenderBands()                       # (frame 5) slot 1: b
+        d.Synchronize()
+        assert frame_digest(*d.download_slot(1)) == want["b"]
+        assert frame_digest(*d.download_slot(0)) == want["a"]   # (untouched)
+
+
 @pytest.mark.parametrize("n", [2, 3])
 def test_dist_bands_without_communicators(n):
     """nranks > 1 made without ids (no RCCL: the multi-GPU bench's `value` leg): rank k's RenderBands writes the
