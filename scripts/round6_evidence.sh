@@ -40,3 +40,6 @@ for W in "3840 2160 0.22" "1920 1080 0.25"; do
   timeout -k 10 200 python3 -u scripts/unpack_probe.py $W 8 50 2>&1 | grep unpack | tee -a $OUT/unpack.txt
 done
 timeout -k 10 300 python3 -u scripts/share_probe.py 1920 1080 0.25 2>&1 | grep -v amdgpu.ids | tee -a $OUT/share.txt
+# the driver's N > 1 flow rehearsed on this box's one GPU (two self-spawned ranks; every leg but the RCCL gather)
+timeout -k 10 400 python -u bench.py --gpus 2 --rehearse --steps 20 --warmup 5 --no-cpu-baseline > $OUT/rehearse2.json 2> $OUT/rehearse2.err
+python3 -c "import json; d=json.loads(open('$OUT/rehearse2.json').read().strip().splitlines()[-1]); print('rehearse2', d['value'], d['ms_per_step'], d['config'].get('parallelism'), d['check']['bit_exact'])" | tee $OUT/rehearse2.txt
