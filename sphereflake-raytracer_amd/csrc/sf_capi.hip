@@ -112,6 +112,35 @@ struct DevGuard {
     }
 };
 
+// A context's stream gets a hardware queue of its own (round 6): it is made with a CU mask of every CU, which the
+// HIP runtime serves with a queue of that stream's own, not one of the GPU_MAX_HW_QUEUES queues it shares out and
+// hands on from destroyed streams. Measured (profiles/r6/multi/queue_reuse/): with shared queues, a dist
+// of 8 slots made after a dist of 3 or 4 had run its loops and been destroyed (the bench's legs; any process that
+// renders a whole frame before a 1/8 band share) traced the share at 0.0132-0.0141 ms per frame instead of
+// 0.0110-0.0113 -- every time, at the same clock, with the same buffers; not after one that made and rendered plain
+// contexts, nor after a dist of 8 or 16 slots. Queues of their own: 0.0110-0.0112 in every such sequence.
+// (The mask covers every CU: no CU is withheld. Such a stream is not a non-blocking one: work on the legacy default
+// stream is ordered with it; the library enqueues nothing there.) SF_STREAM_CUMASK=0: a plain non-blocking stream.
+bool stream_cumask_on()
+{
+    static const bool on = [] {
+        const char* ev = std::getenv("SF_STREAM_CUMASK");
+        return !ev || std::atoi(ev) != 0;
+    }();
+    return on;
+}
+// (the caller has made `device` current)
+hipError_t stream_acquire(int device, hipStream_t* out)
+{
+    if (!stream_cumask_on()) return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
+    int cus = 0;
+    hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (e != hipSuccess) return e;
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xffffffffu);
+    if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+    return hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data());
+}
+
 }  // namespace
 
 struct sf_ctx {
@@ -571,7 +600,7 @@ int sf_create(int device, uint32_t width, uint32_t height, sf_ctx** out)
         return e == hipErrorOutOfMemory ? SF_ENOMEM : SF_EHIP;
     };
     hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+    if ((e = stream_acquire(device, &c->stream)) != hipSuccess) return fail(e);
     if ((e = hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->pos, npx * 16)) != hipSuccess) return fail(e);
     if ((e = hipMalloc(&c->nrm, npx * 16)) != hipSuccess) return fail(e);
