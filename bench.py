@@ -44,10 +44,12 @@ import sys
 import time
 
 # Hardware queues per process (the HIP runtime's GPU_MAX_HW_QUEUES, default 4). Every frame in flight has a stream of
-# its own (plus the order, prefetch and receive streams); with 4 queues, streams share them and one slot's kernel waits
-# in order behind another's. Round 6: a 1080p member's share over 8 GPUs at 8 frames in flight 0.0146 ms with 4
-# queues, 0.0121 with 16; the whole frame at 3 in flight unchanged (profiles/r6/multi/queues.txt). Raised to 16 before
-# the HIP runtime starts (its first call); a larger value already in the environment is kept.
+# its own; with plain streams on 4 queues, streams share them and one slot's kernel waits in order behind another's
+# (round 6: a 1080p member's share over 8 GPUs at 8 frames in flight 0.0146 ms with 4 queues, 0.0121 with 16,
+# profiles/r6/multi/queues.txt). Since the library gives each context's stream a queue of its own (sf_capi.hip,
+# SF_STREAM_CUMASK), the slots no longer depend on this (0.0110-0.0112 ms at 4 or 16, profiles/r6/multi/queue_reuse/);
+# it still serves the other streams of the process. Raised to 16 before the HIP runtime starts (its first call); a
+# larger value already in the environment is kept.
 HW_QUEUES = int(os.environ.get("SF_HW_QUEUES", "16") or 0)   # (SF_HW_QUEUES=0: leave the runtime's setting, A/B)
 if HW_QUEUES > 0 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < HW_QUEUES:
     os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
@@ -150,8 +152,9 @@ def frames_in_flight(requested, cus, width, height, band_rows, n, batch=1):
         return batch * GROUPS_IN_FLIGHT
     rows = sf.lib().sf_slab_rows(height, band_rows, n, 0) if n > 1 else height
     tiles = -(-width // 8) * -(-rows // 8)
+    own_queues = os.environ.get("SF_STREAM_CUMASK", "1") != "0"   # (the library's default: a queue per slot stream)
     if n > 1 and tiles <= TINY_GRID_FRAC * GRID_WAVES_PER_CU * cus \
-            and int(os.environ.get("GPU_MAX_HW_QUEUES", 4)) >= SLOTS_TINY:
+            and (own_queues or int(os.environ.get("GPU_MAX_HW_QUEUES", 4)) >= SLOTS_TINY):
         return SLOTS_TINY   # (band shares only: a whole 640x360 frame measured 0.0186-0.0189 ms at 8 vs 0.0172 at 4)
     return SLOTS_SHARE if tiles <= SHARE_GRID_FRAC * GRID_WAVES_PER_CU * cus else SLOTS_FULL
 

@@ -5,7 +5,7 @@ loops' ms per frame, the steady period the bench derives, and the host's enqueue
 Usage: member_share_probe.py [N=8] [long_steps=600] [reps=2]
 PRE=main,c4,n2,n4 (comma list) runs the bench's legs before it first, as bench.py does (the 1080p N = 1 line with its
 fixed-view, latency and first-render loops; the 4K loop; the N = 2 / 4 shares), to find what slows the shares there.
-EXTRA_STREAMS=k first makes k torch streams, each with one tiny kernel run on it (a hardware queue each), kept alive."""
+SLOTS=k: k frames in flight instead of the bench's policy. EXTRA_STREAMS=k first makes k torch streams, each with one tiny kernel run on it (a hardware queue each), kept alive."""
 import os
 import sys
 
@@ -24,7 +24,7 @@ torch.cuda.set_device(0)
 dev = torch.device("cuda", 0)
 ctl = bench.Control(1, 0)
 cus = torch.cuda.get_device_properties(0).multi_processor_count
-sl = bench.frames_in_flight(0, cus, W, H, 8, N)
+sl = int(os.environ.get("SLOTS", "0") or 0) or bench.frames_in_flight(0, cus, W, H, 8, N)
 extra = [torch.cuda.Stream(device=dev) for _ in range(int(os.environ.get("EXTRA_STREAMS", "0") or 0))]
 for st in extra:
     with torch.cuda.stream(st):

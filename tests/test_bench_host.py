@@ -64,14 +64,18 @@ def test_issue_fractions_on_the_frame_period():
                                         (640, 360, 1, 4), (1280, 720, 1, 3), (3840, 2160, 8, 3), (3840, 2160, 1, 3)])
 def test_frames_in_flight_by_share(w, h, n, want, monkeypatch):
     """8 frames in flight where rank 0's band share of 8x8 tiles is at most 3/4 of a persistent grid (256 CUs x 32
-    waves) and the process has the 16 hardware queues bench.py gives it, 4 up to 1.5 grids (and for small whole
+    waves) and the slot streams have hardware queues of their own (the library's default; else the process needs the
+    16 shared queues bench.py gives it), 4 up to 1.5 grids (and for small whole
     frames), else 3; an explicit --slots wins
     (clamped to batch..16). With multi-frame launches of B frames (round 6), B x GROUPS_IN_FLIGHT slots, and never
     fewer slots than one launch's frames."""
     assert int(bench.os.environ["GPU_MAX_HW_QUEUES"]) >= bench.HW_QUEUES   # (raised at import, before any HIP call)
     assert bench.frames_in_flight(0, 256, w, h, 8, n) == want
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")   # (a process left at HIP's 4 queues keeps 4 for small shares)
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")   # (the slot streams have queues of their own: 4 shared ones do)
+    assert bench.frames_in_flight(0, 256, w, h, 8, n) == want
+    monkeypatch.setenv("SF_STREAM_CUMASK", "0")    # (plain streams on HIP's 4 shared queues: 4 for small shares)
     assert bench.frames_in_flight(0, 256, w, h, 8, n) == (4 if want == 8 else want)
+    monkeypatch.delenv("SF_STREAM_CUMASK")
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", str(bench.HW_QUEUES))
     assert bench.frames_in_flight(5, 256, w, h, 8, n) == 5
     assert bench.frames_in_flight(99, 256, w, h, 8, n) == 16
