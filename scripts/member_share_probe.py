@@ -45,6 +45,10 @@ for pre in [p for p in os.environ.get("PRE", "").split(",") if p]:
         del bufs
         torch.cuda.empty_cache()
         continue
+    elif pre.startswith("churn"):   # churn<k>: k plain 1080p contexts made and destroyed one after the other
+        for _ in range(int(pre[5:])):
+            bench.sf.Sphereflake(W, H, device=0).close()
+        continue
     elif pre.startswith("ctx"):   # ctx<k>[r]: k plain 1080p contexts made (and with r: each renders once), closed
         k = int(pre[3:].rstrip("r"))
         cs = [bench.sf.Sphereflake(W, H, device=0) for _ in range(k)]
