@@ -138,7 +138,9 @@ hipError_t stream_acquire(int device, hipStream_t* out)
     if (e != hipSuccess) return e;
     std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xffffffffu);
     if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
-    return hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data());
+    if (hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data()) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();   // (a runtime without CU-masked queues: a plain stream, as with SF_STREAM_CUMASK=0)
+    return hipStreamCreateWithFlags(out, hipStreamNonBlocking);
 }
 
 }  // namespace
